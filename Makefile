@@ -1,0 +1,23 @@
+# Build libocrk.so: every HIP kernel + the C-ABI, compiled for gfx950 only.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH  ?= gfx950
+CSRC  := cnn_lstm_ctc_ocr_amd/csrc
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+SRC   := $(wildcard $(CSRC)/*.hip)
+OBJ   := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRC))
+HDR   := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
+LIB   := cnn_lstm_ctc_ocr_amd/libocrk.so
+
+all: $(LIB)
+
+$(LIB): $(OBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
+
+build/%.o: $(CSRC)/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

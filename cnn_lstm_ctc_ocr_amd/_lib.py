@@ -1,0 +1,91 @@
+"""ctypes binding of libocrk.so (the C ABI declared in include/ocrk.h).
+
+The library is built in-tree by ``make`` (or ``__graft_entry__.build()``).
+There is no fallback: if the shared object is missing or stale this module
+raises, so a GPU run can never silently route through a CPU path.
+
+``torch`` is imported first on purpose: libocrk.so links libamdhip64.so.7 and
+must bind to the same HIP runtime instance torch already loaded (identical
+SONAME), so device pointers and streams are shared between the two.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring: runtime must be torch's)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libocrk.so")
+
+OCRK_OK = 0
+OCRK_ERR_INVALID_ARG = 1
+OCRK_ERR_HIP = 2
+OCRK_ERR_INFEASIBLE = 3
+
+F32 = 0
+BF16 = 1
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> argtypes (restype is int unless listed in _RESTYPE).
+SIGNATURES = {
+    "ocrk_version": [],
+    "ocrk_last_error": [],
+    "ocrk_preprocess": [_p, _i64, _p, _i32, _p],
+}
+_RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
+
+
+class OcrkError(RuntimeError):
+    """A libocrk entry point returned a non-zero status."""
+
+    def __init__(self, status, message):
+        super().__init__(message)
+        self.status = status
+
+
+class InvalidArgumentError(OcrkError):
+    """Mirrors tf.errors.InvalidArgumentError (e.g. infeasible CTC labels)."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make` in the repo root "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        _lib = handle
+    return _lib
+
+
+def call(name, *args):
+    """Call ocrk_<name>; raise on a non-zero status."""
+    status = getattr(lib(), name)(*args)
+    if status != OCRK_OK:
+        msg = lib().ocrk_last_error().decode(errors="replace")
+        if status in (OCRK_ERR_INFEASIBLE, OCRK_ERR_INVALID_ARG):
+            raise InvalidArgumentError(status, msg)
+        raise OcrkError(status, msg)
+    return status
+
+
+def ptr(t):
+    """Device (or host) address of a tensor, or None for None."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    """The HIP stream handle torch is currently launching on."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
