@@ -35,8 +35,45 @@ SIGNATURES = {
     "ocrk_version": [],
     "ocrk_last_error": [],
     "ocrk_preprocess": [_p, _i64, _p, _i32, _p],
+    "ocrk_ctc_workspace_size": [_i32, _i32, _i32],
+    "ocrk_ctc_loss": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _f32, _p, _p, _p, _p, _sz, _p],
+    "ocrk_ctc_greedy_decode": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
+    "ocrk_conv1_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _p],
+    "ocrk_conv1_wgrad_workspace_size": [_i32, _i32, _i32, _i32],
+    "ocrk_conv1_bwd_weight": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_conv_stats_tiles": [_i64],
+    "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],
+    "ocrk_conv3x3_bwd_data": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _i32, _p],
+    "ocrk_conv3x3_wgrad_workspace_size": [_i32, _i32, _i32, _i32, _i32],
+    "ocrk_conv3x3_bwd_weight": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_bn_finalize": [_p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p],
+    "ocrk_bn_infer_params": [_p, _p, _i32, _f32, _p, _p, _p],
+    "ocrk_bn_relu_pool_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                              _p, _i32, _i32, _p],
+    "ocrk_bn_bwd_workspace_size": [_i32, _i32, _i32, _i32],
+    "ocrk_bn_relu_pool_bwd": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                              _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_gemm_workspace_size": [_i32, _i32, _i32, _i32],
+    "ocrk_gemm": [_i32, _i32, _i32, _i32, _i32, _f32, _p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64,
+                  _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p],
+    "ocrk_adam": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p],
+    "ocrk_cast": [_p, _i32, _p, _i32, _i64, _p],
+    "ocrk_permute3": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p],
+    "ocrk_strided_copy": [_p, _i64, _i64, _i64, _i64, _p, _i32, _i64, _i64, _p],
+    "ocrk_colsum_workspace_size": [_i64, _i32],
+    "ocrk_colsum": [_p, _i64, _i32, _i32, _p, _i32, _p, _sz, _p],
+    "ocrk_relu_mask": [_p, _p, _i64, _f32, _p, _i32, _p],
+    "ocrk_mul_scalar": [_p, _i64, _p, _p],
+    "ocrk_mean": [_p, _i32, _p, _p],
+    "ocrk_seq_len": [_p, _i32, _p, _p],
 }
 _RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
+_RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspace_size")})
+_RESTYPE["ocrk_conv_stats_tiles"] = ctypes.c_size_t
 
 
 class OcrkError(RuntimeError):

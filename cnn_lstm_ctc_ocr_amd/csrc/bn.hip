@@ -1,0 +1,364 @@
+// a3+a4: BatchNorm -> ReLU -> max-pool of the even conv layers
+// (norm_layer src/weinman/model.py:118-123, conv_layer :105-107, pool_layer
+// :111-116, pool8 :145-146).
+//
+// Forward (train): the conv epilogue leaves per-128-row-tile (sum, M2)
+// partials; bn_finalize merges them (Chan, in double) into batch mean/invstd
+// and the moving averages ([TF1] momentum 0.99, moving variance from the
+// unbiased batch variance). bn_relu_pool applies BN + ReLU + pool in one pass
+// (thread = one pooled pixel x 8 channels) and can write the last pool
+// (pool8) straight into the time-major [T, B, C] feature layout the RNN reads
+// (model.py:147 squeeze + :212 transpose folded away).
+// Backward: thread = one pre-pool pixel x 8 channels; it re-derives which
+// pooling windows route their gradient to it ([TF1] MaxPoolGrad: first max of
+// the window), applies the ReLU mask, and a deterministic two-pass
+// (partials -> ordered sum -> apply) BN backward.
+#include "common.h"
+
+struct F8 { float v[8]; };
+
+template <typename T> __device__ __forceinline__ F8 load8(const T* p);
+template <> __device__ __forceinline__ F8 load8<float>(const float* p) {
+    F8 r;
+    float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+template <> __device__ __forceinline__ F8 load8<bf16>(const bf16* p) {
+    union { uint4 q; bf16 e[8]; } u;
+    u.q = *reinterpret_cast<const uint4*>(p);
+    F8 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (float)u.e[i];
+    return r;
+}
+template <typename T> __device__ __forceinline__ void store8(T* p, const F8& x);
+template <> __device__ __forceinline__ void store8<float>(float* p, const F8& x) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const F8& x) {
+    union { uint4 q; bf16 e[8]; } u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u.e[i] = (bf16)x.v[i];
+    *reinterpret_cast<uint4*>(p) = u.q;
+}
+
+// --------------------------------------------------------------- finalize
+// One block per channel: Chan-merge the per-tile (sum, M2) partials.
+__global__ void __launch_bounds__(256)
+bn_finalize_kernel(const float* __restrict__ stats, int tiles, int64_t M, int tile_rows, int C,
+                   float eps, float momentum, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                   float* __restrict__ moving_mean, float* __restrict__ moving_var) {
+    __shared__ double sn[256], smean[256], sm2[256];
+    const int c = blockIdx.x;
+    double n = 0, mean = 0, m2 = 0;
+    for (int t = threadIdx.x; t < tiles; t += 256) {
+        double nb = (double)min<int64_t>(tile_rows, M - (int64_t)t * tile_rows);
+        double sb = stats[(int64_t)t * 2 * C + c];
+        double m2b = stats[(int64_t)t * 2 * C + C + c];
+        double mb = sb / nb;
+        double nt = n + nb, d = mb - mean;
+        mean += d * nb / nt;
+        m2 += m2b + d * d * n * nb / nt;
+        n = nt;
+    }
+    sn[threadIdx.x] = n; smean[threadIdx.x] = mean; sm2[threadIdx.x] = m2;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
+            double nt = na + nb;
+            if (nb > 0) {
+                double d = smean[threadIdx.x + s] - smean[threadIdx.x];
+                smean[threadIdx.x] += d * nb / nt;
+                sm2[threadIdx.x] += sm2[threadIdx.x + s] + d * d * na * nb / nt;
+                sn[threadIdx.x] = nt;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        double nt = sn[0], mu = smean[0], var = sm2[0] / nt;
+        mean_out[c] = (float)mu;
+        invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (moving_mean) {
+            float dec = 1.f - momentum;
+            double var_u = nt > 1 ? sm2[0] / (nt - 1) : var;
+            moving_mean[c] = moving_mean[c] - (moving_mean[c] - (float)mu) * dec;
+            moving_var[c] = moving_var[c] - (moving_var[c] - (float)var_u) * dec;
+        }
+    }
+}
+
+__global__ void bn_infer_params_kernel(const float* mm, const float* mv, int C, float eps,
+                                       float* mean, float* invstd) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) {
+        mean[c] = mm[c];
+        invstd[c] = (float)(1.0 / sqrt((double)mv[c] + (double)eps));
+    }
+}
+
+// ---------------------------------------------------- BN + ReLU + pool fwd
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_relu_pool_fwd_kernel(const T* __restrict__ z, int B, int H, int W, int C,
+                        const float* __restrict__ mean, const float* __restrict__ invstd,
+                        const float* __restrict__ gamma, const float* __restrict__ beta, int kh, int kw,
+                        int sh, int sw, T* __restrict__ out, int time_major) {
+    const int Ho = (H - kh) / sh + 1, Wo = (W - kw) / sw + 1, G = C / 8;
+    const int64_t items = (int64_t)B * Ho * Wo * G;
+    for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < items; it += (int64_t)gridDim.x * 256) {
+        int g = (int)(it % G);
+        int64_t op = it / G;
+        int wo = (int)(op % Wo);
+        int64_t t = op / Wo;
+        int ho = (int)(t % Ho), b = (int)(t / Ho);
+        int c0 = g * 8;
+        float sc[8], sf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sc[i] = gamma[c0 + i] * invstd[c0 + i];
+            sf[i] = beta[c0 + i] - mean[c0 + i] * sc[i];
+        }
+        F8 best;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) best.v[i] = -INFINITY;
+        for (int dh = 0; dh < kh; ++dh)
+            for (int dw = 0; dw < kw; ++dw) {
+                F8 v = load8(z + (((int64_t)b * H + ho * sh + dh) * W + wo * sw + dw) * C + c0);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) best.v[i] = fmaxf(best.v[i], fmaxf(fmaf(v.v[i], sc[i], sf[i]), 0.f));
+            }
+        int64_t o = time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
+                               : (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+        store8(out + o, best);
+    }
+}
+
+// ----------------------------------------------------------- backward
+// Gradient arriving at pre-pool pixel (h, w) for 8 channels: sum of dp over
+// the windows whose first maximum is (h, w), masked by ReLU.
+template <typename T>
+__device__ __forceinline__ void routed_grad(const T* __restrict__ z, const T* __restrict__ dp, int B, int H,
+                                            int W, int C, int b, int h, int w, int c0, int kh, int kw,
+                                            int sh, int sw, int dp_time_major, const float* sc, const float* sf,
+                                            float* da, float* zc) {
+    const int Ho = (H - kh) / sh + 1, Wo = (W - kw) / sw + 1;
+    F8 me = load8(z + (((int64_t)b * H + h) * W + w) * C + c0);
+    float a_me[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        zc[i] = me.v[i];
+        a_me[i] = fmaf(me.v[i], sc[i], sf[i]);
+        da[i] = 0.f;
+    }
+    int ho_lo = max(0, (h - kh + sh) / sh), ho_hi = min(Ho - 1, h / sh);
+    int wo_lo = max(0, (w - kw + sw) / sw), wo_hi = min(Wo - 1, w / sw);
+    if (h - kh + 1 < 0) ho_lo = 0;
+    if (w - kw + 1 < 0) wo_lo = 0;
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+        for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+            if (ho * sh > h || ho * sh + kh <= h || wo * sw > w || wo * sw + kw <= w) continue;
+            // first max over the window (row-major scan) of relu(bn(z))
+            float best[8];
+            int arg[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; arg[i] = -1; }
+            for (int dh = 0; dh < kh; ++dh)
+                for (int dw = 0; dw < kw; ++dw) {
+                    F8 v = load8(z + (((int64_t)b * H + ho * sh + dh) * W + wo * sw + dw) * C + c0);
+                    int pos = dh * kw + dw;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        float y = fmaxf(fmaf(v.v[i], sc[i], sf[i]), 0.f);
+                        if (y > best[i]) { best[i] = y; arg[i] = pos; }
+                    }
+                }
+            int mypos = (h - ho * sh) * kw + (w - wo * sw);
+            int64_t o = dp_time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
+                                      : (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+            F8 g = load8(dp + o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (arg[i] == mypos) da[i] += g.v[i];
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (!(a_me[i] > 0.f)) da[i] = 0.f;
+}
+
+// pass 1: per-block partial sums of da and da*xhat per channel
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
+                     const float* __restrict__ mean, const float* __restrict__ invstd,
+                     const float* __restrict__ gamma, const float* __restrict__ beta, int kh, int kw,
+                     int sh, int sw, int dp_time_major, int64_t items_per_block, float* __restrict__ slab) {
+    __shared__ float red[256][17];
+    const int G = C / 8;
+    const int64_t items = (int64_t)B * H * W * G;
+    const int g = threadIdx.x % G;       // fixed: items_per_block % 256 == 0 and 256 % G == 0
+    const int c0 = g * 8;
+    float sc[8], sf[8], mu[8], is[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        is[i] = invstd[c0 + i];
+        mu[i] = mean[c0 + i];
+        sc[i] = gamma[c0 + i] * is[i];
+        sf[i] = beta[c0 + i] - mu[i] * sc[i];
+    }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+    const int64_t i0 = (int64_t)blockIdx.x * items_per_block;
+    const int64_t i1 = min(items, i0 + items_per_block);
+    for (int64_t it = i0 + threadIdx.x; it < i1; it += 256) {
+        int64_t px = it / G;
+        int w = (int)(px % W);
+        int64_t t = px / W;
+        int h = (int)(t % H), b = (int)(t / H);
+        float da[8], zc[8];
+        routed_grad(z, dp, B, H, W, C, b, h, w, c0, kh, kw, sh, sw, dp_time_major, sc, sf, da, zc);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s1[i] += da[i];
+            s2[i] += da[i] * ((zc[i] - mu[i]) * is[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 2 * C; o += 256) {
+        int which = o / C, c = o % C, gg = c / 8, ci = c % 8;
+        float s = 0.f;
+        for (int q = gg; q < 256; q += G) s += red[q][which * 8 + ci];
+        slab[(int64_t)blockIdx.x * 2 * C + o] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_sum_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ dsum,
+                  float* __restrict__ dbeta, float* __restrict__ dgamma, int accumulate) {
+    int o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= 2 * C) return;
+    double s = 0.0;
+    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * 2 * C + o];
+    dsum[o] = (float)s;
+    float* dst = o < C ? dbeta + o : dgamma + (o - C);
+    *dst = accumulate ? *dst + (float)s : (float)s;
+}
+
+// pass 2: dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n)
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
+                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                    const float* __restrict__ gamma, const float* __restrict__ beta, int kh, int kw,
+                    int sh, int sw, int dp_time_major, const float* __restrict__ dsum, T* __restrict__ dz) {
+    const int G = C / 8;
+    const int64_t items = (int64_t)B * H * W * G;
+    const float inv_n = 1.f / (float)((int64_t)B * H * W);
+    for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < items; it += (int64_t)gridDim.x * 256) {
+        int g = (int)(it % G);
+        int c0 = g * 8;
+        int64_t px = it / G;
+        int w = (int)(px % W);
+        int64_t t = px / W;
+        int h = (int)(t % H), b = (int)(t / H);
+        float sc[8], sf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sc[i] = gamma[c0 + i] * invstd[c0 + i];
+            sf[i] = beta[c0 + i] - mean[c0 + i] * sc[i];
+        }
+        float da[8], zc[8];
+        routed_grad(z, dp, B, H, W, C, b, h, w, c0, kh, kw, sh, sw, dp_time_major, sc, sf, da, zc);
+        F8 out;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int c = c0 + i;
+            float xhat = (zc[i] - mean[c]) * invstd[c];
+            out.v[i] = sc[i] * (da[i] - dsum[c] * inv_n - xhat * dsum[C + c] * inv_n);
+        }
+        store8(dz + px * C + c0, out);
+    }
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps,
+                                float momentum, float* mean, float* invstd, float* moving_mean,
+                                float* moving_var, void* stream) {
+    OCRK_REQUIRE(tiles >= 1 && C >= 1 && M >= 1, "ocrk_bn_finalize: bad sizes");
+    bn_finalize_kernel<<<C, 256, 0, ocrk::as_stream(stream)>>>(stats, tiles, M, 128, C, eps, momentum, mean,
+                                                               invstd, moving_mean, moving_var);
+    return ocrk::launch_status("ocrk_bn_finalize");
+}
+
+extern "C" int ocrk_bn_infer_params(const float* moving_mean, const float* moving_var, int C, float eps,
+                                    float* mean, float* invstd, void* stream) {
+    bn_infer_params_kernel<<<(C + 255) / 256, 256, 0, ocrk::as_stream(stream)>>>(moving_mean, moving_var, C,
+                                                                               eps, mean, invstd);
+    return ocrk::launch_status("ocrk_bn_infer_params");
+}
+
+static unsigned grid_for(int64_t items) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ocrk::cdiv(items, 256), 8192)); }
+
+extern "C" int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, const float* mean,
+                                     const float* invstd, const float* gamma, const float* beta, int kh,
+                                     int kw, int sh, int sw, void* out, int time_major, int dtype,
+                                     void* stream) {
+    OCRK_REQUIRE(C % 8 == 0 && H >= kh && W >= kw, "ocrk_bn_relu_pool_fwd: bad shape");
+    OCRK_REQUIRE(!time_major || (H - kh) / sh + 1 == 1, "ocrk_bn_relu_pool_fwd: time-major output needs Ho == 1");
+    int64_t items = (int64_t)B * ((H - kh) / sh + 1) * ((W - kw) / sw + 1) * (C / 8);
+    if (items == 0) return OCRK_OK;
+    hipStream_t s = ocrk::as_stream(stream);
+    if (dtype == OCRK_BF16)
+        bn_relu_pool_fwd_kernel<bf16><<<grid_for(items), 256, 0, s>>>((const bf16*)z, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, (bf16*)out, time_major);
+    else
+        bn_relu_pool_fwd_kernel<float><<<grid_for(items), 256, 0, s>>>((const float*)z, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, (float*)out, time_major);
+    return ocrk::launch_status("ocrk_bn_relu_pool_fwd");
+}
+
+static int64_t bn_bwd_blocks(int64_t items) { return std::max<int64_t>(1, std::min<int64_t>(2048, ocrk::cdiv(items, 256 * 8))); }
+static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::cdiv(items, nb), 256) * 256; }
+
+extern "C" size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C) {
+    int64_t items = (int64_t)B * H * W * (C / 8);
+    int64_t nb = bn_bwd_blocks(items);
+    nb = ocrk::cdiv(items, bn_bwd_ipb(items, nb));
+    return (size_t)(nb * 2 * C + 2 * C) * sizeof(float);
+}
+
+extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                     void* dz, float* dgamma, float* dbeta, int accumulate, void* ws,
+                                     size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "ocrk_bn_relu_pool_bwd: C=%d unsupported", C);
+    OCRK_REQUIRE(ws_bytes >= ocrk_bn_bwd_workspace_size(B, H, W, C), "ocrk_bn_relu_pool_bwd: workspace too small");
+    int64_t items = (int64_t)B * H * W * (C / 8);
+    if (items == 0) return OCRK_OK;
+    int64_t nb = bn_bwd_blocks(items);
+    int64_t ipb = bn_bwd_ipb(items, nb);
+    nb = ocrk::cdiv(items, ipb);
+    float* slab = (float*)ws;
+    float* dsum = slab + nb * 2 * C;
+    hipStream_t s = ocrk::as_stream(stream);
+    if (dtype == OCRK_BF16)
+        bn_bwd_reduce_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, ipb, slab);
+    else
+        bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, ipb, slab);
+    int st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
+    if (st) return st;
+    bn_bwd_sum_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(slab, (int)nb, C, dsum, dbeta, dgamma, accumulate);
+    st = ocrk::launch_status("ocrk_bn_relu_pool_bwd sum");
+    if (st) return st;
+    if (dtype == OCRK_BF16)
+        bn_bwd_apply_kernel<bf16><<<grid_for(items), 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dsum, (bf16*)dz);
+    else
+        bn_bwd_apply_kernel<float><<<grid_for(items), 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dsum, (float*)dz);
+    return ocrk::launch_status("ocrk_bn_relu_pool_bwd apply");
+}

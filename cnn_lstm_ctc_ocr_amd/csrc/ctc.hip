@@ -1,0 +1,321 @@
+// a9/a10: CTC loss + gradient w.r.t. logits, and the greedy decoder.
+//
+// ctc_loss_layer (src/weinman/model.py:224-229) calls tf.nn.ctc_loss with
+// time_major logits [T, B, C], preprocess_collapse_repeated=False,
+// ctc_merge_repeated=True; blank = C - 1. validate._get_output
+// (src/weinman/validate.py:81-92) calls tf.nn.ctc_greedy_decoder(merge_repeated=True).
+//
+// Layout / work split: one 256-thread workgroup per sequence b. The extended
+// label l' = [blank, l1, blank, l2, ..., blank] (S = 2L+1 states) lives in
+// registers of a single wave: lane j holds states j, j+64, ... (R registers).
+// Wave 0 runs the alpha recursion while wave 1 runs the beta recursion at the
+// same time (wave-synchronous, shuffles only, no barriers inside the time
+// loop); both stream their [T, S] log-lattices to a global workspace, then all
+// four waves form the gradient, one time step per wave.
+#include "common.h"
+
+#define CTC_THREADS 256
+#define CTC_MAX_R 8                 // S <= 512  (labels up to 255 symbols)
+#define CTC_MAX_T 4096
+#define CTC_MAX_C 256
+
+__device__ __forceinline__ float lse2(float a, float b) {
+    float m = fmaxf(a, b);
+    if (m == -INFINITY) return -INFINITY;
+    return m + logf(expf(a - m) + expf(b - m));
+}
+__device__ __forceinline__ float lse3(float a, float b, float c) {
+    float m = fmaxf(fmaxf(a, b), c);
+    if (m == -INFINITY) return -INFINITY;
+    return m + logf(expf(a - m) + expf(b - m) + expf(c - m));
+}
+
+// value of register r at lane-1 (state s-1), across the register boundary.
+__device__ __forceinline__ float shift_up1(const float* a, int r, int lane) {
+    float v = __shfl_up(a[r], 1, 64);
+    float w = __shfl(a[r > 0 ? r - 1 : 0], 63, 64);
+    return lane == 0 ? (r > 0 ? w : -INFINITY) : v;
+}
+__device__ __forceinline__ float shift_up2(const float* a, int r, int lane) {
+    float v = __shfl_up(a[r], 2, 64);
+    float w = __shfl(a[r > 0 ? r - 1 : 0], 62 + lane, 64);
+    return lane < 2 ? (r > 0 ? w : -INFINITY) : v;
+}
+__device__ __forceinline__ float shift_dn1(const float* a, int r, int R, int lane) {
+    float v = __shfl_down(a[r], 1, 64);
+    float w = __shfl(a[r + 1 < R ? r + 1 : r], 0, 64);
+    return lane == 63 ? (r + 1 < R ? w : -INFINITY) : v;
+}
+__device__ __forceinline__ float shift_dn2(const float* a, int r, int R, int lane) {
+    float v = __shfl_down(a[r], 2, 64);
+    float w = __shfl(a[r + 1 < R ? r + 1 : r], lane - 62, 64);
+    return lane >= 62 ? (r + 1 < R ? w : -INFINITY) : v;
+}
+
+template <int R>
+__device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, const int* lab,
+                          int S, int L, int B, int C, int b, int blank, float* __restrict__ alpha_ws) {
+    const int lane = threadIdx.x & 63;
+    int cls[R];
+    bool skip[R];
+    float a[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int s = lane + 64 * r;
+        cls[r] = (s < S) ? ((s & 1) ? lab[s >> 1] : blank) : blank;
+        skip[r] = (s < S) && (s & 1) && s >= 3 && lab[s >> 1] != lab[(s >> 1) - 1];
+        float lp = logits[(size_t)b * C + cls[r]] - lse[0];
+        a[r] = (s < 2 && s < S) ? lp : -INFINITY;
+        if (s < S) alpha_ws[s] = a[r];
+    }
+    for (int t = 1; t < L; ++t) {
+        const float* row = logits + ((size_t)t * B + b) * C;
+        float nxt[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            // shuffles run in every lane (convergent); select afterwards
+            float a1 = shift_up1(a, r, lane);
+            float a2 = shift_up2(a, r, lane);
+            a2 = skip[r] ? a2 : -INFINITY;
+            nxt[r] = lse3(a[r], a1, a2) + (row[cls[r]] - lse[t]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int s = lane + 64 * r;
+            a[r] = s < S ? nxt[r] : -INFINITY;
+            if (s < S) alpha_ws[(size_t)t * S + s] = a[r];
+        }
+    }
+}
+
+template <int R>
+__device__ void ctc_beta(const float* __restrict__ logits, const float* lse, const int* lab,
+                         int S, int L, int B, int C, int b, int blank, float* __restrict__ beta_ws) {
+    const int lane = threadIdx.x & 63;
+    int cls[R];
+    bool skipn[R];   // transition s -> s+2 allowed
+    float bt[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int s = lane + 64 * r;
+        cls[r] = (s < S) ? ((s & 1) ? lab[s >> 1] : blank) : blank;
+        int s2 = s + 2;
+        skipn[r] = (s2 < S) && (s2 & 1) && s2 >= 3 && lab[s2 >> 1] != lab[(s2 >> 1) - 1];
+        bt[r] = (s < S && s >= S - 2) ? 0.f : -INFINITY;
+        if (s < S) beta_ws[(size_t)(L - 1) * S + s] = bt[r];
+    }
+    for (int t = L - 2; t >= 0; --t) {
+        const float* row = logits + ((size_t)(t + 1) * B + b) * C;
+        float nb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int s = lane + 64 * r;
+            nb[r] = s < S ? bt[r] + (row[cls[r]] - lse[t + 1]) : -INFINITY;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float b1 = shift_dn1(nb, r, R, lane);
+            float b2 = shift_dn2(nb, r, R, lane);
+            b2 = skipn[r] ? b2 : -INFINITY;
+            bt[r] = lse3(nb[r], b1, b2);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            int s = lane + 64 * r;
+            if (s < S) beta_ws[(size_t)t * S + s] = bt[r];
+            else bt[r] = -INFINITY;
+        }
+    }
+}
+
+template <int R>
+__global__ void __launch_bounds__(CTC_THREADS)
+ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
+                const int* __restrict__ label_len, const int* __restrict__ seq_len, int T, int B,
+                int C, int max_label, float grad_scale, float* __restrict__ loss,
+                float* __restrict__ grad, int* __restrict__ status, float* __restrict__ ws) {
+    __shared__ float s_lse[CTC_MAX_T];
+    __shared__ float s_occ[CTC_THREADS / 64][CTC_MAX_C];
+    __shared__ float s_logp;
+    __shared__ int s_req;
+    __shared__ int s_lab[CTC_MAX_R * 32];
+
+    const int b = blockIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int blank = C - 1;
+    const int L = min(max(seq_len[b], 0), T);
+    const int Lab = label_len[b];
+    const int S = 2 * Lab + 1;
+    const int Smax = 2 * max_label + 1;
+    float* alpha_ws = ws + (size_t)b * 2 * T * Smax;
+    float* beta_ws = alpha_ws + (size_t)T * Smax;
+
+    for (int i = threadIdx.x; i < Lab; i += CTC_THREADS) s_lab[i] = labels[(size_t)b * max_label + i];
+
+    // feasibility: L + #repeats <= seq_len  ([TF1] ctc_loss_calculator)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int reps = 0;
+        for (int i = 1; i < Lab; ++i) reps += s_lab[i] == s_lab[i - 1];
+        s_req = Lab + reps;
+    }
+    __syncthreads();
+    if (s_req > L || L == 0) {
+        if (threadIdx.x == 0) {
+            loss[b] = INFINITY;
+            if (status) status[b] = 1;
+        }
+        if (grad)
+            for (int i = threadIdx.x; i < T * C; i += CTC_THREADS) {
+                int t = i / C, k = i % C;
+                grad[((size_t)t * B + b) * C + k] = 0.f;
+            }
+        return;
+    }
+    if (status && threadIdx.x == 0) status[b] = 0;
+
+    // log-sum-exp of every valid frame, one frame per wave at a time
+    for (int t = wave; t < L; t += CTC_THREADS / 64) {
+        const float* row = logits + ((size_t)t * B + b) * C;
+        float m = -INFINITY;
+        for (int k = lane; k < C; k += 64) m = fmaxf(m, row[k]);
+        m = wave_max(m);
+        float s = 0.f;
+        for (int k = lane; k < C; k += 64) s += expf(row[k] - m);
+        s = wave_sum(s);
+        if (lane == 0) s_lse[t] = m + logf(s);
+    }
+    __syncthreads();
+
+    if (wave == 0)
+        ctc_alpha<R>(logits, s_lse, s_lab, S, L, B, C, b, blank, alpha_ws);
+    else if (wave == 1)
+        ctc_beta<R>(logits, s_lse, s_lab, S, L, B, C, b, blank, beta_ws);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float* last = alpha_ws + (size_t)(L - 1) * S;
+        s_logp = S >= 2 ? lse2(last[S - 1], last[S - 2]) : last[0];
+    }
+    __syncthreads();
+    const float logp = s_logp;
+    if (threadIdx.x == 0) loss[b] = -logp;
+    if (!grad) return;
+
+    // grad[t,k] = softmax - sum_{s: l'_s = k} exp(alpha + beta - logp)
+    float* occ = s_occ[wave];
+    for (int t = wave; t < T; t += CTC_THREADS / 64) {
+        float* grow = grad + ((size_t)t * B + b) * C;
+        if (t >= L) {
+            for (int k = lane; k < C; k += 64) grow[k] = 0.f;
+            continue;
+        }
+        for (int k = lane; k < C; k += 64) occ[k] = 0.f;
+        __builtin_amdgcn_wave_barrier();
+        for (int s = lane; s < S; s += 64) {
+            float v = expf(alpha_ws[(size_t)t * S + s] + beta_ws[(size_t)t * S + s] - logp);
+            int k = (s & 1) ? s_lab[s >> 1] : blank;
+            atomicAdd(&occ[k], v);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const float* row = logits + ((size_t)t * B + b) * C;
+        for (int k = lane; k < C; k += 64)
+            grow[k] = grad_scale * (expf(row[k] - s_lse[t]) - occ[k]);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ------------------------------------------------------------- greedy decode
+// One wave per sequence. Pass 1: argmax (first max on ties, [TF1] Eigen
+// maxCoeff) of each frame t < seq_len into LDS. Pass 2: lane 0 walks the
+// frames in order: merge repeats, drop blanks, and sums the maxima in frame
+// order (neg_sum_logits, the decoder's log_probability output).
+#define GREEDY_MAX_T 4096
+__global__ void __launch_bounds__(64)
+ctc_greedy_kernel(const float* __restrict__ logits, const int* __restrict__ seq_len, int T, int B,
+                  int C, int merge_repeated, int64_t* __restrict__ out, int* __restrict__ out_len,
+                  float* __restrict__ neg_sum) {
+    __shared__ int s_arg[GREEDY_MAX_T];
+    __shared__ float s_max[GREEDY_MAX_T];
+    __shared__ int s_n;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int L = min(max(seq_len[b], 0), T);
+    const int blank = C - 1;
+    for (int t = 0; t < L; ++t) {
+        const float* row = logits + ((size_t)t * B + b) * C;
+        float best = -INFINITY;
+        int arg = 0x7fffffff;
+        for (int k = lane; k < C; k += 64) {
+            float v = row[k];
+            if (v > best) { best = v; arg = k; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            float ov = __shfl_xor(best, o, 64);
+            int oa = __shfl_xor(arg, o, 64);
+            if (ov > best || (ov == best && oa < arg)) { best = ov; arg = oa; }
+        }
+        if (lane == 0) { s_arg[t] = arg; s_max[t] = best; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
+    if (lane == 0) {
+        int n = 0, prev = -1;
+        float acc = 0.f;
+        for (int t = 0; t < L; ++t) {
+            int k = s_arg[t];
+            acc -= s_max[t];
+            if (k != blank && !(merge_repeated && k == prev)) out[(size_t)b * T + n++] = k;
+            prev = k;
+        }
+        out_len[b] = n;
+        s_n = n;
+        if (neg_sum) neg_sum[b] = acc;
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int i = lane; i < T; i += 64)
+        if (i >= n) out[(size_t)b * T + i] = -1;
+}
+
+// ------------------------------------------------------------------- C ABI
+extern "C" size_t ocrk_ctc_workspace_size(int T, int B, int max_label_len) {
+    return (size_t)B * 2 * T * (2 * (size_t)max_label_len + 1) * sizeof(float);
+}
+
+extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* label_len,
+                             const int* seq_len, int T, int B, int C, int max_label_len,
+                             float grad_scale, float* loss, float* grad, int* status, void* ws,
+                             size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(T > 0 && T <= CTC_MAX_T, "ocrk_ctc_loss: T=%d out of range (1..%d)", T, CTC_MAX_T);
+    OCRK_REQUIRE(B >= 0 && C >= 2 && C <= CTC_MAX_C, "ocrk_ctc_loss: bad B=%d / C=%d", B, C);
+    OCRK_REQUIRE(max_label_len >= 0 && 2 * max_label_len + 1 <= 64 * CTC_MAX_R,
+                 "ocrk_ctc_loss: max_label_len=%d too long (<= %d)", max_label_len, (64 * CTC_MAX_R - 1) / 2);
+    OCRK_REQUIRE(ws_bytes >= ocrk_ctc_workspace_size(T, B, max_label_len),
+                 "ocrk_ctc_loss: workspace too small");
+    if (B == 0) return OCRK_OK;
+    OCRK_REQUIRE(logits && labels && label_len && seq_len && loss && ws, "ocrk_ctc_loss: null pointer");
+    int R = (2 * max_label_len + 1 + 63) / 64;
+    hipStream_t s = ocrk::as_stream(stream);
+#define CTC_LAUNCH(RR)                                                                          \
+    ctc_loss_kernel<RR><<<B, CTC_THREADS, 0, s>>>(logits, labels, label_len, seq_len, T, B, C,  \
+                                                  max_label_len, grad_scale, loss, grad, status, \
+                                                  (float*)ws)
+    if (R <= 1) CTC_LAUNCH(1);
+    else if (R <= 2) CTC_LAUNCH(2);
+    else if (R <= 4) CTC_LAUNCH(4);
+    else CTC_LAUNCH(8);
+#undef CTC_LAUNCH
+    return ocrk::launch_status("ocrk_ctc_loss");
+}
+
+extern "C" int ocrk_ctc_greedy_decode(const float* logits, const int* seq_len, int T, int B, int C,
+                                      int merge_repeated, int64_t* out, int* out_len,
+                                      float* neg_sum_logits, void* stream) {
+    OCRK_REQUIRE(T > 0 && T <= GREEDY_MAX_T && B >= 0 && C >= 1,
+                 "ocrk_ctc_greedy_decode: bad sizes T=%d B=%d C=%d", T, B, C);
+    if (B == 0) return OCRK_OK;
+    OCRK_REQUIRE(logits && seq_len && out && out_len, "ocrk_ctc_greedy_decode: null pointer");
+    ctc_greedy_kernel<<<B, 64, 0, ocrk::as_stream(stream)>>>(logits, seq_len, T, B, C, merge_repeated,
+                                                             out, out_len, neg_sum_logits);
+    return ocrk::launch_status("ocrk_ctc_greedy_decode");
+}

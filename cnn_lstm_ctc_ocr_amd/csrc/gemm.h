@@ -1,0 +1,51 @@
+// MFMA GEMM engine shared by the conv, recurrent-projection and logits ops.
+//
+//   C[M,N] (+)= A[M,K] . B[K,N]  (+ bias[N]) (ReLU) (* mask>0)    fp32 accumulate
+//
+// Operands are staged global -> registers -> LDS (double buffered, one barrier
+// per 32-deep k-step) into a canonical k-contiguous image [rows][32+8]; the
+// staging layer is what makes one kernel serve every op on the path:
+//   A_ROWK         A(m,k) = A[m*lda + k]                 (activations, row major)
+//   A_COLK         A(m,k) = A[k*lda + m]                 (activations, transposed: weight grads)
+//   A_IM2COL       A(m,k) = x[b, h+kh-1, w+kw-1, c]      (3x3 'same' conv forward)
+//   A_IM2COL_FLIP  A(m,k) = dy[b, h-kh+1, w-kw+1, c]     (conv backward-data)
+//   A_IM2COL_T     A(i,k) = x[b, h+kh-1, w+kw-1, c], i=(kh,kw,c), k=(b,h,w)  (conv weight grad)
+//   B_NK           B(k,n) = B[n*ldb + k]                 (weights stored [N][K])
+//   B_KN           B(k,n) = B[k*ldb + n]                 (activations / grads stored [K][N])
+// compute types: bf16 (v_mfma_f32_16x16x32_bf16) and f32 (v_mfma_f32_16x16x4_f32,
+// exact fp32 products).
+#pragma once
+#include "common.h"
+
+namespace ocrk {
+
+enum AMode { A_ROWK = 0, A_COLK = 1, A_IM2COL = 2, A_IM2COL_FLIP = 3, A_IM2COL_T = 4 };
+enum BMode { B_NK = 0, B_KN = 1 };
+
+struct GemmParams {
+    int M, N, K;
+    int batch;                     // independent problems along grid.z (with strides)
+    const void* A; int64_t lda; int64_t strideA;
+    const void* B; int64_t ldb; int64_t strideB;
+    void* C; int64_t ldc; int64_t strideC;
+    int c_bf16;                    // C element type: 0 f32, 1 bf16
+    const float* bias; int64_t strideBias;   // [N] per problem or NULL
+    const void* mask; int64_t ldmask;        // C *= (mask[m,n] > 0); mask has the compute type; or NULL
+    int accumulate;                // C += result (f32 C only)
+    int relu;
+    float alpha;
+    float* stats;                  // per (m-tile, column): [gridDim.x][2][N] sum and M2 of the tile's rows, or NULL
+    float* splitk_ws;              // [batch][splits][M][N] f32 partials when splits > 1
+    int splits;
+    int k_chunk;                   // k-range per split (multiple of 32)
+    int convH, convW, convC;       // im2col source geometry (NHWC) for the A_IM2COL* modes
+};
+
+// Launch C = A.B with the given operand modes. dtype: OCRK_F32 / OCRK_BF16
+// (type of A and B). Picks the tile shape from M, N.
+int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+
+// Split-K GEMM: partials into p.splitk_ws, then a reduce applying the epilogue.
+size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
+
+}  // namespace ocrk

@@ -1,0 +1,384 @@
+// MFMA GEMM engine (see gemm.h for the operand modes).
+//
+// Tile: TBM x TBN x 32, 256 threads = 4 waves in a 2 x 2 grid, each wave owns a
+// (TBM/2) x (TBN/2) block of 16 x 16 MFMA accumulators. Global -> register
+// staging of tile k+1 is issued before the MFMAs of tile k and written to the
+// other LDS buffer after them (one barrier per k-step). LDS rows are padded by
+// 8 elements (16 B for bf16) so the per-lane 16-B fragment reads of a 16-row
+// group fall on distinct bank groups.
+#include "gemm.h"
+#include "mfma_util.h"
+
+namespace ocrk {
+
+// Element (row, k) address for the A operand; ok=false -> zero.
+template <int AM, typename CT>
+__device__ __forceinline__ const CT* a_addr(const GemmParams& p, const CT* A, int m, int k, bool& ok) {
+    if constexpr (AM == A_ROWK) {
+        ok = m < p.M && k < p.K;
+        return A + (int64_t)m * p.lda + k;
+    } else if constexpr (AM == A_COLK) {
+        ok = m < p.M && k < p.K;
+        return A + (int64_t)k * p.lda + m;
+    } else {
+        // pixel index and (tap, channel) index
+        int pix, kidx;
+        if constexpr (AM == A_IM2COL_T) { pix = k; kidx = m; ok = k < p.K && m < p.M; }
+        else { pix = m; kidx = k; ok = m < p.M && k < p.K; }
+        const int C = p.convC, W = p.convW, H = p.convH;
+        int tap = kidx / C, c = kidx - tap * C;
+        int kh = tap / 3, kw = tap - kh * 3;
+        int w = pix % W, t2 = pix / W, h = t2 % H, b = t2 / H;
+        int hh, ww;
+        if constexpr (AM == A_IM2COL_FLIP) { hh = h - kh + 1; ww = w - kw + 1; }
+        else { hh = h + kh - 1; ww = w + kw - 1; }
+        ok = ok && hh >= 0 && hh < H && ww >= 0 && ww < W;
+        return A + (((int64_t)b * H + hh) * W + ww) * C + c;
+    }
+}
+
+template <int BMD, typename CT>
+__device__ __forceinline__ const CT* b_addr(const GemmParams& p, const CT* B, int n, int k, bool& ok) {
+    ok = n < p.N && k < p.K;
+    if constexpr (BMD == B_NK) return B + (int64_t)n * p.ldb + k;
+    else return B + (int64_t)k * p.ldb + n;
+}
+
+template <typename CT, int AM, int BMD, int TBM, int TBN>
+__global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
+    using RT = typename RawT<CT>::T;
+    constexpr int BK = 32, LDK = BK + 8;
+    constexpr int WM = TBM / 2, WN = TBN / 2, TM = WM / 16, TN = WN / 16;
+    constexpr bool A_K = (AM == A_ROWK || AM == A_IM2COL || AM == A_IM2COL_FLIP);
+    constexpr bool B_K = (BMD == B_NK);
+    constexpr int NVA = (TBM * BK / 8 + 255) / 256;
+    constexpr int NVB = (TBN * BK / 8 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) RT sA[2][TBM * LDK];
+    __shared__ __attribute__((aligned(16))) RT sB[2][TBN * LDK];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.x * TBM, n0 = blockIdx.y * TBN;
+    const int zb = blockIdx.z / p.splits, zs = blockIdx.z - zb * p.splits;
+    const CT* A = reinterpret_cast<const CT*>(p.A) + zb * p.strideA;
+    const CT* B = reinterpret_cast<const CT*>(p.B) + zb * p.strideB;
+    const int kbeg = zs * p.k_chunk;
+    const int kend = min(p.K, kbeg + p.k_chunk);
+    const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+
+    V8<CT> ra[NVA], rb[NVB];
+    auto load_tiles = [&](int k0) {
+#pragma unroll
+        for (int v = 0; v < NVA; ++v) {
+            int idx = tid + 256 * v;
+            vzero(ra[v]);
+            if (idx < TBM * BK / 8) {
+                int m, k;
+                if constexpr (A_K) { m = m0 + (idx >> 2); k = k0 + 8 * (idx & 3); }
+                else { k = k0 + idx / (TBM / 8); m = m0 + 8 * (idx % (TBM / 8)); }
+                bool ok;
+                const CT* src = a_addr<AM, CT>(p, A, m, k, ok);
+                if (ok && k < kend) vload(ra[v], src);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+            int idx = tid + 256 * v;
+            vzero(rb[v]);
+            if (idx < TBN * BK / 8) {
+                int n, k;
+                if constexpr (B_K) { n = n0 + (idx >> 2); k = k0 + 8 * (idx & 3); }
+                else { k = k0 + idx / (TBN / 8); n = n0 + 8 * (idx % (TBN / 8)); }
+                bool ok;
+                const CT* src = b_addr<BMD, CT>(p, B, n, k, ok);
+                if (ok && k < kend) vload(rb[v], src);
+            }
+        }
+    };
+    auto store_tiles = [&](int buf) {
+#pragma unroll
+        for (int v = 0; v < NVA; ++v) {
+            int idx = tid + 256 * v;
+            if (idx < TBM * BK / 8) {
+                if constexpr (A_K) {
+                    vstore_lds(&sA[buf][(idx >> 2) * LDK + 8 * (idx & 3)], ra[v]);
+                } else {
+                    int kk = idx / (TBM / 8), r0 = 8 * (idx % (TBM / 8));
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) sA[buf][(r0 + i) * LDK + kk] = ra[v].e(i);
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+            int idx = tid + 256 * v;
+            if (idx < TBN * BK / 8) {
+                if constexpr (B_K) {
+                    vstore_lds(&sB[buf][(idx >> 2) * LDK + 8 * (idx & 3)], rb[v]);
+                } else {
+                    int kk = idx / (TBN / 8), r0 = 8 * (idx % (TBN / 8));
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) sB[buf][(r0 + i) * LDK + kk] = rb[v].e(i);
+                }
+            }
+        }
+    };
+
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) {
+        load_tiles(kbeg);
+        store_tiles(0);
+        __syncthreads();
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+        const RT* a_base = &sA[buf][(wm * WM + (lane & 15)) * LDK + 8 * (lane >> 4)];
+        const RT* b_base = &sB[buf][(wn * WN + (lane & 15)) * LDK + 8 * (lane >> 4)];
+        if constexpr (sizeof(CT) == 2) {
+            bf16x8 af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a_base + i * 16 * LDK);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b_base + j * 16 * LDK);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        } else {
+            // f32: lane group g = lane>>4 feeds k-slot g with k = 8g + kk (same map for A and B)
+            V8<float> af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) vload_lds(af[i], a_base + i * 16 * LDK);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) vload_lds(bfr[j], b_base + j * 16 * LDK);
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].e(kk), bfr[j].e(kk), acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_tiles(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ------------------------------------------------------------ epilogue
+    const int row_base = m0 + wm * WM + (lane >> 4) * 4;
+    const int col_base = n0 + wn * WN + (lane & 15);
+    if (p.splits > 1) {
+        float* ws = p.splitk_ws + ((int64_t)zb * p.splits + zs) * (int64_t)p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int row = row_base + i * 16 + r, col = col_base + j * 16;
+                    if (row < p.M && col < p.N) ws[(int64_t)row * p.N + col] = acc[i][j][r];
+                }
+        return;
+    }
+    const float* bias = p.bias ? p.bias + zb * p.strideBias : nullptr;
+    const CT* mask = reinterpret_cast<const CT*>(p.mask);
+    float* Cf = reinterpret_cast<float*>(p.C) + zb * p.strideC;
+    bf16* Cb = reinterpret_cast<bf16*>(p.C) + zb * p.strideC;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            int col = col_base + j * 16;
+            float bcol = (bias && col < p.N) ? bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int row = row_base + i * 16 + r;
+                float v = p.alpha * acc[i][j][r] + bcol;
+                if (row < p.M && col < p.N) {
+                    if (mask && !(to_f32(mask[(int64_t)row * p.ldmask + col]) > 0.f)) v = 0.f;
+                    if (p.relu) v = fmaxf(v, 0.f);
+                    int64_t off = (int64_t)row * p.ldc + col;
+                    if (p.c_bf16) {
+                        Cb[off] = (bf16)v;
+                    } else {
+                        if (p.accumulate) v += Cf[off];
+                        Cf[off] = v;
+                    }
+                }
+                acc[i][j][r] = v;   // keep the epilogue value for the statistics below
+            }
+        }
+    if (!p.stats) return;
+
+    // Per-column (sum, M2) of this tile's valid rows, pre-activation values.
+    // Two register passes (tile mean first) keep the later Chan merge stable.
+    __shared__ float s_red[2][TBN];
+    const int valid_rows = min(TBM, p.M - m0);
+    float tsum[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (row_base + i * 16 + r < p.M) s += acc[i][j][r];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        tsum[j] = s;
+    }
+    if (lane < 16)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) s_red[wm][wn * WN + j * 16 + lane] = tsum[j];
+    __syncthreads();
+    float tmean[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        int c = wn * WN + j * 16 + (lane & 15);
+        tsum[j] = s_red[0][c] + s_red[1][c];
+        tmean[j] = tsum[j] / (float)valid_rows;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (row_base + i * 16 + r < p.M) {
+                    float d = acc[i][j][r] - tmean[j];
+                    s += d * d;
+                }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (lane < 16) s_red[wm][wn * WN + j * 16 + lane] = s;
+    }
+    __syncthreads();
+    if (wm == 0 && lane < 16) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            int c = wn * WN + j * 16 + lane;
+            if (n0 + c < p.N) {
+                float* st = p.stats + (int64_t)blockIdx.x * 2 * p.N;
+                st[n0 + c] = tsum[j];
+                st[p.N + n0 + c] = s_red[0][c] + s_red[1][c];
+            }
+        }
+    }
+}
+
+// Sum the split-K partials and apply the epilogue (bias / relu / accumulate).
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmParams p) {
+    const int64_t MN = (int64_t)p.M * p.N;
+    const int zb = blockIdx.y;
+    const float* ws = p.splitk_ws + (int64_t)zb * p.splits * MN;
+    const float* bias = p.bias ? p.bias + zb * p.strideBias : nullptr;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += (int64_t)gridDim.x * 256) {
+        float v = 0.f;
+        for (int s = 0; s < p.splits; ++s) v += ws[s * MN + e];
+        int row = (int)(e / p.N), col = (int)(e - (int64_t)row * p.N);
+        v = p.alpha * v + (bias ? bias[col] : 0.f);
+        if (p.relu) v = fmaxf(v, 0.f);
+        int64_t off = zb * p.strideC + (int64_t)row * p.ldc + col;
+        if (p.c_bf16) {
+            reinterpret_cast<bf16*>(p.C)[off] = (bf16)v;
+        } else {
+            float* C = reinterpret_cast<float*>(p.C);
+            C[off] = p.accumulate ? C[off] + v : v;
+        }
+    }
+}
+
+size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
+    return splits > 1 ? (size_t)batch * splits * M * N * sizeof(float) : 0;
+}
+
+template <typename CT, int AM, int BMD>
+static int launch_tiles(const GemmParams& p0, hipStream_t stream) {
+    GemmParams p = p0;
+    int TBM = 128, TBN = p.N <= 32 ? 32 : (p.N <= 64 ? 64 : 128);
+    dim3 grid((unsigned)cdiv(p.M, TBM), (unsigned)cdiv(p.N, TBN), (unsigned)(p.batch * p.splits));
+    if (TBN == 32) gemm_kernel<CT, AM, BMD, 128, 32><<<grid, 256, 0, stream>>>(p);
+    else if (TBN == 64) gemm_kernel<CT, AM, BMD, 128, 64><<<grid, 256, 0, stream>>>(p);
+    else gemm_kernel<CT, AM, BMD, 128, 128><<<grid, 256, 0, stream>>>(p);
+    int st = launch_status("gemm");
+    if (st != OCRK_OK || p.splits <= 1) return st;
+    int64_t MN = (int64_t)p.M * p.N;
+    dim3 rg((unsigned)std::min<int64_t>(cdiv(MN, 256), 4096), (unsigned)p.batch);
+    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(p);
+    return launch_status("gemm splitk reduce");
+}
+
+template <typename CT>
+static int dispatch_modes(const GemmParams& p, int amode, int bmode, hipStream_t s) {
+#define GM(AMx, BMx) if (amode == AMx && bmode == BMx) return launch_tiles<CT, AMx, BMx>(p, s)
+    GM(A_ROWK, B_NK);
+    GM(A_ROWK, B_KN);
+    GM(A_COLK, B_KN);
+    GM(A_IM2COL, B_NK);
+    GM(A_IM2COL_FLIP, B_NK);
+    GM(A_IM2COL_T, B_KN);
+#undef GM
+    set_error("gemm: unsupported operand modes A=%d B=%d", amode, bmode);
+    return OCRK_ERR_INVALID_ARG;
+}
+
+int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {
+    if (p.M <= 0 || p.N <= 0 || p.batch <= 0) return OCRK_OK;
+    OCRK_REQUIRE(p.K >= 0 && p.splits >= 1 && p.k_chunk > 0 && p.k_chunk % 32 == 0,
+                 "gemm: bad K=%d splits=%d k_chunk=%d", p.K, p.splits, p.k_chunk);
+    bool a_rows = (amode == A_COLK || amode == A_IM2COL_T);
+    OCRK_REQUIRE(p.K % 8 == 0 || (a_rows && bmode == B_KN),
+                 "gemm: K=%d must be a multiple of 8 for k-contiguous operands", p.K);
+    OCRK_REQUIRE(!a_rows || p.M % 8 == 0, "gemm: M=%d must be a multiple of 8 for this A mode", p.M);
+    OCRK_REQUIRE(bmode != B_KN || p.N % 8 == 0, "gemm: N=%d must be a multiple of 8 for B_KN", p.N);
+    OCRK_REQUIRE(amode < A_IM2COL || p.convC % 8 == 0, "gemm: conv channels must be a multiple of 8");
+    OCRK_REQUIRE(!(p.stats && (p.splits > 1 || p.batch > 1)), "gemm: stats need splits=1, batch=1");
+    OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
+    if (dtype == OCRK_BF16) return dispatch_modes<bf16>(p, amode, bmode, stream);
+    if (dtype == OCRK_F32) return dispatch_modes<float>(p, amode, bmode, stream);
+    set_error("gemm: unsupported dtype %d", dtype);
+    return OCRK_ERR_INVALID_ARG;
+}
+
+}  // namespace ocrk
+
+// ------------------------------------------------------------------- C ABI
+// Generic dense GEMM used by the recurrent projections and the logits layer:
+// C[b] = alpha * op(A[b]) . op(B[b]) + bias (ReLU), op per trans flags:
+//   trans_a = 0: A is [M][K] (lda), 1: A is [K][M];  trans_b = 0: B is [K][N], 1: B is [N][K].
+extern "C" size_t ocrk_gemm_workspace_size(int M, int N, int batch, int splits) {
+    return ocrk::gemm_splitk_ws_bytes(M, N, batch, splits);
+}
+
+extern "C" int ocrk_gemm(int trans_a, int trans_b, int M, int N, int K, float alpha, const void* A,
+                         int64_t lda, int64_t stride_a, const void* B, int64_t ldb, int64_t stride_b,
+                         void* C, int64_t ldc, int64_t stride_c, int c_dtype, const float* bias,
+                         int relu, int accumulate, int batch, int dtype, int splits, void* ws,
+                         size_t ws_bytes, void* stream) {
+    ocrk::GemmParams p = {};
+    p.M = M; p.N = N; p.K = K; p.batch = batch < 1 ? 1 : batch;
+    p.A = A; p.lda = lda; p.strideA = stride_a;
+    p.B = B; p.ldb = ldb; p.strideB = stride_b;
+    p.C = C; p.ldc = ldc; p.strideC = stride_c;
+    p.c_bf16 = c_dtype == OCRK_BF16;
+    p.bias = bias; p.strideBias = 0;
+    p.relu = relu; p.accumulate = accumulate; p.alpha = alpha;
+    p.splits = splits < 1 ? 1 : splits;
+    int kc = (int)ocrk::cdiv(K, p.splits);
+    p.k_chunk = (int)ocrk::cdiv(kc < 32 ? 32 : kc, 32) * 32;
+    p.splits = (int)ocrk::cdiv(K > 0 ? K : 1, p.k_chunk);
+    p.splitk_ws = (float*)ws;
+    OCRK_REQUIRE(p.splits == 1 || ws_bytes >= ocrk::gemm_splitk_ws_bytes(M, N, p.batch, p.splits),
+                 "ocrk_gemm: split-K workspace too small");
+    int amode = trans_a ? ocrk::A_COLK : ocrk::A_ROWK;
+    int bmode = trans_b ? ocrk::B_NK : ocrk::B_KN;
+    return ocrk::gemm(p, amode, bmode, dtype, ocrk::as_stream(stream));
+}

@@ -1,0 +1,49 @@
+// Register/LDS staging helpers shared by the MFMA kernels (gemm.hip, lstm.hip).
+#pragma once
+#include "common.h"
+
+namespace ocrk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 8 consecutive elements of the compute type held in registers. Plain
+// ext-vector members (no unions, no struct copies from memory): loads become
+// vector loads and SROA keeps every staging set in VGPRs.
+template <typename CT> struct V8;
+template <> struct V8<bf16> {
+    u32x4 q;
+    __device__ __forceinline__ unsigned short e(int i) const {
+        return (unsigned short)(q[i >> 1] >> (16 * (i & 1)));
+    }
+};
+template <> struct V8<float> {
+    f32x4 q0, q1;
+    __device__ __forceinline__ float e(int i) const { return i < 4 ? q0[i] : q1[i - 4]; }
+};
+template <typename CT> struct RawT;
+template <> struct RawT<bf16> { using T = unsigned short; };
+template <> struct RawT<float> { using T = float; };
+
+__device__ __forceinline__ void vzero(V8<bf16>& x) { x.q = u32x4{0u, 0u, 0u, 0u}; }
+__device__ __forceinline__ void vzero(V8<float>& x) { x.q0 = x.q1 = f32x4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ void vload(V8<bf16>& x, const bf16* p) { x.q = *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void vload(V8<float>& x, const float* p) {
+    x.q0 = reinterpret_cast<const f32x4*>(p)[0];
+    x.q1 = reinterpret_cast<const f32x4*>(p)[1];
+}
+__device__ __forceinline__ void vload_lds(V8<bf16>& x, const unsigned short* p) { x.q = *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void vload_lds(V8<float>& x, const float* p) {
+    x.q0 = reinterpret_cast<const f32x4*>(p)[0];
+    x.q1 = reinterpret_cast<const f32x4*>(p)[1];
+}
+__device__ __forceinline__ void vstore_lds(unsigned short* d, const V8<bf16>& x) { *reinterpret_cast<u32x4*>(d) = x.q; }
+__device__ __forceinline__ void vstore_lds(float* d, const V8<float>& x) {
+    reinterpret_cast<f32x4*>(d)[0] = x.q0;
+    reinterpret_cast<f32x4*>(d)[1] = x.q1;
+}
+
+}  // namespace ocrk

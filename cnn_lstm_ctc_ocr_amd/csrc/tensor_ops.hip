@@ -1,0 +1,179 @@
+// Small byte-moving kernels around the hot ops: dtype casts, the weight-image
+// permutes (HWIO -> [Cout][kh][kw][Cin] for the forward conv GEMM and
+// [Cin][kh][kw][Cout] for backward-data), deterministic column sums (bias
+// gradients) and the ReLU-mask product of the logits layer backward.
+#include "common.h"
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        out[i] = from_f32<TO>(to_f32(in[i]));
+}
+
+// out[i1][i0][i2] = in[i0][i1][i2]
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) permute3_kernel(const TI* __restrict__ in, int d0, int d1, int d2,
+                                                       TO* __restrict__ out) {
+    const int64_t n = (int64_t)d0 * d1 * d2;
+    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += (int64_t)gridDim.x * 256) {
+        int i2 = (int)(o % d2);
+        int64_t t = o / d2;
+        int i0 = (int)(t % d0);
+        int i1 = (int)(t / d0);
+        out[o] = from_f32<TO>(to_f32(in[((int64_t)i0 * d1 + i1) * d2 + i2]));
+    }
+}
+
+// column sums of [M][N]: block partials over row ranges, then an ordered sum.
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict__ in, int64_t M, int N,
+                                                             int64_t rows_per_block, float* __restrict__ slab) {
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    for (int c = threadIdx.x; c < N; c += 256) {
+        float s = 0.f;
+        for (int64_t r = r0; r < r1; ++r) s += to_f32(in[r * N + c]);
+        slab[(int64_t)blockIdx.x * N + c] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ slab, int nslab, int N,
+                                                           float* __restrict__ out, int accumulate) {
+    int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= N) return;
+    double s = 0.0;
+    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * N + c];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+template <typename TO>
+__global__ void __launch_bounds__(256) relu_mask_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                        int64_t n, float scale, TO* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        out[i] = from_f32<TO>(y[i] > 0.f ? dy[i] * scale : 0.f);
+}
+
+static unsigned grid1d(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ocrk::cdiv(n, 256), 16384)); }
+
+extern "C" int ocrk_cast(const void* in, int in_dtype, void* out, int out_dtype, int64_t n, void* stream) {
+    if (n == 0) return OCRK_OK;
+    hipStream_t s = ocrk::as_stream(stream);
+    if (in_dtype == OCRK_F32 && out_dtype == OCRK_BF16) cast_kernel<float, bf16><<<grid1d(n), 256, 0, s>>>((const float*)in, (bf16*)out, n);
+    else if (in_dtype == OCRK_BF16 && out_dtype == OCRK_F32) cast_kernel<bf16, float><<<grid1d(n), 256, 0, s>>>((const bf16*)in, (float*)out, n);
+    else if (in_dtype == OCRK_F32 && out_dtype == OCRK_F32) cast_kernel<float, float><<<grid1d(n), 256, 0, s>>>((const float*)in, (float*)out, n);
+    else cast_kernel<bf16, bf16><<<grid1d(n), 256, 0, s>>>((const bf16*)in, (bf16*)out, n);
+    return ocrk::launch_status("ocrk_cast");
+}
+
+extern "C" int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d2, void* out, int out_dtype,
+                             void* stream) {
+    int64_t n = (int64_t)d0 * d1 * d2;
+    if (n == 0) return OCRK_OK;
+    hipStream_t s = ocrk::as_stream(stream);
+    OCRK_REQUIRE(in_dtype == OCRK_F32, "ocrk_permute3: f32 input only");
+    if (out_dtype == OCRK_BF16) permute3_kernel<float, bf16><<<grid1d(n), 256, 0, s>>>((const float*)in, d0, d1, d2, (bf16*)out);
+    else permute3_kernel<float, float><<<grid1d(n), 256, 0, s>>>((const float*)in, d0, d1, d2, (float*)out);
+    return ocrk::launch_status("ocrk_permute3");
+}
+
+static int64_t colsum_blocks(int64_t M) { return std::max<int64_t>(1, std::min<int64_t>(1024, ocrk::cdiv(M, 256))); }
+
+extern "C" size_t ocrk_colsum_workspace_size(int64_t M, int N) {
+    return (size_t)colsum_blocks(M) * N * sizeof(float);
+}
+
+extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
+                           size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(ws_bytes >= ocrk_colsum_workspace_size(M, N), "ocrk_colsum: workspace too small");
+    if (N == 0) return OCRK_OK;
+    int64_t nb = colsum_blocks(M);
+    int64_t rpb = ocrk::cdiv(M, nb);
+    nb = std::max<int64_t>(1, ocrk::cdiv(M, rpb));
+    hipStream_t s = ocrk::as_stream(stream);
+    if (dtype == OCRK_BF16) colsum_partial_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)in, M, N, rpb, (float*)ws);
+    else colsum_partial_kernel<float><<<nb, 256, 0, s>>>((const float*)in, M, N, rpb, (float*)ws);
+    int st = ocrk::launch_status("ocrk_colsum");
+    if (st) return st;
+    colsum_final_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws, (int)nb, N, out, accumulate);
+    return ocrk::launch_status("ocrk_colsum final");
+}
+
+extern "C" int ocrk_relu_mask(const float* dy, const float* y, int64_t n, float scale, void* out, int out_dtype,
+                              void* stream) {
+    if (n == 0) return OCRK_OK;
+    hipStream_t s = ocrk::as_stream(stream);
+    if (out_dtype == OCRK_BF16) relu_mask_kernel<bf16><<<grid1d(n), 256, 0, s>>>(dy, y, n, scale, (bf16*)out);
+    else relu_mask_kernel<float><<<grid1d(n), 256, 0, s>>>(dy, y, n, scale, (float*)out);
+    return ocrk::launch_status("ocrk_relu_mask");
+}
+
+// out[r*out_rs + c*out_cs] = in[r*in_rs + c*in_cs]  (weight images for the GEMMs)
+template <typename TO>
+__global__ void __launch_bounds__(256) strided_copy_kernel(const float* __restrict__ in, int64_t rows, int64_t cols,
+                                                           int64_t in_rs, int64_t in_cs, TO* __restrict__ out,
+                                                           int64_t out_rs, int64_t out_cs) {
+    const int64_t n = rows * cols;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        int64_t r = i / cols, c = i - r * cols;
+        out[r * out_rs + c * out_cs] = from_f32<TO>(in[r * in_rs + c * in_cs]);
+    }
+}
+
+extern "C" int ocrk_strided_copy(const float* in, int64_t rows, int64_t cols, int64_t in_rs, int64_t in_cs,
+                                 void* out, int out_dtype, int64_t out_rs, int64_t out_cs, void* stream) {
+    int64_t n = rows * cols;
+    if (n == 0) return OCRK_OK;
+    hipStream_t s = ocrk::as_stream(stream);
+    if (out_dtype == OCRK_BF16)
+        strided_copy_kernel<bf16><<<grid1d(n), 256, 0, s>>>(in, rows, cols, in_rs, in_cs, (bf16*)out, out_rs, out_cs);
+    else
+        strided_copy_kernel<float><<<grid1d(n), 256, 0, s>>>(in, rows, cols, in_rs, in_cs, (float*)out, out_rs, out_cs);
+    return ocrk::launch_status("ocrk_strided_copy");
+}
+
+// x[i] *= s[0]  (upstream scalar gradient applied on device, no host sync)
+__global__ void __launch_bounds__(256) mul_scalar_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ s) {
+    const float v = s[0];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) x[i] *= v;
+}
+
+extern "C" int ocrk_mul_scalar(float* x, int64_t n, const float* s, void* stream) {
+    if (n == 0) return OCRK_OK;
+    mul_scalar_kernel<<<grid1d(n), 256, 0, ocrk::as_stream(stream)>>>(x, n, s);
+    return ocrk::launch_status("ocrk_mul_scalar");
+}
+
+// out[0] = mean(x[0:n]) in a fixed order (reduce_mean of the CTC losses, model.py:228)
+__global__ void __launch_bounds__(256) mean_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+    __shared__ double s[256];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) acc += x[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) s[threadIdx.x] += s[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = n > 0 ? (float)(s[0] / n) : 0.f;
+}
+
+extern "C" int ocrk_mean(const float* x, int n, float* out, void* stream) {
+    mean_kernel<<<1, 256, 0, ocrk::as_stream(stream)>>>(x, n, out);
+    return ocrk::launch_status("ocrk_mean");
+}
+
+// convnet_layers tail (src/weinman/model.py:152-163): seq_len = floor((w - 2) / 2) - 2
+__global__ void seq_len_kernel(const int* __restrict__ widths, int n, int* __restrict__ out) {
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        int a = widths[i] - 2;
+        int q = a >= 0 ? a / 2 : -((-a + 1) / 2);   // floor division
+        out[i] = q - 1 - 1;
+    }
+}
+
+extern "C" int ocrk_seq_len(const int* widths, int n, int* out, void* stream) {
+    if (n == 0) return OCRK_OK;
+    seq_len_kernel<<<(n + 255) / 256, 256, 0, ocrk::as_stream(stream)>>>(widths, n, out);
+    return ocrk::launch_status("ocrk_seq_len");
+}

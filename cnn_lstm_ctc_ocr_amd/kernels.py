@@ -1,0 +1,321 @@
+"""Thin torch-tensor wrappers over the libocrk C ABI (one per entry point).
+
+They check shapes/dtypes/devices on the host, allocate outputs and workspaces
+with the torch caching allocator, and launch on torch's current stream. They
+do no math themselves: every call lands in libocrk.so (include/ocrk.h).
+"""
+import torch
+
+from . import _lib
+from ._lib import ptr, call
+
+F32, BF16 = _lib.F32, _lib.BF16
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtype_code(dt):
+    try:
+        return _DT[dt]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dt}; libocrk computes in float32 or bfloat16")
+
+
+def _stream(t):
+    return _lib.stream_ptr(t.device)
+
+
+def _chk(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("libocrk ops take device tensors (got a CPU tensor)")
+        if not t.is_contiguous():
+            raise ValueError("libocrk ops take contiguous tensors")
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------- preprocess
+def preprocess(img_u8, dtype=torch.float32):
+    """validate._preprocess_image (src/weinman/validate.py:56-68)."""
+    if img_u8.dtype != torch.uint8:
+        raise TypeError("preprocess expects uint8 pixels")
+    _chk(img_u8)
+    out = torch.empty(img_u8.shape, dtype=dtype, device=img_u8.device)
+    call("ocrk_preprocess", ptr(img_u8), img_u8.numel(), ptr(out), dtype_code(dtype), _stream(img_u8))
+    return out
+
+
+def seq_len(widths):
+    """model.py:152-163 on device: floor((w-2)/2) - 2 (int32)."""
+    _chk(widths)
+    w = widths if widths.dtype == torch.int32 else widths.to(torch.int32)
+    out = torch.empty_like(w)
+    call("ocrk_seq_len", ptr(w), w.numel(), ptr(out), _stream(w))
+    return out
+
+
+# --------------------------------------------------------------------- conv
+def conv1_fwd(x, w, b, dtype):
+    """x: uint8 [B,H,W] (fused preprocess) or float [B,H,W]; w f32 [3,3,1,C]; -> [B,H-2,W-2,C]."""
+    _chk(x, w, b)
+    B, H, W = x.shape[0], x.shape[1], x.shape[2]
+    C = w.shape[-1]
+    y = torch.empty(B, H - 2, W - 2, C, dtype=dtype, device=x.device)
+    is_u8 = x.dtype == torch.uint8
+    if not is_u8 and x.dtype != dtype:
+        raise TypeError("conv1 float input must have the compute dtype")
+    call("ocrk_conv1_fwd", ptr(x), int(is_u8), B, H, W, ptr(w), ptr(b), C, ptr(y), dtype_code(dtype), _stream(x))
+    return y
+
+
+def conv1_bwd_weight(x, dz, dw, db, accumulate=True):
+    _chk(x, dz, dw, db)
+    B, H, W = x.shape[0], x.shape[1], x.shape[2]
+    C = dz.shape[-1]
+    nb = _lib.lib().ocrk_conv1_wgrad_workspace_size(B, H, W, C)
+    ws = _ws(nb, x.device)
+    call("ocrk_conv1_bwd_weight", ptr(x), int(x.dtype == torch.uint8), ptr(dz), B, H, W, C, ptr(dw), ptr(db),
+         int(accumulate), ptr(ws), nb, dtype_code(dz.dtype), _stream(x))
+
+
+def conv_stats_tiles(M):
+    return _lib.lib().ocrk_conv_stats_tiles(M)
+
+
+def conv3x3_fwd(x, w_nk, bias, relu, stats=None, y_dtype=None):
+    _chk(x, w_nk, bias, stats)
+    B, H, W, Cin = x.shape
+    Cout = w_nk.shape[0]
+    y_dtype = y_dtype or x.dtype
+    y = torch.empty(B, H, W, Cout, dtype=y_dtype, device=x.device)
+    call("ocrk_conv3x3_fwd", ptr(x), B, H, W, Cin, ptr(w_nk), ptr(bias), Cout, ptr(y), dtype_code(y_dtype),
+         int(relu), ptr(stats), dtype_code(x.dtype), _stream(x))
+    return y
+
+
+def conv3x3_bwd_data(dy, w_bwd, relu_mask=None):
+    _chk(dy, w_bwd, relu_mask)
+    B, H, W, Cout = dy.shape
+    Cin = w_bwd.shape[0]
+    dx = torch.empty(B, H, W, Cin, dtype=dy.dtype, device=dy.device)
+    call("ocrk_conv3x3_bwd_data", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_mask),
+         dtype_code(dy.dtype), _stream(dy))
+    return dx
+
+
+def conv3x3_bwd_weight(x, dy, dw, accumulate=True):
+    _chk(x, dy, dw)
+    B, H, W, Cin = x.shape
+    Cout = dy.shape[-1]
+    nb = _lib.lib().ocrk_conv3x3_wgrad_workspace_size(B, H, W, Cin, Cout)
+    ws = _ws(nb, x.device)
+    call("ocrk_conv3x3_bwd_weight", ptr(x), ptr(dy), B, H, W, Cin, Cout, ptr(dw), int(accumulate), ptr(ws), nb,
+         dtype_code(x.dtype), _stream(x))
+
+
+# -------------------------------------------------------------- batch norm
+def bn_finalize(stats, M, C, eps, momentum, moving_mean=None, moving_var=None):
+    _chk(stats, moving_mean, moving_var)
+    tiles = stats.shape[0]
+    mean = torch.empty(C, dtype=torch.float32, device=stats.device)
+    invstd = torch.empty_like(mean)
+    call("ocrk_bn_finalize", ptr(stats), tiles, M, C, float(eps), float(momentum), ptr(mean), ptr(invstd),
+         ptr(moving_mean), ptr(moving_var), _stream(stats))
+    return mean, invstd
+
+
+def bn_infer_params(moving_mean, moving_var, eps):
+    _chk(moving_mean, moving_var)
+    C = moving_mean.numel()
+    mean = torch.empty(C, dtype=torch.float32, device=moving_mean.device)
+    invstd = torch.empty_like(mean)
+    call("ocrk_bn_infer_params", ptr(moving_mean), ptr(moving_var), C, float(eps), ptr(mean), ptr(invstd),
+         _stream(moving_mean))
+    return mean, invstd
+
+
+def bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=False):
+    _chk(z, mean, invstd, gamma, beta)
+    B, H, W, C = z.shape
+    kh, kw, sh, sw = pool
+    Ho, Wo = (H - kh) // sh + 1, (W - kw) // sw + 1
+    shape = (Wo, B, C) if time_major else (B, Ho, Wo, C)
+    out = torch.empty(shape, dtype=z.dtype, device=z.device)
+    call("ocrk_bn_relu_pool_fwd", ptr(z), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), kh, kw, sh, sw,
+         ptr(out), int(time_major), dtype_code(z.dtype), _stream(z))
+    return out
+
+
+def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True):
+    _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta)
+    B, H, W, C = z.shape
+    kh, kw, sh, sw = pool
+    nb = _lib.lib().ocrk_bn_bwd_workspace_size(B, H, W, C)
+    ws = _ws(nb, z.device)
+    dz = torch.empty_like(z)
+    call("ocrk_bn_relu_pool_bwd", ptr(z), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+         kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(ws), nb,
+         dtype_code(z.dtype), _stream(z))
+    return dz
+
+
+# ---------------------------------------------------------------- GEMM
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, out=None, out_dtype=torch.float32,
+         accumulate=False, alpha=1.0, M=None, N=None, K=None, lda=None, ldb=None, ldc=None,
+         batch=1, stride_a=0, stride_b=0, stride_c=0, splits=1):
+    """C = alpha op(A) op(B) (+bias) (relu) (+= C). A, B contiguous 2-D unless explicit
+    sizes/leading dimensions are given (then they may be strided views)."""
+    for t in (a, b, bias, out):
+        if t is not None and not t.is_cuda:
+            raise ValueError("libocrk ops take device tensors (got a CPU tensor)")
+    if M is None:
+        _chk(a, b)
+        M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+        N = b.shape[0] if trans_b else b.shape[1]
+        lda, ldb = a.shape[1], b.shape[1]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+        ldc = N
+    ldc = ldc if ldc is not None else N
+    if a.dtype != b.dtype:
+        raise TypeError("gemm operands must share a dtype")
+    kc = -(-(-(-K // splits)) // 32) * 32 if splits > 1 else K
+    splits = -(-K // kc) if splits > 1 else 1
+    nb = _lib.lib().ocrk_gemm_workspace_size(M, N, batch, splits) if splits > 1 else 0
+    ws = _ws(nb, a.device) if nb else None
+    call("ocrk_gemm", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(a), lda, stride_a, ptr(b), ldb,
+         stride_b, ptr(out), ldc, stride_c, dtype_code(out.dtype), ptr(bias), int(relu), int(accumulate),
+         batch, dtype_code(a.dtype), splits, ptr(ws), nb, _stream(a))
+    return out
+
+
+# ------------------------------------------------------------------ LSTM
+def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
+    _chk(gx, whT, seq_len)
+    dev = gx.device
+    h_state = torch.zeros(2, 2, B, H, dtype=dtype, device=dev)
+    c_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
+    out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+    hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+    cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
+    acts = torch.empty(T, B, 2, 4 * H, dtype=torch.float32, device=dev)
+    call("ocrk_lstm_fwd", ptr(gx), ptr(whT), ptr(h_state), ptr(c_state), ptr(seq_len), T, B, H, ptr(out),
+         ptr(hprev), ptr(cprev), ptr(acts), dtype_code(dtype), _stream(gx))
+    return out, hprev, cprev, acts
+
+
+def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
+    _chk(wh, seq_len, dout, cprev, acts)
+    dtype = dout.dtype
+    dev = dout.device
+    dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
+    dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
+    dG = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
+    call("ocrk_lstm_bwd", ptr(wh), ptr(dg_state), ptr(dc_state), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev),
+         ptr(acts), ptr(dG), dtype_code(dtype), _stream(dout))
+    return dG
+
+
+# ----------------------------------------------------------------- misc
+def cast(x, dtype, out=None):
+    _chk(x)
+    out = out if out is not None else torch.empty(x.shape, dtype=dtype, device=x.device)
+    call("ocrk_cast", ptr(x), dtype_code(x.dtype), ptr(out), dtype_code(out.dtype), x.numel(), _stream(x))
+    return out
+
+
+def permute3(x, d0, d1, d2, dtype, out=None):
+    _chk(x)
+    out = out if out is not None else torch.empty(d1, d0, d2, dtype=dtype, device=x.device)
+    call("ocrk_permute3", ptr(x), dtype_code(x.dtype), d0, d1, d2, ptr(out), dtype_code(out.dtype), _stream(x))
+    return out
+
+
+def strided_copy(src, rows, cols, in_rs, in_cs, out, out_rs, out_cs, out_offset=0, in_offset=0):
+    """out.flat[out_offset + r*out_rs + c*out_cs] = src.flat[in_offset + r*in_rs + c*in_cs]."""
+    _chk(src, out)
+    sp = ctypes_offset(src, in_offset)
+    op = ctypes_offset(out, out_offset)
+    call("ocrk_strided_copy", sp, rows, cols, in_rs, in_cs, op, dtype_code(out.dtype), out_rs, out_cs, _stream(src))
+
+
+def ctypes_offset(t, elems):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr() + elems * t.element_size())
+
+
+def colsum(x, M, N, out, accumulate=True):
+    _chk(x, out)
+    nb = _lib.lib().ocrk_colsum_workspace_size(M, N)
+    ws = _ws(nb, x.device)
+    call("ocrk_colsum", ptr(x), M, N, dtype_code(x.dtype), ptr(out), int(accumulate), ptr(ws), nb, _stream(x))
+
+
+def relu_mask(dy, y, out_dtype, scale=1.0):
+    _chk(dy, y)
+    out = torch.empty(dy.shape, dtype=out_dtype, device=dy.device)
+    call("ocrk_relu_mask", ptr(dy), ptr(y), dy.numel(), float(scale), ptr(out), dtype_code(out_dtype), _stream(dy))
+    return out
+
+
+def mul_scalar_(x, s):
+    _chk(x, s)
+    call("ocrk_mul_scalar", ptr(x), x.numel(), ptr(s), _stream(x))
+    return x
+
+
+def mean(x):
+    _chk(x)
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    call("ocrk_mean", ptr(x), x.numel(), ptr(out), _stream(x))
+    return out
+
+
+def adam_(p, g, m, v, lr_t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0):
+    _chk(p, g, m, v)
+    call("ocrk_adam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr_t), float(beta1), float(beta2),
+         float(eps), float(grad_scale), _stream(p))
+
+
+# ----------------------------------------------------------------------- CTC
+def ctc_loss(logits, labels, label_len, seq_len, grad_scale=1.0, need_grad=True, status=None):
+    """Per-sequence CTC loss (and grad_scale * dloss/dlogits).
+
+    logits f32 [T,B,C]; labels i32 [B,Lmax]; label_len, seq_len i32 [B].
+    Returns (loss [B], grad [T,B,C] or None, status i32 [B])."""
+    if logits.dtype != torch.float32:
+        raise TypeError("ctc_loss takes float32 logits")
+    _chk(logits, labels, label_len, seq_len)
+    T, B, C = logits.shape
+    Lmax = labels.shape[1] if labels.dim() == 2 else 0
+    labels = labels.reshape(B, Lmax)
+    if labels.numel() == 0:
+        labels = torch.zeros(B, 1, dtype=torch.int32, device=logits.device)
+        Lmax = 1
+    nb = _lib.lib().ocrk_ctc_workspace_size(T, B, Lmax)
+    ws = _ws(nb, logits.device)
+    loss = torch.empty(B, dtype=torch.float32, device=logits.device)
+    grad = torch.empty_like(logits) if need_grad else None
+    if status is None:
+        status = torch.empty(B, dtype=torch.int32, device=logits.device)
+    call("ocrk_ctc_loss", ptr(logits), ptr(labels), ptr(label_len), ptr(seq_len), T, B, C, Lmax,
+         float(grad_scale), ptr(loss), ptr(grad), ptr(status), ptr(ws), nb, _stream(logits))
+    return loss, grad, status
+
+
+def ctc_greedy_decode(logits, seq_len, merge_repeated=True):
+    """Greedy decode. Returns (out i64 [B,T] -1 padded, out_len i32 [B], neg_sum f32 [B])."""
+    if logits.dtype != torch.float32:
+        raise TypeError("ctc_greedy_decode takes float32 logits")
+    _chk(logits, seq_len)
+    T, B, C = logits.shape
+    out = torch.empty(B, T, dtype=torch.int64, device=logits.device)
+    out_len = torch.empty(B, dtype=torch.int32, device=logits.device)
+    neg = torch.empty(B, dtype=torch.float32, device=logits.device)
+    call("ocrk_ctc_greedy_decode", ptr(logits), ptr(seq_len), T, B, C, int(bool(merge_repeated)),
+         ptr(out), ptr(out_len), ptr(neg), _stream(logits))
+    return out, out_len, neg

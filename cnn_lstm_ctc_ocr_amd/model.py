@@ -1,0 +1,342 @@
+"""Drop-in for src/weinman/model.py: convnet_layers -> rnn_layers -> ctc_loss_layer.
+
+Same names, argument order and meaning as the reference graph builders, run
+eagerly on device tensors:
+
+    features, sequence_length = convnet_layers(inputs, widths, mode)   # model.py:126
+    logits = rnn_layers(features, sequence_length, num_classes)        # model.py:202
+    loss = ctc_loss_layer(logits, sequence_labels, sequence_length)    # model.py:224
+
+Variables live in a ParamStore (the TF graph's variables): pass `store=` or
+install a default with `use_store(...)`. Every op is a torch.autograd.Function
+whose forward and backward are libocrk HIP kernels; variable gradients are
+written straight into the store's flat gradient buffer (the buffer the
+all-reduce and the Adam kernel consume), so those Functions return None for
+the variable inputs.
+
+Structure of the launches (NHWC activations, compute dtype = store.cfg.dtype):
+  conv block k (k = 1..4) = conv_{2k-1} (+ReLU) -> conv_{2k} -> BN -> ReLU -> pool,
+  the last block writing features time-major; then per recurrent layer one
+  input-projection GEMM + T recurrent steps; then the logits GEMM (+ReLU);
+  then the CTC lattice.
+"""
+import contextlib
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .config import BN_EPS, BN_MOMENTUM, INFER, LAYER_PARAMS, POOLS, TRAIN, ModelConfig, rnn_size  # noqa: F401
+from .params import ParamStore
+
+layer_params = LAYER_PARAMS
+
+_DEFAULT = []
+
+
+@contextlib.contextmanager
+def use_store(store):
+    """Make `store` the implicit variable scope (TF get_variable analogue)."""
+    _DEFAULT.append(store)
+    try:
+        yield store
+    finally:
+        _DEFAULT.pop()
+
+
+def default_store():
+    if not _DEFAULT:
+        raise RuntimeError("no ParamStore: pass store= or wrap the calls in model.use_store(store)")
+    return _DEFAULT[-1]
+
+
+def _grad_enabled(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+# ------------------------------------------------------------------ convnet
+class _ConvBlock(torch.autograd.Function):
+    """conv_{2k-1} -> conv_{2k} -> BN -> ReLU -> pool (model.py:134-146)."""
+
+    @staticmethod
+    def forward(ctx, x, store, k, training, *variables):
+        dt = store.cfg.dtype
+        odd, even = f"conv{2 * k - 1}", f"conv{2 * k}"
+        P = store.params
+        pe = f"convnet/{even}"
+        if k == 1:
+            y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
+        else:
+            w_nk, _ = store.conv_images(odd, dt)
+            y_odd = K.conv3x3_fwd(x, w_nk, P[f"convnet/{odd}/bias"], relu=True)
+        B, H, W, _ = y_odd.shape
+        M = B * H * W
+        w_nk, _ = store.conv_images(even, dt)
+        C = w_nk.shape[0]
+        if training:
+            stats = torch.empty(K.conv_stats_tiles(M), 2, C, dtype=torch.float32, device=x.device)
+            z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False, stats=stats)
+            mean, invstd = K.bn_finalize(stats, M, C, BN_EPS, BN_MOMENTUM,
+                                         store.stats[pe + "/batch_norm/moving_mean"],
+                                         store.stats[pe + "/batch_norm/moving_variance"])
+        else:
+            z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False)
+            mean, invstd = K.bn_infer_params(store.stats[pe + "/batch_norm/moving_mean"],
+                                             store.stats[pe + "/batch_norm/moving_variance"], BN_EPS)
+        p = K.bn_relu_pool_fwd(z, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
+                               POOLS[even], time_major=(k == 4))
+        ctx.store, ctx.k = store, k
+        ctx.save_for_backward(x, y_odd, z, mean, invstd)
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        store, k = ctx.store, ctx.k
+        x, y_odd, z, mean, invstd = ctx.saved_tensors
+        dt = store.cfg.dtype
+        P, G = store.params, store.grads
+        odd, even = f"conv{2 * k - 1}", f"conv{2 * k}"
+        pe, po = f"convnet/{even}", f"convnet/{odd}"
+        dp = dp.contiguous()
+        if dp.dtype != dt:
+            dp = K.cast(dp, dt)
+        dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
+                                POOLS[even], dp_time_major=(k == 4),
+                                dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"])
+        B, H, W, C = dz.shape
+        K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
+        K.colsum(dz, B * H * W, C, G[pe + "/bias"])
+        _, w_bwd = store.conv_images(even, dt)
+        dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd)     # ReLU of conv_{2k-1} fused
+        dx = None
+        if k == 1:
+            K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
+        else:
+            Bo, Ho, Wo, Co = dy_odd.shape
+            K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
+            K.colsum(dy_odd, Bo * Ho * Wo, Co, G[po + "/bias"])
+            if ctx.needs_input_grad[0]:
+                _, w_bwd_odd = store.conv_images(odd, dt)
+                dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
+        return (dx, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
+
+
+def _block_variables(store, k):
+    names = [f"convnet/conv{2 * k - 1}/kernel", f"convnet/conv{2 * k - 1}/bias",
+             f"convnet/conv{2 * k}/kernel", f"convnet/conv{2 * k}/bias",
+             f"convnet/conv{2 * k}/batch_norm/gamma", f"convnet/conv{2 * k}/batch_norm/beta"]
+    return [store.params[n] for n in names]
+
+
+def convnet_layers(inputs, widths, mode, store=None):
+    """convnet_layers (src/weinman/model.py:126-165).
+
+    inputs: [B, 32, W, 1] -- uint8 pixels (validate._preprocess_image is then
+    fused into the first conv) or already preprocessed floats in the compute
+    dtype. widths: int [B] true image widths. mode: TRAIN or INFER.
+    Returns (features [B, T, 256] (a view of time-major storage), seq_len i32 [B])."""
+    store = store or default_store()
+    training = mode == TRAIN
+    x = inputs
+    if x.dim() == 4:
+        if x.shape[-1] != 1:
+            raise ValueError("inputs must be [batch, 32, width, 1]")
+        x = x[..., 0]
+    x = x.contiguous()
+    if x.dtype not in (torch.uint8, store.cfg.dtype):
+        x = K.cast(x, store.cfg.dtype)
+    track = torch.is_grad_enabled() and training
+    h = x
+    for k in (1, 2, 3, 4):
+        variables = _block_variables(store, k) if track else []
+        if track:
+            for v in variables:
+                v.requires_grad_(True)
+        h = _ConvBlock.apply(h, store, k, training, *variables)
+    if not isinstance(widths, torch.Tensor):
+        widths = torch.as_tensor(np.asarray(widths), dtype=torch.int32)
+    widths = widths.to(device=h.device, dtype=torch.int32)
+    sequence_length = K.seq_len(widths)
+    return h.transpose(0, 1), sequence_length
+
+
+# ---------------------------------------------------------------- recurrent
+class _BiLSTM(torch.autograd.Function):
+    """rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199)."""
+
+    @staticmethod
+    def forward(ctx, x, seq_len, store, layer, *variables):
+        dt = store.cfg.dtype
+        T, B, n_in = x.shape
+        H = store.cfg.rnn_sizes[layer - 1]
+        wxT, _wx, whT, _wh, bias = store.lstm_images(layer, dt)
+        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias)          # [T*B, 8H] f32
+        out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt)
+        ctx.store, ctx.layer, ctx.H = store, layer, H
+        ctx.save_for_backward(x, seq_len, hprev, cprev, acts)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        store, layer, H = ctx.store, ctx.layer, ctx.H
+        x, seq_len, hprev, cprev, acts = ctx.saved_tensors
+        dt = store.cfg.dtype
+        T, B, n_in = x.shape
+        G4 = 4 * H
+        dout = dout.contiguous()
+        if dout.dtype != dt:
+            dout = K.cast(dout, dt)
+        _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
+        dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H)               # [T,B,2,4H]
+        pre = f"rnn/bdrnn{layer}"
+        R = T * B
+        for d, dn in enumerate(("fw", "bw")):
+            gk = store.grads[f"{pre}/{dn}/lstm_cell/kernel"]                   # [In+H, 4H] f32
+            dgd = dG.view(R, 2 * G4)[:, d * G4:]                                 # view, ldb = 8H
+            # dW_x = x^T . dG_d ; dW_h = h_prev^T . dG_d  (split-K over T*B)
+            K.gemm(x, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
+                   ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R))
+            K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
+                   M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R))
+        K.colsum(dG, R, 2 * G4, store.flat_bias_pair_grad(layer))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
+        return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def _splits(M, N, Kdim):
+    tiles = -(-M // 128) * -(-N // 128)
+    return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
+
+
+class _Logits(torch.autograd.Function):
+    """tf.layers.dense(num_classes + 1, activation=relu) (model.py:216-220)."""
+
+    @staticmethod
+    def forward(ctx, x, store, *variables):
+        dt = store.cfg.dtype
+        T, B, D = x.shape
+        w = store.logits_image(dt)
+        logits = K.gemm(x.view(T * B, D), w, bias=store.params["rnn/logits/bias"], relu=True)
+        logits = logits.view(T, B, -1)
+        ctx.store = store
+        ctx.save_for_backward(x, logits)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        store = ctx.store
+        x, logits = ctx.saved_tensors
+        dt = store.cfg.dtype
+        T, B, D = x.shape
+        C = logits.shape[-1]
+        R = T * B
+        dpre = K.relu_mask(dlogits.contiguous(), logits, dt)                       # [T,B,C]
+        K.gemm(x, dpre, trans_a=True, out=store.grads["rnn/logits/kernel"], accumulate=True,
+               M=D, N=C, K=R, lda=D, ldb=C, ldc=C, splits=_splits(D, C, R))
+        K.colsum(dpre, R, C, store.grads["rnn/logits/bias"])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(dpre.view(R, C), store.logits_image(dt), trans_b=True, out_dtype=dt).view(T, B, D)
+        return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
+def rnn_layers(features, sequence_length, num_classes, store=None):
+    """rnn_layers (src/weinman/model.py:202-221): time-major transpose, two
+    bidirectional recurrent layers, dense + ReLU logits [T, B, num_classes+1]."""
+    store = store or default_store()
+    cfg = store.cfg
+    if num_classes != cfg.num_classes:
+        raise ValueError(f"store was built for {cfg.num_classes} classes, got {num_classes}")
+    if cfg.cell != "lstm":
+        raise NotImplementedError("GRU recurrent kernels are not in libocrk yet (cell='lstm', model_bu.py)")
+    x = features.transpose(0, 1)                                                  # model.py:212
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if x.dtype != cfg.dtype:
+        x = K.cast(x, cfg.dtype)
+    sequence_length = sequence_length.to(device=x.device, dtype=torch.int32).contiguous()
+    track = torch.is_grad_enabled() and x.requires_grad
+    for layer in range(1, len(cfg.rnn_sizes) + 1):
+        variables = []
+        if track:
+            pre = f"rnn/bdrnn{layer}"
+            variables = [store.params[f"{pre}/{d}/lstm_cell/{v}"] for d in ("fw", "bw") for v in ("kernel", "bias")]
+        x = _BiLSTM.apply(x, sequence_length, store, layer, *variables)
+    variables = [store.params["rnn/logits/kernel"], store.params["rnn/logits/bias"]] if track else []
+    return _Logits.apply(x, store, *variables)
+
+
+# ---------------------------------------------------------------------- CTC
+class _CTCLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, label_len, seq_len):
+        B = logits.shape[1]
+        loss_b, grad, status = K.ctc_loss(logits.contiguous(), labels, label_len, seq_len,
+                                          grad_scale=1.0 / max(B, 1), need_grad=logits.requires_grad)
+        ctx.save_for_backward(grad if grad is not None else loss_b)
+        ctx.status = status
+        return K.mean(loss_b)                                                      # model.py:228
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return K.mul_scalar_(grad, g.to(torch.float32).contiguous()), None, None, None
+
+
+def dense_labels(sequence_labels, batch, device):
+    """SparseTensor-like labels -> (dense int32 [B, Lmax], lengths int32 [B]).
+
+    Accepts a list of label sequences, a (indices [N,2], values [N], dense_shape)
+    triple as produced by the reference input pipeline (mjsynth.py:71-72), or an
+    already dense (labels [B, Lmax], label_len [B]) pair of tensors."""
+    if isinstance(sequence_labels, (tuple, list)) and len(sequence_labels) == 2 and \
+            isinstance(sequence_labels[0], torch.Tensor):
+        lab, ln = sequence_labels
+        return lab.to(device=device, dtype=torch.int32).contiguous(), ln.to(device=device, dtype=torch.int32)
+    if isinstance(sequence_labels, (tuple, list)) and len(sequence_labels) == 3 and \
+            np.asarray(sequence_labels[0]).ndim == 2:
+        idx, vals, shape = (np.asarray(a) for a in sequence_labels)
+        seqs = [[] for _ in range(int(shape[0]))]
+        for (b, _t), v in sorted(zip(map(tuple, idx), vals)):
+            seqs[int(b)].append(int(v))
+    else:
+        seqs = [list(map(int, s)) for s in sequence_labels]
+    if len(seqs) != batch:
+        raise ValueError(f"{len(seqs)} label sequences for a batch of {batch}")
+    lmax = max([len(s) for s in seqs] + [1])
+    dense = np.zeros((batch, lmax), np.int32)
+    for i, s in enumerate(seqs):
+        dense[i, :len(s)] = s
+    lens = np.array([len(s) for s in seqs], np.int32)
+    return torch.from_numpy(dense).to(device), torch.from_numpy(lens).to(device)
+
+
+def check_feasible(sequence_labels_dense, label_len, seq_len):
+    """[TF1] InvalidArgumentError when a label needs more frames than its
+    sequence has (L + repeats > seq_len). Host check (one small D2H copy)."""
+    lab = sequence_labels_dense.cpu().numpy()
+    ln = label_len.cpu().numpy()
+    sl = seq_len.cpu().numpy()
+    for b in range(lab.shape[0]):
+        l = lab[b, :ln[b]]
+        need = len(l) + int(np.sum(l[1:] == l[:-1]))
+        if need > sl[b]:
+            from ._lib import InvalidArgumentError
+            raise InvalidArgumentError(3, f"Not enough time for target transition sequence "
+                                          f"(required: {need}, available: {sl[b]}), batch {b}")
+
+
+def ctc_loss_layer(rnn_logits, sequence_labels, sequence_length, check=False):
+    """ctc_loss_layer (src/weinman/model.py:224-229): mean over the batch of
+    tf.nn.ctc_loss(labels, logits, seq_len, time_major=True)."""
+    T, B, _ = rnn_logits.shape
+    lab, ln = dense_labels(sequence_labels, B, rnn_logits.device)
+    if check:
+        check_feasible(lab, ln, sequence_length)
+    return _CTCLoss.apply(rnn_logits, lab, ln, sequence_length.to(torch.int32).contiguous())
+
+
+__all__ = ["convnet_layers", "rnn_layers", "ctc_loss_layer", "layer_params", "rnn_size", "TRAIN", "INFER",
+           "ParamStore", "ModelConfig", "use_store", "default_store", "dense_labels", "check_feasible"]

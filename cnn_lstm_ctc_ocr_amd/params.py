@@ -1,0 +1,215 @@
+"""Parameter store: every variable of the reference graph in ONE flat fp32
+buffer in HBM (plus a flat gradient buffer and a flat buffer of BatchNorm
+moving statistics), addressed by the TF1 variable names of
+src/weinman/model.py / model_bu.py (`convnet/conv3/kernel`,
+`rnn/bdrnn1/fw/lstm_cell/kernel`, `rnn/logits/bias`, ...).
+
+One buffer means one all-reduce and one Adam launch per step; the per-name
+tensors are views. The compute-dtype weight images the kernels read (GEMM
+layouts, bf16 casts) are derived from the master copy once per parameter
+version (see `images()`).
+"""
+import numpy as np
+import torch
+
+from . import kernels as K
+from .config import LAYER_PARAMS, ModelConfig
+
+_ALIGN = 64  # elements (256 B): every view starts 16-B aligned for vector loads
+
+
+def param_shapes(cfg):
+    """(name, shape, trainable) in buffer order. Forward and backward
+    direction biases of one recurrent layer sit next to each other so one
+    column-sum kernel writes both."""
+    out = []
+    cin = 1
+    for filters, k, _pad, name, bn in LAYER_PARAMS:
+        out.append((f"convnet/{name}/kernel", (k, k, cin, filters), True))
+        out.append((f"convnet/{name}/bias", (filters,), True))
+        if bn:
+            out.append((f"convnet/{name}/batch_norm/gamma", (filters,), True))
+            out.append((f"convnet/{name}/batch_norm/beta", (filters,), True))
+            out.append((f"convnet/{name}/batch_norm/moving_mean", (filters,), False))
+            out.append((f"convnet/{name}/batch_norm/moving_variance", (filters,), False))
+        cin = filters
+    n_in = cin
+    for li, H in enumerate(cfg.rnn_sizes, start=1):
+        pre = f"rnn/bdrnn{li}"
+        if cfg.cell == "lstm":
+            for d in ("fw", "bw"):
+                out.append((f"{pre}/{d}/lstm_cell/kernel", (n_in + H, 4 * H), True))
+            for d in ("fw", "bw"):
+                out.append((f"{pre}/{d}/lstm_cell/bias", (4 * H,), True))
+        else:
+            for d in ("fw", "bw"):
+                out.append((f"{pre}/{d}/gru_cell/gates/kernel", (n_in + H, 2 * H), True))
+                out.append((f"{pre}/{d}/gru_cell/gates/bias", (2 * H,), True))
+                out.append((f"{pre}/{d}/gru_cell/candidate/kernel", (n_in + H, H), True))
+                out.append((f"{pre}/{d}/gru_cell/candidate/bias", (H,), True))
+        n_in = 2 * H
+    out.append(("rnn/logits/kernel", (n_in, cfg.num_classes + 1), True))
+    out.append(("rnn/logits/bias", (cfg.num_classes + 1,), True))
+    return out
+
+
+def _trunc_normal(rng, shape, std):
+    """[TF1] truncated_normal: redraw values beyond two standard deviations."""
+    x = rng.standard_normal(shape)
+    bad = np.abs(x) > 2
+    while bad.any():
+        x[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(x) > 2
+    return x * std
+
+
+def reference_init(cfg, seed=0):
+    """Initial values with the reference's initialisers (numpy, host):
+    conv + logits kernels: contrib variance_scaling_initializer() -> truncated
+    normal, std sqrt(1.3*2/fan_in) (model.py:94, :207); biases 0; BN gamma 1,
+    beta 0, moving mean 0 / variance 1; LSTM kernels truncated normal 0.01,
+    bias 0 (model_bu.py:170-180); GRU kernels and biases truncated normal 0.01
+    (model.py:170-180)."""
+    rng = np.random.default_rng(seed)
+    vals = {}
+    for name, shape, _tr in param_shapes(cfg):
+        leaf = name.rsplit("/", 1)[1]
+        if name.startswith("convnet") and leaf == "kernel":
+            v = _trunc_normal(rng, shape, np.sqrt(2.6 / (shape[0] * shape[1] * shape[2])))
+        elif name == "rnn/logits/kernel":
+            v = _trunc_normal(rng, shape, np.sqrt(2.6 / shape[0]))
+        elif "gru_cell" in name or ("lstm_cell" in name and leaf == "kernel"):
+            v = _trunc_normal(rng, shape, 0.01)
+        elif leaf in ("gamma", "moving_variance"):
+            v = np.ones(shape)
+        else:
+            v = np.zeros(shape)
+        vals[name] = v.astype(np.float32)
+    return vals
+
+
+class ParamStore:
+    def __init__(self, cfg=None, device="cuda", seed=0, values=None):
+        self.cfg = cfg or ModelConfig()
+        self.device = torch.device(device)
+        self.spec = param_shapes(self.cfg)
+        self.offsets = {}
+        sizes = {True: 0, False: 0}
+        for name, shape, tr in self.spec:
+            n = int(np.prod(shape))
+            self.offsets[name] = (tr, sizes[tr], shape)
+            sizes[tr] += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.n_trainable = sum(int(np.prod(s)) for _, s, tr in self.spec if tr)
+        self.flat = torch.zeros(sizes[True], dtype=torch.float32, device=self.device)
+        self.flat_grad = torch.zeros_like(self.flat)
+        self.flat_stats = torch.zeros(max(sizes[False], _ALIGN), dtype=torch.float32, device=self.device)
+        self.params, self.grads, self.stats = {}, {}, {}
+        for name, shape, tr in self.spec:
+            _, off, _ = self.offsets[name]
+            n = int(np.prod(shape))
+            if tr:
+                self.params[name] = self.flat[off:off + n].view(shape)
+                self.grads[name] = self.flat_grad[off:off + n].view(shape)
+            else:
+                self.stats[name] = self.flat_stats[off:off + n].view(shape)
+        self.version = 0
+        self._images = {}
+        self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
+
+    # ------------------------------------------------------------ state
+    def state_dict(self):
+        """name -> host numpy array (trainable variables and BN moving stats)."""
+        out = {k: v.detach().cpu().numpy().copy() for k, v in self.params.items()}
+        out.update({k: v.detach().cpu().numpy().copy() for k, v in self.stats.items()})
+        return out
+
+    def load_state_dict(self, values):
+        for name, _shape, _tr in self.spec:
+            if name not in values:
+                raise KeyError(f"missing variable {name}")
+            dst = self.params.get(name, self.stats.get(name))
+            src = torch.as_tensor(np.asarray(values[name], dtype=np.float32))
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f"{name}: shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            dst.copy_(src.to(self.device))
+        self.bump()
+
+    def save(self, path):
+        np.savez(path, **{k.replace("/", "__"): v for k, v in self.state_dict().items()})
+
+    def load(self, path):
+        with np.load(path, allow_pickle=False) as z:
+            self.load_state_dict({k.replace("__", "/"): z[k] for k in z.files})
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+
+    def bump(self):
+        """The master values changed: derived weight images are stale."""
+        self.version += 1
+        self._images.clear()
+
+    # ---------------------------------------------------- weight images
+    def images(self, key, builder):
+        """Cache of compute-dtype weight layouts, rebuilt once per version."""
+        img = self._images.get(key)
+        if img is None:
+            img = builder()
+            self._images[key] = img
+        return img
+
+    def conv_images(self, name, dtype):
+        """conv2..8: w_nk [Cout][3][3][Cin] (forward), w_bwd [Cin][3][3][Cout]."""
+        def build():
+            w = self.params[f"convnet/{name}/kernel"]
+            kh, kw, cin, cout = w.shape
+            w_nk = K.permute3(w, kh * kw * cin, cout, 1, dtype).view(cout, kh * kw * cin)
+            w_bwd = K.permute3(w, kh * kw, cin, cout, dtype).view(cin, kh * kw * cout)
+            return w_nk, w_bwd
+        return self.images(("conv", name, dtype), build)
+
+    def lstm_images(self, layer, dtype):
+        """Recurrent layer `layer` (1-based): WxT_cat [8H][In], Wx_cat [In][8H],
+        whT [2][4H][H], wh [2][H][4H] in dtype, bias_cat f32 [8H]."""
+        def build():
+            pre = f"rnn/bdrnn{layer}"
+            kf = self.params[f"{pre}/fw/lstm_cell/kernel"]
+            rows, G = kf.shape
+            H = G // 4
+            n_in = rows - H
+            dev = kf.device
+            wxT = torch.empty(2 * G, n_in, dtype=dtype, device=dev)
+            wx = torch.empty(n_in, 2 * G, dtype=dtype, device=dev)
+            whT = torch.empty(2, G, H, dtype=dtype, device=dev)
+            wh = torch.empty(2, H, G, dtype=dtype, device=dev)
+            for d, dn in enumerate(("fw", "bw")):
+                k = self.params[f"{pre}/{dn}/lstm_cell/kernel"]
+                K.strided_copy(k, n_in, G, G, 1, wxT, 1, n_in, out_offset=d * G * n_in)
+                K.strided_copy(k, n_in, G, G, 1, wx, 2 * G, 1, out_offset=d * G)
+                K.strided_copy(k, H, G, G, 1, whT, 1, H, out_offset=d * G * H, in_offset=n_in * G)
+                K.strided_copy(k, H, G, G, 1, wh, G, 1, out_offset=d * H * G, in_offset=n_in * G)
+            bias = self.flat_bias_pair(layer)
+            return wxT, wx, whT, wh, bias
+        return self.images(("lstm", layer, dtype), build)
+
+    def flat_bias_pair(self, layer):
+        """[8H] view over the adjacent fw/bw LSTM biases of `layer`."""
+        pre = f"rnn/bdrnn{layer}"
+        bf = self.params[f"{pre}/fw/lstm_cell/bias"]
+        _, off, _ = self.offsets[f"{pre}/fw/lstm_cell/bias"]
+        _, off2, _ = self.offsets[f"{pre}/bw/lstm_cell/bias"]
+        n = bf.numel()
+        if off2 != off + n:
+            raise RuntimeError("LSTM biases must be adjacent in the flat buffer")
+        return self.flat[off:off + 2 * n]
+
+    def flat_bias_pair_grad(self, layer):
+        pre = f"rnn/bdrnn{layer}"
+        _, off, _ = self.offsets[f"{pre}/fw/lstm_cell/bias"]
+        n = self.params[f"{pre}/fw/lstm_cell/bias"].numel()
+        return self.flat_grad[off:off + 2 * n]
+
+    def logits_image(self, dtype):
+        def build():
+            return K.cast(self.params["rnn/logits/kernel"].contiguous(), dtype)
+        return self.images(("logits", dtype), build)

@@ -49,6 +49,140 @@ const char* ocrk_last_error(void);
  * out[i] = float32(in[i]) * float32(1/255) - 0.5, n elements. */
 int ocrk_preprocess(const uint8_t* in, int64_t n, void* out, int dtype, void* stream);
 
+/* a9 -- ctc_loss_layer (src/weinman/model.py:224-229) = tf.nn.ctc_loss(labels,
+ * logits, seq_len, time_major=True), preprocess_collapse_repeated=False,
+ * ctc_merge_repeated=True, blank = C-1, softmax taken inside.
+ *   logits  f32 [T, B, C]           labels   i32 [B, max_label_len] (dense, padded)
+ *   label_len i32 [B]               seq_len  i32 [B] (frames used per sequence)
+ *   loss    f32 [B]  (-log p; +inf and status[b]=1 when infeasible)
+ *   grad    f32 [T, B, C] or NULL: grad_scale * d loss_b / d logits (0 for t >= seq_len)
+ *   status  i32 [B] or NULL        ws: >= ocrk_ctc_workspace_size(T, B, max_label_len) bytes */
+size_t ocrk_ctc_workspace_size(int T, int B, int max_label_len);
+int ocrk_ctc_loss(const float* logits, const int* labels, const int* label_len, const int* seq_len,
+                  int T, int B, int C, int max_label_len, float grad_scale, float* loss, float* grad,
+                  int* status, void* ws, size_t ws_bytes, void* stream);
+
+/* a10 -- validate._get_output (src/weinman/validate.py:81-92) =
+ * tf.nn.ctc_greedy_decoder(logits, seq_len, merge_repeated) + sparse_to_dense(-1):
+ *   out i64 [B, T] (labels then -1), out_len i32 [B], neg_sum_logits f32 [B] or NULL. */
+int ocrk_ctc_greedy_decode(const float* logits, const int* seq_len, int T, int B, int C,
+                           int merge_repeated, int64_t* out, int* out_len, float* neg_sum_logits,
+                           void* stream);
+
+
+/* ------------------------------------------------------------- conv tower
+ * a1+a2 conv1 -- conv_layer(layer_params[0]) (src/weinman/model.py:84-109,134):
+ * 3x3 'valid', Cin = 1, bias + ReLU, fused with the uint8 preprocess of
+ * validate._preprocess_image when x_is_u8 (x: u8 or dtype [B,H,W]); w f32 HWIO
+ * [3][3][1][cout], bias f32 [cout]; y dtype [B,H-2,W-2,cout]. */
+int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, const float* w, const float* bias,
+                   int cout, void* y, int dtype, void* stream);
+/* conv1 weight/bias gradient from dz = dL/d(pre-ReLU conv1), f32 outputs. */
+size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
+int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,
+                          float* dw, float* db, int accumulate, void* ws, size_t ws_bytes, int dtype,
+                          void* stream);
+
+/* a2 conv2..conv8 -- conv_layer (model.py:84-109) with 'same' padding as an
+ * implicit GEMM on MFMA. x [B,H,W,cin]; w_nk [cout][3][3][cin] (dtype);
+ * y [B,H,W,cout] in y_dtype; bias f32 or NULL; relu 0/1. stats (or NULL):
+ * [ocrk_conv_stats_tiles(B*H*W)][2][cout] per-tile (sum, M2) of the output,
+ * the BatchNorm statistics input of ocrk_bn_finalize. */
+size_t ocrk_conv_stats_tiles(int64_t M);
+int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias,
+                     int cout, void* y, int y_dtype, int relu, float* stats, int dtype, void* stream);
+/* dx [B,H,W,cin] = conv3x3 backward-data of dy [B,H,W,cout] with w_bwd
+ * [cin][3][3][cout]; if relu_mask != NULL, dx *= (relu_mask > 0) (the ReLU of
+ * the layer that produced x). */
+int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
+                          void* dx, const void* relu_mask, int dtype, void* stream);
+/* dw f32 HWIO [3][3][cin][cout] (+)= im2col(x)^T . dy (split-K). */
+size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin, int cout);
+int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, int cin, int cout,
+                            float* dw, int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
+
+/* a3+a4 -- norm_layer (model.py:118-123) + ReLU (:107) + pool_layer / pool8
+ * (:111-116, :145-146). bn_finalize: TRAIN-mode batch statistics from the conv
+ * epilogue partials (mean, 1/sqrt(var+eps)) and the [TF1] moving averages
+ * (moving_mean/var may be NULL = no update). bn_infer_params: INFER mode. */
+int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
+                     float* mean, float* invstd, float* moving_mean, float* moving_var, void* stream);
+int ocrk_bn_infer_params(const float* moving_mean, const float* moving_var, int C, float eps,
+                         float* mean, float* invstd, void* stream);
+/* out = maxpool(relu(gamma (z-mean) invstd + beta)), window kh x kw, stride
+ * sh x sw, 'valid'. time_major (requires Ho == 1): out is [Wo, B, C], the
+ * features tensor of model.py:147 already transposed as at model.py:212. */
+int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, int kh, int kw,
+                          int sh, int sw, void* out, int time_major, int dtype, void* stream);
+/* Backward of the above: dz [B,H,W,C] from dp (pooled gradient, time-major if
+ * dp_time_major); dgamma/dbeta f32 (accumulate 0/1). */
+size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C);
+int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, int kh, int kw,
+                          int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
+                          int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
+
+/* ------------------------------------------------------------- recurrent
+ * a7' -- rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199), both
+ * directions, one launch per time step. Layouts (time order, d = direction):
+ *   gx      f32 [T][B][2][4H]  = x . W_x + b  (ocrk_gemm, N = 8H)
+ *   whT     dtype [2][4H][H]   (recurrent kernel rows of [In+H][4H], transposed)
+ *   wh      dtype [2][H][4H]   (recurrent kernel rows as stored)
+ *   h_state dtype [2 bufs][2][B][H], c_state f32 [2][B][H] (zero before s = 0)
+ *   out     dtype [T][B][2H]   (layer output, must be zeroed: t >= len stays 0)
+ *   hprev_t dtype [T][B][2][H], cprev_t f32 [T][B][2][H], acts_t f32 [T][B][2][4H]
+ *   dout    dtype [T][B][2H]   dG_t dtype [T][B][2][4H]
+ *   dg_state dtype [2 bufs][2][B][4H], dc_state f32 [2][B][H] (zero before the loop) */
+int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void* h_out, float* c_state,
+                       const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t,
+                       float* cprev_t, float* acts_t, int dtype, void* stream);
+int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* dc_state, const int* seq_len,
+                       int s, int T, int B, int H, const void* dout, const float* cprev_t,
+                       const float* acts_t, void* dG_t, int dtype, void* stream);
+int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
+                  int T, int B, int H, void* out, void* hprev_t, float* cprev_t, float* acts_t, int dtype,
+                  void* stream);
+int ocrk_lstm_bwd(const void* wh, void* dg_state, float* dc_state, const int* seq_len, int T, int B, int H,
+                  const void* dout, const float* cprev_t, const float* acts_t, void* dG_t, int dtype,
+                  void* stream);
+
+/* ------------------------------------------------------- dense / generic
+ * MFMA GEMM: C[b] = alpha op(A[b]) op(B[b]) + bias (ReLU) (+= C if accumulate).
+ * trans_a: 0 A=[M][K] (lda), 1 A=[K][M]; trans_b: 0 B=[K][N] (ldb), 1 B=[N][K].
+ * A/B in dtype, C in c_dtype (accumulate needs f32). Used for the recurrent
+ * input projections (model.py:187-192), the logits layer (model.py:216-220)
+ * and their gradients. splits > 1 = split-K through ws. */
+size_t ocrk_gemm_workspace_size(int M, int N, int batch, int splits);
+int ocrk_gemm(int trans_a, int trans_b, int M, int N, int K, float alpha, const void* A, int64_t lda,
+              int64_t stride_a, const void* B, int64_t ldb, int64_t stride_b, void* C, int64_t ldc,
+              int64_t stride_c, int c_dtype, const float* bias, int relu, int accumulate, int batch,
+              int dtype, int splits, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- train op
+ * a13 -- Adam of train.py:128-137 ([TF1] ApplyAdam) on a flat f32 buffer;
+ * lr_t = lr sqrt(1-b2^t)/(1-b1^t) computed by the caller; g is scaled by
+ * grad_scale (e.g. 1/world_size after a summing all-reduce). */
+int ocrk_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_t, float beta1,
+              float beta2, float eps, float grad_scale, void* stream);
+
+/* -------------------------------------------------------------- utilities */
+int ocrk_cast(const void* in, int in_dtype, void* out, int out_dtype, int64_t n, void* stream);
+int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d2, void* out, int out_dtype,
+                  void* stream);  /* out[i1][i0][i2] = in[i0][i1][i2] */
+int ocrk_strided_copy(const float* in, int64_t rows, int64_t cols, int64_t in_rs, int64_t in_cs, void* out,
+                      int out_dtype, int64_t out_rs, int64_t out_cs, void* stream);
+size_t ocrk_colsum_workspace_size(int64_t M, int N);
+int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
+                size_t ws_bytes, void* stream);
+/* out = (y > 0) ? dy * scale : 0 (ReLU backward of the logits, model.py:216) */
+int ocrk_relu_mask(const float* dy, const float* y, int64_t n, float scale, void* out, int out_dtype,
+                   void* stream);
+int ocrk_mul_scalar(float* x, int64_t n, const float* s, void* stream);
+int ocrk_mean(const float* x, int n, float* out, void* stream);
+/* model.py:152-163: seq_len = floor((width - 2) / 2) - 2 */
+int ocrk_seq_len(const int* widths, int n, int* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

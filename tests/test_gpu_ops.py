@@ -1,0 +1,201 @@
+"""Per-op parity of the HIP kernels against the oracle / numpy (fp32 within
+float tolerances; index work bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_graph as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    return t.to(dtype) if dtype is not None else t
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+# --------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(200, 96, 160), (64, 512, 1000), (296, 40, 72)])
+def test_gemm_modes(cuda, dtype, ta, tb, M, N, K):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    if dtype == torch.bfloat16:   # compare against the bf16-rounded operands
+        A = torch.from_numpy(A).bfloat16().float().numpy()
+        B = torch.from_numpy(B).bfloat16().float().numpy()
+    ref = (A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64) + bias
+    out = Kn.gemm(_t(A, cuda, dtype), _t(B, cuda, dtype), trans_a=ta, trans_b=tb, bias=_t(bias, cuda))
+    assert _rel(out.cpu().numpy(), ref) < 2e-6
+    out = Kn.gemm(_t(A, cuda, dtype), _t(B, cuda, dtype), trans_a=ta, trans_b=tb, bias=_t(bias, cuda), relu=True,
+                  splits=3)
+    assert _rel(out.cpu().numpy(), np.maximum(ref, 0)) < 2e-6
+
+
+def test_gemm_accumulate_and_bf16_out(cuda):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((128, 64)).astype(np.float32)
+    B = rng.standard_normal((64, 32)).astype(np.float32)
+    C = rng.standard_normal((128, 32)).astype(np.float32)
+    c = _t(C, cuda)
+    Kn.gemm(_t(A, cuda), _t(B, cuda), out=c, accumulate=True)
+    np.testing.assert_allclose(c.cpu().numpy(), C + A @ B, rtol=1e-5, atol=1e-5)
+    ob = Kn.gemm(_t(A, cuda), _t(B, cuda), out_dtype=torch.bfloat16)
+    np.testing.assert_allclose(ob.float().cpu().numpy(), A @ B, rtol=1e-2, atol=1e-2)
+
+
+# --------------------------------------------------------------------- conv
+def test_conv1_fwd_and_wgrad(cuda):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (3, 32, 40)).astype(np.uint8)
+    w = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
+    b = rng.standard_normal(32).astype(np.float32)
+    x = G.preprocess(img)[..., None]
+    ref = G.relu(G.conv2d(x, w, b, "valid"))
+    y = Kn.conv1_fwd(_t(img, cuda), _t(w, cuda), _t(b, cuda), torch.float32)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    dz = rng.standard_normal(ref.shape).astype(np.float32)
+    _, dw_ref, db_ref = G.conv2d_bwd(x, w, dz, "valid", need_dx=False)
+    dw = torch.zeros(3, 3, 1, 32, device=cuda)
+    db = torch.zeros(32, device=cuda)
+    Kn.conv1_bwd_weight(_t(img, cuda), _t(dz, cuda), dw, db, accumulate=False)
+    np.testing.assert_allclose(dw.cpu().numpy(), dw_ref, rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(db.cpu().numpy(), db_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,cout,relu", [(32, 32, False), (64, 128, True), (256, 256, False)])
+def test_conv3x3_fwd_bwd(cuda, cin, cout, relu):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(cin + cout)
+    x = rng.standard_normal((2, 5, 13, cin)).astype(np.float32)
+    w = (rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    z = G.conv2d(x, w, b, "same")
+    ref = G.relu(z) if relu else z
+    w_nk = Kn.permute3(_t(w, cuda), 9 * cin, cout, 1, torch.float32).view(cout, 9 * cin)
+    w_bwd = Kn.permute3(_t(w, cuda), 9, cin, cout, torch.float32).view(cin, 9 * cout)
+    M = 2 * 5 * 13
+    stats = torch.empty(Kn.conv_stats_tiles(M), 2, cout, device=cuda)
+    y = Kn.conv3x3_fwd(_t(x, cuda), w_nk, _t(b, cuda), relu, stats=stats)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
+    mean, invstd = Kn.bn_finalize(stats, M, cout, 1e-3, 0.99)
+    np.testing.assert_allclose(mean.cpu().numpy(), ref.reshape(-1, cout).mean(0), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(invstd.cpu().numpy(), 1 / np.sqrt(ref.reshape(-1, cout).var(0) + 1e-3), rtol=1e-4)
+    dy = rng.standard_normal(z.shape).astype(np.float32)
+    dx_ref, dw_ref, _ = G.conv2d_bwd(x, w, dy, "same")
+    mask = rng.standard_normal(x.shape).astype(np.float32)
+    dx = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd, relu_mask=_t(mask, cuda))
+    np.testing.assert_allclose(dx.cpu().numpy(), dx_ref * (mask > 0), rtol=1e-4, atol=1e-4)
+    dw = torch.zeros(3, 3, cin, cout, device=cuda)
+    Kn.conv3x3_bwd_weight(_t(x, cuda), _t(dy, cuda), dw, accumulate=False)
+    np.testing.assert_allclose(dw.cpu().numpy(), dw_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("pool", [(2, 2, 2, 2), (2, 2, 2, 1), (3, 1, 3, 1)])
+def test_bn_relu_pool(cuda, pool):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(sum(pool))
+    B, H, W, C = 2, 7 if pool[0] == 2 else 3, 11, 32
+    z = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    gamma = rng.standard_normal(C).astype(np.float32)
+    beta = rng.standard_normal(C).astype(np.float32)
+    a, mean, var, var_u, cache = G.bn_train(z, gamma, beta)
+    y = G.relu(a)
+    p_ref = G.maxpool(y, *pool)
+    mean_d = _t(mean, cuda)
+    inv_d = _t((1 / np.sqrt(var.astype(np.float64) + 1e-3)).astype(np.float32), cuda)
+    tm = pool == (3, 1, 3, 1)
+    p = Kn.bn_relu_pool_fwd(_t(z, cuda), mean_d, inv_d, _t(gamma, cuda), _t(beta, cuda), pool, time_major=tm)
+    p = p.cpu().numpy()
+    if tm:
+        p = p.transpose(1, 0, 2)[:, None]
+    np.testing.assert_allclose(p, p_ref, rtol=1e-5, atol=1e-5)
+    dp = rng.standard_normal(p_ref.shape).astype(np.float32)
+    dy = G.maxpool_bwd(y, dp, *pool)
+    dz_ref, dg_ref, db_ref = G.bn_bwd(G.relu_bwd(y, dy), cache, gamma)
+    dg = torch.zeros(C, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    dp_d = _t(dp[:, 0].transpose(1, 0, 2) if tm else dp, cuda)
+    dz = Kn.bn_relu_pool_bwd(_t(z, cuda), dp_d, mean_d, inv_d, _t(gamma, cuda), _t(beta, cuda), pool, tm, dg, db,
+                             accumulate=False)
+    np.testing.assert_allclose(dz.cpu().numpy(), dz_ref, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(dg.cpu().numpy(), dg_ref, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(db.cpu().numpy(), db_ref, rtol=1e-4, atol=1e-5)
+
+
+# --------------------------------------------------------------------- LSTM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_lstm_layer_fwd_bwd(cuda, dtype):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(5)
+    T, B, n_in, H = 9, 64, 64, 128
+    x = rng.standard_normal((T, B, n_in)).astype(np.float32)
+    seq = rng.integers(1, T + 1, B).astype(np.int32)
+    seq[0] = T
+    ks = [(rng.standard_normal((n_in + H, 4 * H)) * 0.2).astype(np.float32) for _ in range(2)]
+    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
+    if dtype == torch.bfloat16:
+        x = torch.from_numpy(x).bfloat16().float().numpy()
+        ks = [torch.from_numpy(k).bfloat16().float().numpy() for k in ks]
+    outs, caches = [], []
+    for d, rev in enumerate((False, True)):
+        o, c = G.lstm_dir_fwd(x, seq, ks[d], bs[d], rev)
+        outs.append(o)
+        caches.append(c)
+    ref = np.concatenate(outs, axis=2)
+    # device images, as ParamStore.lstm_images builds them
+    G4 = 4 * H
+    wxT = np.concatenate([k[:n_in].T for k in ks], 0)              # [8H][In]
+    wx = np.concatenate([k[:n_in] for k in ks], 1)                 # [In][8H]
+    whT = np.stack([k[n_in:].T for k in ks])                       # [2][4H][H]
+    wh = np.stack([k[n_in:] for k in ks])                          # [2][H][4H]
+    bias = np.concatenate(bs)
+    seq_d = _t(seq, cuda)
+    gx = Kn.gemm(_t(x.reshape(T * B, n_in), cuda, dtype), _t(wxT, cuda, dtype), trans_b=True, bias=_t(bias, cuda))
+    out, hprev, cprev, acts = Kn.lstm_fwd(gx, _t(whT, cuda, dtype), seq_d, T, B, H, dtype)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(out.float().cpu().numpy(), ref) < tol
+    dout = rng.standard_normal(ref.shape).astype(np.float32)
+    if dtype == torch.bfloat16:
+        dout = torch.from_numpy(dout).bfloat16().float().numpy()
+    dG = Kn.lstm_bwd(_t(wh, cuda, dtype), seq_d, _t(dout, cuda, dtype), cprev, acts, T, B, H)
+    dx_dev = Kn.gemm(dG.view(T * B, 2 * G4), _t(wx, cuda, dtype), trans_b=True).view(T, B, n_in)
+    dxr = np.zeros_like(x)
+    for d in range(2):
+        ddx, dk, db = G.lstm_dir_bwd(np.ascontiguousarray(dout[:, :, d * H:(d + 1) * H]), caches[d], ks[d], n_in)
+        dxr += ddx
+        dgd = dG.view(T * B, 2 * G4)[:, d * G4:]
+        gk = torch.zeros(n_in + H, G4, device=cuda)
+        Kn.gemm(_t(x, cuda, dtype), dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=T * B, lda=n_in,
+                ldb=2 * G4, ldc=G4)
+        Kn.gemm(hprev.view(T * B, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True, M=H, N=G4,
+                K=T * B, lda=2 * H, ldb=2 * G4, ldc=G4, splits=2)
+        assert _rel(gk.cpu().numpy(), dk) < (1e-4 if dtype == torch.float32 else 5e-2)
+    assert _rel(dx_dev.cpu().numpy(), dxr) < (1e-4 if dtype == torch.float32 else 5e-2)
+
+
+def test_adam_matches_oracle(cuda):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(2)
+    n = 1000
+    p, g = rng.standard_normal(n).astype(np.float32), rng.standard_normal(n).astype(np.float32)
+    m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    pd, gd, md, vd = _t(p, cuda), _t(g, cuda), _t(m, cuda), _t(v, cuda)
+    for t in (1, 2, 3):
+        lr = G.learning_rate(t - 1)
+        p, m, v = G.adam_update(p, g, m, v, lr, t)
+        lr_t = lr * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        Kn.adam_(pd, gd, md, vd, lr_t)
+    np.testing.assert_allclose(pd.cpu().numpy(), p, rtol=1e-6, atol=1e-7)
+    # the device forms (1 - beta2) in float32 like TF's ApplyAdam (0.00099998713 vs 0.001)
+    np.testing.assert_allclose(vd.cpu().numpy(), v, rtol=3e-5, atol=1e-9)
