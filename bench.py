@@ -1,0 +1,207 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): line-crops/sec per TRAIN STEP at
+32x256, batch 256 per GPU, CNN -> BiLSTM(512, 512) -> CTC (src/weinman/model_bu.py),
+bf16 compute, Adam update included -- configs[2] "Batch=256 synthetic 32x256
+training step (conv+BiLSTM+CTC grad), 1xMI355X bf16"; with --gpus N the same
+per-GPU batch runs data-parallel (weak scaling, one RCCL all-reduce per step).
+
+One step = convnet_layers -> rnn_layers -> ctc_loss_layer forward, backward,
+gradient all-reduce (N > 1) and the Adam kernel, on synthetic uint8 crops and
+labels already resident in HBM. Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_F32_TFLOPS = 157.3       # f32 MFMA = f32 vector peak
+PEAK_HBM_GBS = 8000.0         # HBM3E spec
+
+
+def synthetic_batch(rng, B, W, T, device):
+    """uint8 crops U{0..255}; labels: length U{2..19}, chars U{0..94}, resampled
+    until L + #repeats <= T."""
+    img = torch.from_numpy(rng.integers(0, 256, (B, 32, W, 1), dtype=np.uint8)).to(device)
+    widths = torch.full((B,), W, dtype=torch.int32, device=device)
+    lab = np.zeros((B, 19), np.int32)
+    ln = np.zeros(B, np.int32)
+    for b in range(B):
+        while True:
+            L = int(rng.integers(2, 20))
+            s = rng.integers(0, 95, L)
+            if L + int(np.sum(s[1:] == s[:-1])) <= T:
+                break
+        lab[b, :L] = s
+        ln[b] = L
+    return img, widths, (torch.from_numpy(lab).to(device), torch.from_numpy(ln).to(device))
+
+
+def work_conv_fwd(args):
+    # (x, B, H, W, cin, w_nk, bias, cout, ...): 2 * pixels * 9 * cin * cout FLOP
+    return 2.0 * args[1] * args[2] * args[3] * 9 * args[4] * args[7]
+
+
+def work_lstm_fwd(args):
+    # (gx, whT, h, c, seq_len, T, B, H, ...): recurrent h.W_h FLOP, both directions
+    T, B, H = args[5], args[6], args[7]
+    return 2.0 * 2 * T * B * H * 4 * H
+
+
+def work_gemm(args):
+    # (ta, tb, M, N, K, ...., batch at index 19)
+    return 2.0 * args[2] * args[3] * args[4] * args[19]
+
+
+ROOFLINE_OPS = {
+    "conv": ("ocrk_conv3x3_fwd", work_conv_fwd, "conv2-conv8 forward implicit-GEMM launches (MFMA bf16)"),
+    "lstm": ("ocrk_lstm_fwd", work_lstm_fwd, "recurrent h.W_h time loop, both directions (MFMA bf16)"),
+    "gemm": ("ocrk_gemm", work_gemm, "dense GEMM launches"),
+}
+
+
+def cpu_baseline(sample, steps=3, threads=16):
+    """The oracle (NumPy restatement of the reference graph) train step timed on
+    the host cores: a bounded sample of `sample` 32x256 crops."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ref_graph as G
+    from oracle import ref_model as M
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    rng = np.random.default_rng(20260)
+    vals = M.init_params(seed=0)
+    img = rng.integers(0, 256, (sample, 32, 256, 1)).astype(np.uint8)
+    x = G.preprocess(img)
+    widths = np.full(sample, 256, np.int32)
+    labels = [list(rng.integers(0, 95, 8)) for _ in range(sample)]
+    with threadpool_limits(limits=threads):
+        M.train_step(vals, {}, 0, x, widths, labels)                 # warm-up
+        t0 = time.perf_counter()
+        for i in range(steps):
+            M.train_step(vals, {}, i, x, widths, labels)
+        dt = time.perf_counter() - t0
+    return {"value": round(sample * steps / dt, 3), "unit": "line-crops/sec", "cores": threads, "kind": "port",
+            "sample": f"{steps} oracle train steps (NumPy fp32, LSTM 512/512) on {sample} synthetic 32x256 crops, "
+                      f"{threads} BLAS threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="crops per GPU")
+    ap.add_argument("--width", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--roofline", default="conv", choices=sorted(ROOFLINE_OPS))
+    ap.add_argument("--breakdown", action="store_true", help="per-entry-point event timing table on stderr")
+    ap.add_argument("--cpu-sample", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, _lib
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    B, W = args.batch, args.width
+    T = (W - 2) // 2 - 2
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=dtype), device=device, seed=0)
+    trainer = Trainer(store)
+    rng = np.random.default_rng(1234 + rank)                # per-rank seed = base + rank
+    img, widths, labels = synthetic_batch(rng, B, W, T, device)
+
+    for _ in range(args.warmup):
+        trainer.step(img, widths, labels)
+    torch.cuda.synchronize()
+
+    op_name, work_fn, op_desc = ROOFLINE_OPS[args.roofline]
+    probe = []
+    _lib.PROBES[op_name] = (work_fn, probe)
+    table = {}
+    if args.breakdown:
+        for name in _lib.SIGNATURES:
+            if name != op_name and not name.endswith(("_size", "version", "last_error", "tiles")):
+                table[name] = []
+                _lib.PROBES[name] = (None, table[name])
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(img, widths, labels)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.PROBES.clear()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms = [a.elapsed_time(b) for a, b, _ in probe]
+    work = sum(w for _, _, w in probe)
+    avg_ms = sum(ms) / max(len(ms), 1)
+    achieved = work / max(sum(ms), 1e-9) / 1e9          # FLOP/ms -> TFLOP/s
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+
+    if args.breakdown and rank == 0:
+        rows = [(n, sum(a.elapsed_time(b) for a, b, _ in r) / args.steps, len(r) // args.steps)
+                for n, r in table.items() if r]
+        rows.append((op_name, sum(ms) / args.steps, len(ms) // args.steps))
+        tot = sum(r[1] for r in rows)
+        print(f"# per-step device time by entry point (sum {tot:.2f} ms, wall {1e3 * elapsed / args.steps:.2f} ms)",
+              file=sys.stderr)
+        for n, t, c in sorted(rows, key=lambda r: -r[1]):
+            print(f"#  {n:32s} {t:9.3f} ms  {c:4d} calls", file=sys.stderr)
+
+    value = world * B * args.steps / elapsed
+    result = {
+        "metric": "line-crops/sec (train step) at 32x256 bs=256; CER vs ref",
+        "value": round(value, 2),
+        "unit": "line-crops/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+        "data": "synthetic (uint8 crops U{0..255}, labels len U{2..19}; random-init weights, reference initialisers)",
+        "config": {"workload": "C3: train step (conv+BiLSTM+CTC grad+Adam), LSTM 512/512 (model_bu.py)",
+                   "global_batch": B * world, "per_gpu_batch": B, "image": f"32x{W}", "seq_len": T,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "launches_per_step": len(ms) // max(args.steps, 1), "avg_launch_ms": round(avg_ms, 4),
+                     "algorithmic_flop_per_launch": work / max(len(ms), 1)},
+        "loss": round(float(loss.item()), 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -107,9 +107,25 @@ def lib():
     return _lib
 
 
+# Optional launch probes (bench.py): name -> (work_fn(args) or None, records list).
+# A probed entry point is bracketed by HIP events on torch's current stream --
+# the stream every wrapper launches on -- and (start, end, work) is recorded.
+PROBES = {}
+
+
 def call(name, *args):
     """Call ocrk_<name>; raise on a non-zero status."""
-    status = getattr(lib(), name)(*args)
+    probe = PROBES.get(name)
+    if probe is not None:
+        work_fn, records = probe
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        status = getattr(lib(), name)(*args)
+        ev1.record()
+        records.append((ev0, ev1, work_fn(args) if work_fn else 0.0))
+    else:
+        status = getattr(lib(), name)(*args)
     if status != OCRK_OK:
         msg = lib().ocrk_last_error().decode(errors="replace")
         if status in (OCRK_ERR_INFEASIBLE, OCRK_ERR_INVALID_ARG):
