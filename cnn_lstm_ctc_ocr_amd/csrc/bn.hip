@@ -239,16 +239,26 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
     }
 }
 
+// dsum[o] = sum_i slab[i][o] (o < 2C; fixed order), then dbeta = dsum[:C], dgamma = dsum[C:]
 __global__ void __launch_bounds__(256)
 bn_bwd_sum_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ dsum,
                   float* __restrict__ dbeta, float* __restrict__ dgamma, int accumulate) {
-    int o = blockIdx.x * 256 + threadIdx.x;
-    if (o >= 2 * C) return;
+    __shared__ double part[4][64];
+    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int o = blockIdx.x * 64 + cl;
     double s = 0.0;
-    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * 2 * C + o];
-    dsum[o] = (float)s;
-    float* dst = o < C ? dbeta + o : dgamma + (o - C);
-    *dst = accumulate ? *dst + (float)s : (float)s;
+    if (o < 2 * C) {
+#pragma unroll 8
+        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * 2 * C + o];
+    }
+    part[q][cl] = s;
+    __syncthreads();
+    if (q == 0 && o < 2 * C) {
+        double t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
+        dsum[o] = (float)t;
+        float* dst = o < C ? dbeta + o : dgamma + (o - C);
+        *dst = accumulate ? *dst + (float)t : (float)t;
+    }
 }
 
 // pass 2: dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n)
@@ -353,7 +363,7 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
         bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, ipb, slab);
     int st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
     if (st) return st;
-    bn_bwd_sum_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(slab, (int)nb, C, dsum, dbeta, dgamma, accumulate);
+    bn_bwd_sum_kernel<<<(2 * C + 63) / 64, 256, 0, s>>>(slab, (int)nb, C, dsum, dbeta, dgamma, accumulate);
     st = ocrk::launch_status("ocrk_bn_relu_pool_bwd sum");
     if (st) return st;
     if (dtype == OCRK_BF16)

@@ -132,18 +132,24 @@ conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B,
     }
 }
 
+// out0 <- first n0 columns of sum_i slab[i][:], out1 <- the rest (fixed order)
 __global__ void __launch_bounds__(256)
 sum_slabs_kernel(const float* __restrict__ slab, int nslab, int width, float* __restrict__ out0,
                  int n0, float* __restrict__ out1, int accumulate) {
-    // out0 <- first n0 columns, out1 <- the rest (may be NULL)
-    for (int o = blockIdx.x * 256 + threadIdx.x; o < width; o += gridDim.x * 256) {
-        double s = 0.0;
-        for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * width + o];
-        if (o < n0) {
-            out0[o] = accumulate ? out0[o] + (float)s : (float)s;
-        } else if (out1) {
-            out1[o - n0] = accumulate ? out1[o - n0] + (float)s : (float)s;
-        }
+    __shared__ double part[4][64];
+    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int o = blockIdx.x * 64 + cl;
+    double s = 0.0;
+    if (o < width) {
+#pragma unroll 8
+        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * width + o];
+    }
+    part[q][cl] = s;
+    __syncthreads();
+    if (q == 0 && o < width) {
+        float t = (float)(part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl]);
+        if (o < n0) out0[o] = accumulate ? out0[o] + t : t;
+        else if (out1) out1[o - n0] = accumulate ? out1[o - n0] + t : t;
     }
 }
 
@@ -192,7 +198,7 @@ extern "C" int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz,
     }
     int st = ocrk::launch_status("ocrk_conv1_bwd_weight");
     if (st) return st;
-    sum_slabs_kernel<<<2, 256, 0, s>>>(slab, (int)nb, 10 * cout, dw, 9 * cout, db, accumulate);
+    sum_slabs_kernel<<<(10 * cout + 63) / 64, 256, 0, s>>>(slab, (int)nb, 10 * cout, dw, 9 * cout, db, accumulate);
     return ocrk::launch_status("ocrk_conv1_bwd_weight reduce");
 }
 

@@ -51,10 +51,22 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
     constexpr int WM = TBM / 2, WN = TBN / 2, TM = WM / 16, TN = WN / 16;
     constexpr bool A_K = (AM == A_ROWK || AM == A_IM2COL || AM == A_IM2COL_FLIP);
     constexpr bool B_K = (BMD == B_NK);
+    constexpr bool BF = sizeof(CT) == 2;
+    // bf16 operands whose source is contiguous along the row (m or n) are kept
+    // row-contiguous in LDS ([k][row], written with 16-B stores) and read as
+    // MFMA fragments with ds_read_b64_tr_b16. Row stride T+16 elements puts
+    // the 8 rows of a 32-lane half on 8 distinct 32-B bank slots.
+    constexpr bool A_TR = BF && !A_K, B_TR = BF && !B_K;
+    // With a transposed image the MFMA k-slot order is permuted (same for A
+    // and B): lane group g, element j holds k = (j < 4 ? 4g + j : 16 + 4g + j - 4).
+    constexpr bool PERM = A_TR || B_TR;
+    constexpr int LDA_R = TBM + 16, LDB_R = TBN + 16;
+    constexpr int A_ELEMS = A_TR ? BK * LDA_R : TBM * LDK;
+    constexpr int B_ELEMS = B_TR ? BK * LDB_R : TBN * LDK;
     constexpr int NVA = (TBM * BK / 8 + 255) / 256;
     constexpr int NVB = (TBN * BK / 8 + 255) / 256;
-    __shared__ __attribute__((aligned(16))) RT sA[2][TBM * LDK];
-    __shared__ __attribute__((aligned(16))) RT sB[2][TBN * LDK];
+    __shared__ __attribute__((aligned(16))) RT sA[2][A_ELEMS];
+    __shared__ __attribute__((aligned(16))) RT sB[2][B_ELEMS];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -104,8 +116,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
                     vstore_lds(&sA[buf][(idx >> 2) * LDK + 8 * (idx & 3)], ra[v]);
                 } else {
                     int kk = idx / (TBM / 8), r0 = 8 * (idx % (TBM / 8));
+                    if constexpr (A_TR) {
+                        vstore_lds(&sA[buf][kk * LDA_R + r0], ra[v]);
+                    } else {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) sA[buf][(r0 + i) * LDK + kk] = ra[v].e(i);
+                        for (int i = 0; i < 8; ++i) sA[buf][(r0 + i) * LDK + kk] = ra[v].e(i);
+                    }
                 }
             }
         }
@@ -117,8 +133,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
                     vstore_lds(&sB[buf][(idx >> 2) * LDK + 8 * (idx & 3)], rb[v]);
                 } else {
                     int kk = idx / (TBN / 8), r0 = 8 * (idx % (TBN / 8));
+                    if constexpr (B_TR) {
+                        vstore_lds(&sB[buf][kk * LDB_R + r0], rb[v]);
+                    } else {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) sB[buf][(r0 + i) * LDK + kk] = rb[v].e(i);
+                        for (int i = 0; i < 8; ++i) sB[buf][(r0 + i) * LDK + kk] = rb[v].e(i);
+                    }
                 }
             }
         }
@@ -135,24 +155,41 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
         store_tiles(0);
         __syncthreads();
     }
+    const int g = lane >> 4, i16 = lane & 15;
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
-        const RT* a_base = &sA[buf][(wm * WM + (lane & 15)) * LDK + 8 * (lane >> 4)];
-        const RT* b_base = &sB[buf][(wn * WN + (lane & 15)) * LDK + 8 * (lane >> 4)];
-        if constexpr (sizeof(CT) == 2) {
+        if constexpr (BF) {
             bf16x8 af[TM], bfr[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a_base + i * 16 * LDK);
+            for (int i = 0; i < TM; ++i) {
+                if constexpr (A_TR) {
+                    const RT* ap = &sA[buf][(4 * g + (i16 >> 2)) * LDA_R + wm * WM + i * 16 + 4 * (i16 & 3)];
+                    af[i] = frag_tr(ap, 16 * LDA_R);
+                } else {
+                    const RT* ap = &sA[buf][(wm * WM + i * 16 + i16) * LDK];
+                    af[i] = PERM ? frag_perm(ap, g) : *reinterpret_cast<const bf16x8*>(ap + 8 * g);
+                }
+            }
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b_base + j * 16 * LDK);
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (B_TR) {
+                    const RT* bp = &sB[buf][(4 * g + (i16 >> 2)) * LDB_R + wn * WN + j * 16 + 4 * (i16 & 3)];
+                    bfr[j] = frag_tr(bp, 16 * LDB_R);
+                } else {
+                    const RT* bp = &sB[buf][(wn * WN + j * 16 + i16) * LDK];
+                    bfr[j] = PERM ? frag_perm(bp, g) : *reinterpret_cast<const bf16x8*>(bp + 8 * g);
+                }
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         } else {
-            // f32: lane group g = lane>>4 feeds k-slot g with k = 8g + kk (same map for A and B)
+            // f32: lane group g feeds k-slot g with k = 8g + kk (same map for A and B)
+            const RT* a_base = &sA[buf][(wm * WM + i16) * LDK + 8 * g];
+            const RT* b_base = &sB[buf][(wn * WN + i16) * LDK + 8 * g];
             V8<float> af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) vload_lds(af[i], a_base + i * 16 * LDK);

@@ -37,6 +37,8 @@ struct RecurCore {
     static constexpr int EPI_BYTES = BR * (NC + 1) * 4;
     static constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
     static_assert(TILES % 4 == 0 || TILES < 4, "tile split");
+    static constexpr bool FULL_A = (BR * KC / 8) % 256 == 0;
+    static constexpr bool FULL_B = (NC * KC / 8) % 256 == 0;
 
     template <typename BCol>
     __device__ __forceinline__ static void load(V8<CT> (&ra)[NVA], V8<CT> (&rb)[NVB], const CT* __restrict__ a_rows,
@@ -45,7 +47,7 @@ struct RecurCore {
 #pragma unroll
         for (int v = 0; v < NVA; ++v) {
             int idx = tid + 256 * v;
-            if (idx < BR * KC / 8) {
+            if (FULL_A || idx < BR * KC / 8) {
                 int r = idx / (KC / 8), kq = idx % (KC / 8);
                 vload(ra[v], a_rows + (int64_t)r * lda + k0 + 8 * kq);
             }
@@ -53,7 +55,7 @@ struct RecurCore {
 #pragma unroll
         for (int v = 0; v < NVB; ++v) {
             int idx = tid + 256 * v;
-            if (idx < NC * KC / 8) {
+            if (FULL_B || idx < NC * KC / 8) {
                 int n = idx / (KC / 8), kq = idx % (KC / 8);
                 vload(rb[v], bcol(n) + k0 + 8 * kq);
             }
@@ -65,13 +67,13 @@ struct RecurCore {
 #pragma unroll
         for (int v = 0; v < NVA; ++v) {
             int idx = tid + 256 * v;
-            if (idx < BR * KC / 8)
+            if (FULL_A || idx < BR * KC / 8)
                 vstore_lds(sA + buf * BR * LDK + (idx / (KC / 8)) * LDK + 8 * (idx % (KC / 8)), ra[v]);
         }
 #pragma unroll
         for (int v = 0; v < NVB; ++v) {
             int idx = tid + 256 * v;
-            if (idx < NC * KC / 8)
+            if (FULL_B || idx < NC * KC / 8)
                 vstore_lds(sB + buf * NC * LDK + (idx / (KC / 8)) * LDK + 8 * (idx % (KC / 8)), rb[v]);
         }
     }
@@ -103,18 +105,25 @@ struct RecurCore {
     }
 
     // acc <- A[BR, K] . Bcols[NC, K]^T ; A rows at a_rows + r*lda, B col n at bcol(n).
-    // Two register sets (chunks c+1, c+2) in flight while chunk c is on MFMA.
+    // begin() issues the loads of chunks 0 and 1 (so the caller can overlap
+    // other loads with them); finish() runs the pipeline: two register sets
+    // in flight while one chunk is on MFMA.
+    V8<CT> ra0[NVA], rb0[NVB], ra1[NVA], rb1[NVB];
+
     template <typename BCol>
-    __device__ __forceinline__ static void run(const CT* __restrict__ a_rows, int64_t lda, const BCol& bcol, int K,
-                                               char* lds, floatx4 (&acc)[TPW]) {
+    __device__ __forceinline__ void begin(const CT* __restrict__ a_rows, int64_t lda, const BCol& bcol, int K) {
+        load(ra0, rb0, a_rows, lda, bcol, 0);
+        if (K / KC > 1) load(ra1, rb1, a_rows, lda, bcol, KC);
+    }
+
+    template <typename BCol>
+    __device__ __forceinline__ void finish(const CT* __restrict__ a_rows, int64_t lda, const BCol& bcol, int K,
+                                           char* lds, floatx4 (&acc)[TPW]) {
         RT* sA = reinterpret_cast<RT*>(lds);
         RT* sB = sA + 2 * BR * LDK;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-        V8<CT> ra0[NVA], rb0[NVB], ra1[NVA], rb1[NVB];
         const int nch = K / KC;
-        load(ra0, rb0, a_rows, lda, bcol, 0);
-        if (nch > 1) load(ra1, rb1, a_rows, lda, bcol, KC);
         store(ra0, rb0, sA, sB, 0);
         __syncthreads();
         for (int c = 0; c < nch; c += 2) {
@@ -131,7 +140,7 @@ struct RecurCore {
     }
 
     // accumulators -> LDS [BR][NC+1] f32 (call after run(); ends with a barrier)
-    __device__ static void spill(const floatx4 (&acc)[TPW], char* lds) {
+    __device__ __forceinline__ static void spill(const floatx4 (&acc)[TPW], char* lds) {
         float* sG = reinterpret_cast<float*>(lds);
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -147,61 +156,132 @@ struct RecurCore {
     }
 };
 
+// Diagnostic stamps (tools/bench_lstm.py --stamps): thread 0 of every
+// workgroup writes s_memrealtime (100 MHz) at fixed points into dbg.
+__device__ __forceinline__ void stamp(long long* dbg, int i) {
+    if (dbg && threadIdx.x == 0) {
+        long long t = __builtin_amdgcn_s_memrealtime();
+        dbg[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + i] = t;
+    }
+}
+
+// 4 consecutive elements of CT (8 B for bf16, 16 B for f32)
+template <typename CT> struct V4;
+template <> struct V4<bf16> { typedef unsigned int u32x2 __attribute__((ext_vector_type(2))); u32x2 q; };
+template <> struct V4<float> { f32x4 q; };
+__device__ __forceinline__ void ld4(float (&v)[4], const bf16* p) {
+    V4<bf16>::u32x2 q = *reinterpret_cast<const V4<bf16>::u32x2*>(p);
+    v[0] = __builtin_bit_cast(float, q[0] << 16); v[1] = __builtin_bit_cast(float, q[0] & 0xffff0000u);
+    v[2] = __builtin_bit_cast(float, q[1] << 16); v[3] = __builtin_bit_cast(float, q[1] & 0xffff0000u);
+}
+__device__ __forceinline__ void ld4(float (&v)[4], const float* p) {
+    f32x4 q = *reinterpret_cast<const f32x4*>(p);
+    v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+}
+__device__ __forceinline__ void st4(bf16* p, const float (&v)[4]) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 q = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = q;
+}
+__device__ __forceinline__ void st4(float* p, const float (&v)[4]) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+}
+// exp-based gate nonlinearities (one v_exp each)
+__device__ __forceinline__ float sig_fast(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+
 __device__ __forceinline__ int step_time(int dir, int s, int len) {
     return (dir == 0 || s >= len) ? s : len - 1 - s;
 }
 
 // --------------------------------------------------------------- forward
+// Epilogue operands (gx, c, h, len) do not depend on the GEMM: they are loaded
+// into registers at kernel entry so their HBM latency hides under the GEMM.
 template <typename CT, int BR, int HU, int KC>
 __global__ void __launch_bounds__(256)
 lstm_fwd_step_kernel(const float* __restrict__ gx, const CT* __restrict__ whT, const CT* __restrict__ h_in,
                      CT* __restrict__ h_out, float* __restrict__ c_state, const int* __restrict__ seq_len,
                      int s, int T, int B, int H, CT* __restrict__ out, CT* __restrict__ hprev_t,
-                     float* __restrict__ cprev_t, float* __restrict__ acts_t) {
+                     float* __restrict__ cprev_t, CT* __restrict__ acts_t, long long* __restrict__ dbg) {
     using Core = RecurCore<CT, BR, 4 * HU, KC>;
+    stamp(dbg, 0);
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
     const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const int G4 = 4 * H;
+
+    // thread <-> (row r, 4 consecutive units u..u+3) of the epilogue
+    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+    static_assert(HU % 4 == 0, "4-unit epilogue vectors");
+    constexpr bool EFULL = (BR * UQ) % 256 == 0;     // whole passes: no lane guard (bf16 tiles)
+    // 1. sequence lengths; 2. the GEMM's first chunks; 3. the epilogue
+    // operands (t depends on len) -- all loads unconditional, no lane branches.
+    int plen[EPQ4];
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min((int)threadIdx.x + 256 * q, BR * UQ - 1) / UQ];
     const CT* a_rows = h_in + ((int64_t)dir * B + b0) * H;
     const CT* wdir = whT + (int64_t)dir * 4 * H * H;
     auto bcol = [&](int n) { return wdir + (int64_t)((n / HU) * H + u0 + (n % HU)) * H; };
+    Core core;
+    core.begin(a_rows, H, bcol, H);
+    stamp(dbg, 1);
+    float pg[EPQ4][4][4], pc[EPQ4][4], ph[EPQ4][4];
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) {
+        const int idx = threadIdx.x + 256 * q;
+        if (!EFULL && idx >= BR * UQ) continue;
+        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+        const int64_t st = ((int64_t)dir * B + b) * H + uu;
+        ld4(pc[q], c_state + st);
+        ld4(ph[q], h_in + st);
+        const int t = step_time(dir, s, plen[q]);
+        const float* g = gx + (((int64_t)t * B + b) * 2 + dir) * G4 + uu;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ld4(pg[q][k], g + k * H);
+    }
+    stamp(dbg, 2);
     floatx4 acc[Core::TPW];
-    Core::run(a_rows, H, bcol, H, lds, acc);
+    core.finish(a_rows, H, bcol, H, lds, acc);
+    stamp(dbg, 3);
     Core::spill(acc, lds);
+    stamp(dbg, 4);
     const float* sG = reinterpret_cast<const float*>(lds);
-    const int G4 = 4 * H;
-    for (int idx = threadIdx.x; idx < BR * HU; idx += 256) {
-        const int r = idx / HU, u = idx % HU, b = b0 + r, uu = u0 + u;
-        const int len = seq_len[b];
-        const bool valid = s < len;
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) {
+        const int idx = threadIdx.x + 256 * q;
+        if (!EFULL && idx >= BR * UQ) continue;
+        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+        const int len = plen[q];
         const int t = step_time(dir, s, len);
         const int64_t st = ((int64_t)dir * B + b) * H + uu;          // state index
         const int64_t tb = ((int64_t)t * B + b) * 2 + dir;           // time-order row
-        const float hp = to_f32(h_in[st]);
-        const float cp = c_state[st];
-        if (valid) {
-            const float* g = gx + tb * G4;
-            float pi = sG[r * (4 * HU + 1) + 0 * HU + u] + g[0 * H + uu];
-            float pj = sG[r * (4 * HU + 1) + 1 * HU + u] + g[1 * H + uu];
-            float pf = sG[r * (4 * HU + 1) + 2 * HU + u] + g[2 * H + uu];
-            float po = sG[r * (4 * HU + 1) + 3 * HU + u] + g[3 * H + uu];
-            float ai = sigmoidf_(pi), aj = tanhf(pj), af = sigmoidf_(pf + 1.0f), ao = sigmoidf_(po);
-            float c = af * cp + ai * aj;
-            float h = ao * tanhf(c);
-            c_state[st] = c;
-            h_out[st] = from_f32<CT>(h);
-            out[((int64_t)t * B + b) * 2 * H + dir * H + uu] = from_f32<CT>(h);
-            hprev_t[tb * H + uu] = from_f32<CT>(hp);
-            cprev_t[tb * H + uu] = cp;
-            float* a = acts_t + tb * G4;
-            a[0 * H + uu] = ai; a[1 * H + uu] = aj; a[2 * H + uu] = af; a[3 * H + uu] = ao;
+        CT* a = acts_t + tb * G4 + uu;
+        if (s < len) {
+            const float* gl = sG + r * (4 * HU + 1) + u;
+            float ai[4], aj[4], af[4], ao[4], c[4], h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                ai[e] = sig_fast(gl[0 * HU + e] + pg[q][0][e]);
+                aj[e] = tanh_fast(gl[1 * HU + e] + pg[q][1][e]);
+                af[e] = sig_fast(gl[2 * HU + e] + pg[q][2][e] + 1.0f);   // forget_bias = 1
+                ao[e] = sig_fast(gl[3 * HU + e] + pg[q][3][e]);
+                c[e] = af[e] * pc[q][e] + ai[e] * aj[e];
+                h[e] = ao[e] * tanh_fast(c[e]);
+            }
+            st4(c_state + st, c);
+            st4(h_out + st, h);
+            st4(out + ((int64_t)t * B + b) * 2 * H + dir * H + uu, h);
+            st4(hprev_t + tb * H + uu, ph[q]);
+            st4(cprev_t + tb * H + uu, pc[q]);
+            st4(a + 0 * H, ai); st4(a + 1 * H, aj); st4(a + 2 * H, af); st4(a + 3 * H, ao);
         } else {
-            h_out[st] = h_in[st];
-            hprev_t[tb * H + uu] = from_f32<CT>(0.f);
-            cprev_t[tb * H + uu] = 0.f;
-            float* a = acts_t + tb * G4;
-            a[0 * H + uu] = 0.f; a[1 * H + uu] = 0.f; a[2 * H + uu] = 0.f; a[3 * H + uu] = 0.f;
+            const float z[4] = {0.f, 0.f, 0.f, 0.f};
+            st4(h_out + st, ph[q]);
+            st4(hprev_t + tb * H + uu, z);
+            st4(cprev_t + tb * H + uu, z);
+            st4(a + 0 * H, z); st4(a + 1 * H, z); st4(a + 2 * H, z); st4(a + 3 * H, z);
         }
     }
+    stamp(dbg, 5);
 }
 
 // -------------------------------------------------------------- backward
@@ -210,88 +290,121 @@ __global__ void __launch_bounds__(256)
 lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT* __restrict__ dg_out,
                      float* __restrict__ dc_state, const int* __restrict__ seq_len, int s, int T, int B, int H,
                      const CT* __restrict__ dout, const float* __restrict__ cprev_t,
-                     const float* __restrict__ acts_t, CT* __restrict__ dG_t) {
+                     const CT* __restrict__ acts_t, CT* __restrict__ dG_t) {
     using Core = RecurCore<CT, BR, HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
     const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
     const int G4 = 4 * H;
+
+    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+    static_assert(HU % 4 == 0, "4-unit epilogue vectors");
+    constexpr bool EFULL = (BR * UQ) % 256 == 0;     // whole passes: no lane guard (bf16 tiles)
+    int plen[EPQ4];
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min((int)threadIdx.x + 256 * q, BR * UQ - 1) / UQ];
     const CT* a_rows = dg_in + ((int64_t)dir * B + b0) * G4;
     const CT* wdir = wh + (int64_t)dir * H * G4;
     auto bcol = [&](int n) { return wdir + (int64_t)(u0 + n) * G4; };
+    Core core;
+    core.begin(a_rows, G4, bcol, G4);
+    float pa[EPQ4][4][4], pcp[EPQ4][4], pdc[EPQ4][4], pdo[EPQ4][4];
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) {
+        const int idx = threadIdx.x + 256 * q;
+        if (!EFULL && idx >= BR * UQ) continue;
+        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+        ld4(pdc[q], dc_state + ((int64_t)dir * B + b) * H + uu);
+        const int t = step_time(dir, s, plen[q]);
+        const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
+        const CT* a = acts_t + tb * G4 + uu;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ld4(pa[q][k], a + k * H);
+        ld4(pcp[q], cprev_t + tb * H + uu);
+        ld4(pdo[q], dout + ((int64_t)t * B + b) * 2 * H + dir * H + uu);
+    }
     floatx4 acc[Core::TPW];
-    Core::run(a_rows, G4, bcol, G4, lds, acc);
+    core.finish(a_rows, G4, bcol, G4, lds, acc);
     Core::spill(acc, lds);
     const float* sG = reinterpret_cast<const float*>(lds);
-    for (int idx = threadIdx.x; idx < BR * HU; idx += 256) {
-        const int r = idx / HU, u = idx % HU, b = b0 + r, uu = u0 + u;
-        const int len = seq_len[b];
-        const bool valid = s < len;
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) {
+        const int idx = threadIdx.x + 256 * q;
+        if (!EFULL && idx >= BR * UQ) continue;
+        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+        const int len = plen[q];
         const int t = step_time(dir, s, len);
         const int64_t st = ((int64_t)dir * B + b) * H + uu;
         const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
-        CT* dgo = dg_out + ((int64_t)dir * B + b) * G4;
-        CT* dgt = dG_t + tb * G4;
-        if (valid) {
-            float dh = sG[r * (HU + 1) + u] + to_f32(dout[((int64_t)t * B + b) * 2 * H + dir * H + uu]);
-            const float* a = acts_t + tb * G4;
-            float ai = a[0 * H + uu], aj = a[1 * H + uu], af = a[2 * H + uu], ao = a[3 * H + uu];
-            float cp = cprev_t[tb * H + uu];
-            float c = af * cp + ai * aj;
-            float tc = tanhf(c);
-            float dc = dc_state[st] + dh * ao * (1.f - tc * tc);
-            float d_o = dh * tc * ao * (1.f - ao);
-            float d_i = dc * aj * ai * (1.f - ai);
-            float d_j = dc * ai * (1.f - aj * aj);
-            float d_f = dc * cp * af * (1.f - af);
-            dc_state[st] = dc * af;
-            CT vi = from_f32<CT>(d_i), vj = from_f32<CT>(d_j), vf = from_f32<CT>(d_f), vo = from_f32<CT>(d_o);
-            dgo[0 * H + uu] = vi; dgo[1 * H + uu] = vj; dgo[2 * H + uu] = vf; dgo[3 * H + uu] = vo;
-            dgt[0 * H + uu] = vi; dgt[1 * H + uu] = vj; dgt[2 * H + uu] = vf; dgt[3 * H + uu] = vo;
+        CT* dgo = dg_out + ((int64_t)dir * B + b) * G4 + uu;
+        CT* dgt = dG_t + tb * G4 + uu;
+        if (s < len) {
+            float di[4], dj[4], df[4], dO[4], dcn[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float dh = sG[r * (HU + 1) + u + e] + pdo[q][e];
+                float ai = pa[q][0][e], aj = pa[q][1][e], af = pa[q][2][e], ao = pa[q][3][e];
+                float cp = pcp[q][e];
+                float c = af * cp + ai * aj;
+                float tc = tanh_fast(c);
+                float dc = pdc[q][e] + dh * ao * (1.f - tc * tc);
+                dO[e] = dh * tc * ao * (1.f - ao);
+                di[e] = dc * aj * ai * (1.f - ai);
+                dj[e] = dc * ai * (1.f - aj * aj);
+                df[e] = dc * cp * af * (1.f - af);
+                dcn[e] = dc * af;
+            }
+            st4(dc_state + st, dcn);
+            st4(dgo + 0 * H, di); st4(dgo + 1 * H, dj); st4(dgo + 2 * H, df); st4(dgo + 3 * H, dO);
+            st4(dgt + 0 * H, di); st4(dgt + 1 * H, dj); st4(dgt + 2 * H, df); st4(dgt + 3 * H, dO);
         } else {
-            CT z = from_f32<CT>(0.f);
-            dc_state[st] = 0.f;
-            dgo[0 * H + uu] = z; dgo[1 * H + uu] = z; dgo[2 * H + uu] = z; dgo[3 * H + uu] = z;
-            dgt[0 * H + uu] = z; dgt[1 * H + uu] = z; dgt[2 * H + uu] = z; dgt[3 * H + uu] = z;
+            const float z[4] = {0.f, 0.f, 0.f, 0.f};
+            st4(dc_state + st, z);
+            st4(dgo + 0 * H, z); st4(dgo + 1 * H, z); st4(dgo + 2 * H, z); st4(dgo + 3 * H, z);
+            st4(dgt + 0 * H, z); st4(dgt + 1 * H, z); st4(dgt + 2 * H, z); st4(dgt + 3 * H, z);
         }
     }
 }
 
 // ------------------------------------------------------------------ C ABI
+static long long* g_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
+
+extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_dbg = buf; return OCRK_OK; }
+
 // Tile shapes: bf16 BR=64 x HU=16 (fwd K-chunk 128, bwd 256); f32 BR=32 x HU=8/16.
-#define FWD_BF16 bf16, 64, 16, 128
+#define FWD_BF16 bf16, 64, 16, 256
 #define FWD_F32 float, 32, 8, 64
 #define BWD_BF16 bf16, 64, 16, 256
 #define BWD_F32 float, 32, 16, 128
 
 extern "C" int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void* h_out,
                                   float* c_state, const int* seq_len, int s, int T, int B, int H, void* out,
-                                  void* hprev_t, float* cprev_t, float* acts_t, int dtype, void* stream) {
+                                  void* hprev_t, float* cprev_t, void* acts_t, int dtype, void* stream) {
     hipStream_t st = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16) {
-        OCRK_REQUIRE(H % 128 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 128 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
+        OCRK_REQUIRE(H % 256 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 256 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 16, B / 64, 2);
-        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, acts_t);
+        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_dbg);
     } else {
         OCRK_REQUIRE(H % 64 == 0 && B % 32 == 0, "ocrk_lstm_fwd_step: f32 needs H %% 64 == 0 and B %% 32 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 8, B / 32, 2);
-        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>(gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, acts_t);
+        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>(gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, (float*)acts_t, g_dbg);
     }
     return ocrk::launch_status("ocrk_lstm_fwd_step");
 }
 
 extern "C" int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* dc_state,
                                   const int* seq_len, int s, int T, int B, int H, const void* dout,
-                                  const float* cprev_t, const float* acts_t, void* dG_t, int dtype,
+                                  const float* cprev_t, const void* acts_t, void* dG_t, int dtype,
                                   void* stream) {
     hipStream_t st = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 64 == 0 && B % 64 == 0, "ocrk_lstm_bwd_step: bf16 needs H %% 64 == 0 and B %% 64 == 0");
         dim3 grid(H / 16, B / 64, 2);
-        lstm_bwd_step_kernel<BWD_BF16><<<grid, 256, 0, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, H, (const bf16*)dout, cprev_t, acts_t, (bf16*)dG_t);
+        lstm_bwd_step_kernel<BWD_BF16><<<grid, 256, 0, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, H, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t);
     } else {
         OCRK_REQUIRE(H % 32 == 0 && B % 32 == 0, "ocrk_lstm_bwd_step: f32 needs H %% 32 == 0 and B %% 32 == 0");
         dim3 grid(H / 16, B / 32, 2);
-        lstm_bwd_step_kernel<BWD_F32><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, acts_t, (float*)dG_t);
+        lstm_bwd_step_kernel<BWD_F32><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, (const float*)acts_t, (float*)dG_t);
     }
     return ocrk::launch_status("ocrk_lstm_bwd_step");
 }
@@ -299,7 +412,7 @@ extern "C" int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_ou
 // Whole time loops (T launches each) so a binding makes one call per layer.
 extern "C" int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state /*[2 bufs][2][B][H]*/,
                              float* c_state, const int* seq_len, int T, int B, int H, void* out, void* hprev_t,
-                             float* cprev_t, float* acts_t, int dtype, void* stream) {
+                             float* cprev_t, void* acts_t, int dtype, void* stream) {
     size_t esz = dtype == OCRK_BF16 ? 2 : 4;
     char* hs = (char*)h_state;
     size_t hbytes = (size_t)2 * B * H * esz;
@@ -313,7 +426,7 @@ extern "C" int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state /*[
 
 extern "C" int ocrk_lstm_bwd(const void* wh, void* dg_state /*[2 bufs][2][B][4H]*/, float* dc_state,
                              const int* seq_len, int T, int B, int H, const void* dout, const float* cprev_t,
-                             const float* acts_t, void* dG_t, int dtype, void* stream) {
+                             const void* acts_t, void* dG_t, int dtype, void* stream) {
     size_t esz = dtype == OCRK_BF16 ? 2 : 4;
     char* ds = (char*)dg_state;
     size_t gbytes = (size_t)2 * B * 4 * H * esz;

@@ -46,4 +46,24 @@ __device__ __forceinline__ void vstore_lds(float* d, const V8<float>& x) {
     reinterpret_cast<f32x4*>(d)[1] = x.q1;
 }
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// bf16 MFMA fragment from a row-contiguous [k][row] LDS image: two
+// ds_read_b64_tr_b16, the second `second` elements (16 k-rows) further on.
+__device__ __forceinline__ bf16x8 frag_tr(const unsigned short* p, int second) {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + second));
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+// the same permuted k order from a k-contiguous row: k = 4g..4g+3 and 16+4g..16+4g+3
+__device__ __forceinline__ bf16x8 frag_perm(const unsigned short* row, int g) {
+    s16x4 lo = *reinterpret_cast<const s16x4*>(row + 4 * g);
+    s16x4 hi = *reinterpret_cast<const s16x4*>(row + 16 + 4 * g);
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
 }  // namespace ocrk

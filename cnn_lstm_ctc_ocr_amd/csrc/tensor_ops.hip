@@ -24,26 +24,61 @@ __global__ void __launch_bounds__(256) permute3_kernel(const TI* __restrict__ in
     }
 }
 
-// column sums of [M][N]: block partials over row ranges, then an ordered sum.
+// column sums of [M][N]: each block reduces a row range with 8-column vector
+// loads (TPR threads per row), combines its threads in a fixed order, and
+// writes one slab row; reduce_slabs then sums the slabs in a fixed order
+// (deterministic for a given shape).
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict__ in, int64_t M, int N,
                                                              int64_t rows_per_block, float* __restrict__ slab) {
+    __shared__ float red[256 * 9];
+    const int G = N / 8;                       // column groups of 8
+    const int TPR = G < 256 ? G : 256;         // threads per row
+    const int RPP = 256 / TPR;                 // rows per pass
+    const int tg = threadIdx.x % TPR, tr = threadIdx.x / TPR;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
-    for (int c = threadIdx.x; c < N; c += 256) {
-        float s = 0.f;
-        for (int64_t r = r0; r < r1; ++r) s += to_f32(in[r * N + c]);
-        slab[(int64_t)blockIdx.x * N + c] = s;
+    for (int g0 = 0; g0 < G; g0 += TPR) {
+        const int g = g0 + tg;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (tr < RPP && g < G) {
+#pragma unroll 4
+            for (int64_t r = r0 + tr; r < r1; r += RPP) {
+                const T* p = in + r * N + g * 8;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc[i] += to_f32(p[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[threadIdx.x * 9 + i] = acc[i];
+        __syncthreads();
+        for (int o = threadIdx.x; o < TPR * 8; o += 256) {
+            int gg = o / 8, i = o % 8;
+            float sum = 0.f;
+            for (int q = 0; q < RPP; ++q) sum += red[(q * TPR + gg) * 9 + i];
+            if (g0 + gg < G) slab[(int64_t)blockIdx.x * N + (g0 + gg) * 8 + i] = sum;
+        }
+        __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ slab, int nslab, int N,
+// out[c] (+)= sum_i slab[i][c], 64 columns x 4 slab lanes per block, fixed order.
+__global__ void __launch_bounds__(256) reduce_slabs_kernel(const float* __restrict__ slab, int nslab, int N,
                                                            float* __restrict__ out, int accumulate) {
-    int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= N) return;
+    __shared__ double part[4][64];
+    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
     double s = 0.0;
-    for (int i = 0; i < nslab; ++i) s += slab[(int64_t)i * N + c];
-    out[c] = accumulate ? out[c] + (float)s : (float)s;
+    if (c < N) {
+#pragma unroll 8
+        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * N + c];
+    }
+    part[q][cl] = s;
+    __syncthreads();
+    if (q == 0 && c < N) {
+        double t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
+        out[c] = accumulate ? out[c] + (float)t : (float)t;
+    }
 }
 
 template <typename TO>
@@ -76,7 +111,7 @@ extern "C" int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d
     return ocrk::launch_status("ocrk_permute3");
 }
 
-static int64_t colsum_blocks(int64_t M) { return std::max<int64_t>(1, std::min<int64_t>(1024, ocrk::cdiv(M, 256))); }
+static int64_t colsum_blocks(int64_t M) { return std::max<int64_t>(1, std::min<int64_t>(256, ocrk::cdiv(M, 512))); }
 
 extern "C" size_t ocrk_colsum_workspace_size(int64_t M, int N) {
     return (size_t)colsum_blocks(M) * N * sizeof(float);
@@ -85,6 +120,7 @@ extern "C" size_t ocrk_colsum_workspace_size(int64_t M, int N) {
 extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
                            size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ws_bytes >= ocrk_colsum_workspace_size(M, N), "ocrk_colsum: workspace too small");
+    OCRK_REQUIRE(N % 8 == 0, "ocrk_colsum: N=%d must be a multiple of 8", N);
     if (N == 0) return OCRK_OK;
     int64_t nb = colsum_blocks(M);
     int64_t rpb = ocrk::cdiv(M, nb);
@@ -94,7 +130,7 @@ extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* o
     else colsum_partial_kernel<float><<<nb, 256, 0, s>>>((const float*)in, M, N, rpb, (float*)ws);
     int st = ocrk::launch_status("ocrk_colsum");
     if (st) return st;
-    colsum_final_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws, (int)nb, N, out, accumulate);
+    reduce_slabs_kernel<<<(N + 63) / 64, 256, 0, s>>>((const float*)ws, (int)nb, N, out, accumulate);
     return ocrk::launch_status("ocrk_colsum final");
 }
 

@@ -202,7 +202,7 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
     out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
     hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
     cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
-    acts = torch.empty(T, B, 2, 4 * H, dtype=torch.float32, device=dev)
+    acts = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
     call("ocrk_lstm_fwd", ptr(gx), ptr(whT), ptr(h_state), ptr(c_state), ptr(seq_len), T, B, H, ptr(out),
          ptr(hprev), ptr(cprev), ptr(acts), dtype_code(dtype), _stream(gx))
     return out, hprev, cprev, acts

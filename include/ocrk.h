@@ -131,20 +131,23 @@ int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, in
  *   wh      dtype [2][H][4H]   (recurrent kernel rows as stored)
  *   h_state dtype [2 bufs][2][B][H], c_state f32 [2][B][H] (zero before s = 0)
  *   out     dtype [T][B][2H]   (layer output, must be zeroed: t >= len stays 0)
- *   hprev_t dtype [T][B][2][H], cprev_t f32 [T][B][2][H], acts_t f32 [T][B][2][4H]
+ *   hprev_t dtype [T][B][2][H], cprev_t f32 [T][B][2][H], acts_t dtype [T][B][2][4H] (gate activations)
  *   dout    dtype [T][B][2H]   dG_t dtype [T][B][2][4H]
  *   dg_state dtype [2 bufs][2][B][4H], dc_state f32 [2][B][H] (zero before the loop) */
 int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void* h_out, float* c_state,
                        const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t,
-                       float* cprev_t, float* acts_t, int dtype, void* stream);
+                       float* cprev_t, void* acts_t, int dtype, void* stream);
 int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* dc_state, const int* seq_len,
                        int s, int T, int B, int H, const void* dout, const float* cprev_t,
-                       const float* acts_t, void* dG_t, int dtype, void* stream);
+                       const void* acts_t, void* dG_t, int dtype, void* stream);
+/* Diagnostics: when buf != NULL every forward step kernel's workgroups write
+ * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
+int ocrk_lstm_debug_stamps(long long* buf);
 int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
-                  int T, int B, int H, void* out, void* hprev_t, float* cprev_t, float* acts_t, int dtype,
+                  int T, int B, int H, void* out, void* hprev_t, float* cprev_t, void* acts_t, int dtype,
                   void* stream);
 int ocrk_lstm_bwd(const void* wh, void* dg_state, float* dc_state, const int* seq_len, int T, int B, int H,
-                  const void* dout, const float* cprev_t, const float* acts_t, void* dG_t, int dtype,
+                  const void* dout, const float* cprev_t, const void* acts_t, void* dG_t, int dtype,
                   void* stream);
 
 /* ------------------------------------------------------- dense / generic

@@ -109,7 +109,7 @@ def test_bf16_train_step_close_to_fp32(cuda):
     from cnn_lstm_ctc_ocr_amd.train import Trainer
     losses = []
     for dt in (torch.float32, torch.bfloat16):
-        store, vals, img, widths, labels, T = _setup(cuda, dt, B=64, seed=5, sizes=(128, 128))
+        store, vals, img, widths, labels, T = _setup(cuda, dt, B=64, seed=5, sizes=(256, 256))
         tr = Trainer(store)
         l0 = tr.step(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), labels).item()
         l1 = tr.step(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), labels).item()

@@ -138,7 +138,7 @@ def test_bn_relu_pool(cuda, pool):
 def test_lstm_layer_fwd_bwd(cuda, dtype):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     rng = np.random.default_rng(5)
-    T, B, n_in, H = 9, 64, 64, 128
+    T, B, n_in, H = 9, 64, 64, 256
     x = rng.standard_normal((T, B, n_in)).astype(np.float32)
     seq = rng.integers(1, T + 1, B).astype(np.int32)
     seq[0] = T

@@ -1,0 +1,55 @@
+"""Micro-benchmark of the recurrent step kernels (diagnostics, not the product path)."""
+import sys, os, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cnn_lstm_ctc_ocr_amd import kernels as K, _lib
+
+def run(B, H=512, n_in=1024, T=125, reps=3, dt=torch.bfloat16):
+    dev = torch.device("cuda")
+    gx = torch.randn(T * B, 8 * H, device=dev)
+    whT = (torch.randn(2, 4 * H, H, device=dev) * 0.02).to(dt)
+    wh = (torch.randn(2, H, 4 * H, device=dev) * 0.02).to(dt)
+    seq = torch.full((B,), T, dtype=torch.int32, device=dev)
+    out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq, T, B, H, dt)
+    dout = torch.randn(T, B, 2 * H, device=dev).to(dt)
+    K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record()
+    for _ in range(reps):
+        K.lstm_fwd(gx, whT, seq, T, B, H, dt)
+    e[1].record()
+    for _ in range(reps):
+        K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    e[2].record()
+    torch.cuda.synchronize()
+    f = e[0].elapsed_time(e[1]) / reps / T * 1e3
+    b = e[1].elapsed_time(e[2]) / reps / T * 1e3
+    print(f"B={B:4d} H={H}: fwd step {f:7.2f} us   bwd step {b:7.2f} us", flush=True)
+
+for B in (64, 128, 256, 512):
+    run(B)
+
+# in-kernel stamps of one forward step (thread 0 of each workgroup, 100 MHz clock)
+if "--stamps" in sys.argv:
+    import numpy as np
+    B, H, T = 256, 512, 8
+    dev = torch.device("cuda")
+    dbg = torch.zeros(2 * 4 * 32 * 8, dtype=torch.int64, device=dev)
+    gx = torch.randn(T * B, 8 * H, device=dev)
+    whT = (torch.randn(2, 4 * H, H, device=dev) * 0.02).bfloat16()
+    seq = torch.full((B,), T, dtype=torch.int32, device=dev)
+    K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", _lib.ptr(dbg))
+    K.lstm_fwd(gx, whT, seq, 1, B, H, torch.bfloat16)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", None)
+    st = dbg.view(-1, 8)[:, :6].cpu().numpy().astype(np.float64) * 10.0   # ns
+    t0 = st[:, 0].min()
+    print("stamp (ns since first WG start): median / max over workgroups")
+    names = ["start", "gemm loads issued", "epilogue loads issued", "gemm done", "spill done", "end"]
+    for i, n in enumerate(names):
+        print(f"  {n:24s} {np.median(st[:, i] - t0):9.0f} {np.max(st[:, i] - t0):9.0f}")
+    d = st[:, 1:] - st[:, :-1]
+    for i in range(5):
+        print(f"  {names[i]} -> {names[i+1]}: median {np.median(d[:, i]):8.0f} ns")
