@@ -22,6 +22,17 @@ from .config import TRAIN
 from .model import convnet_layers, ctc_loss_layer, rnn_layers
 
 
+def allreduce_mean_scale(flat_grad, group=None):
+    """In-place SUM all-reduce of `flat_grad` across the process group (no-op
+    for a single process); returns 1/world_size."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    world = dist.get_world_size(group)
+    if world > 1:
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
+    return 1.0 / world
+
+
 class Trainer:
     def __init__(self, store, learning_rate=1e-4, momentum=0.9, decay_rate=0.9, decay_steps=2 ** 16,
                  decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0):
@@ -61,16 +72,19 @@ class Trainer:
         loss.backward()
         return loss
 
+    def reduce_gradients(self):
+        """Sum the flat gradient buffer over the data-parallel ranks (one RCCL
+        all-reduce); returns the factor that turns the sum into the mean."""
+        return allreduce_mean_scale(self.store.flat_grad, self.group)
+
     def apply_gradients(self):
         store = self.store
-        world = self.world_size()
-        if world > 1:
-            dist.all_reduce(store.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+        grad_scale = self.reduce_gradients()
         t = self.global_step + 1
         lr = self.learning_rate()
         lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
         K.adam_(store.flat, store.flat_grad, self.m, self.v, lr_t, self.beta1, self.beta2, self.eps,
-                grad_scale=1.0 / world)
+                grad_scale=grad_scale)
         store.bump()
         self.global_step += 1
 
