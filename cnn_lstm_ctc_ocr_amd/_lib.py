@@ -55,6 +55,9 @@ SIGNATURES = {
                               _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],
+    "ocrk_lstm_fwd_persistent_workspace_size": [_i32, _i32],
+    "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_debug_stamps": [_p],
     "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],

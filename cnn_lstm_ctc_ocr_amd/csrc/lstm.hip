@@ -366,9 +366,9 @@ lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT
 }
 
 // ------------------------------------------------------------------ C ABI
-static long long* g_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
+long long* g_lstm_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
 
-extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_dbg = buf; return OCRK_OK; }
+extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return OCRK_OK; }
 
 // Tile shapes: bf16 BR=64 x HU=16 (fwd K-chunk 128, bwd 256); f32 BR=32 x HU=8/16.
 #define FWD_BF16 bf16, 64, 16, 256
@@ -383,11 +383,11 @@ extern "C" int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* 
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 256 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 256 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 16, B / 64, 2);
-        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_dbg);
+        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
     } else {
         OCRK_REQUIRE(H % 64 == 0 && B % 32 == 0, "ocrk_lstm_fwd_step: f32 needs H %% 64 == 0 and B %% 32 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 8, B / 32, 2);
-        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>(gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, (float*)acts_t, g_dbg);
+        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>(gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, (float*)acts_t, g_lstm_dbg);
     }
     return ocrk::launch_status("ocrk_lstm_fwd_step");
 }

@@ -194,9 +194,45 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, out=None, ou
 
 
 # ------------------------------------------------------------------ LSTM
+_PERSISTENT = {}
+
+
+def lstm_persistent_ok(B, H, dtype):
+    """bf16 persistent time loop enabled (OCRK_LSTM_PERSISTENT=1) and usable (grid co-resident)?
+    Off by default: measured 14.1-14.5 us/step vs 11.4 us for the per-step kernels at B=256
+    (DESIGN.md section 5)."""
+    import os
+    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "0") != "1":
+        return False
+    key = (B, H)
+    if key not in _PERSISTENT:
+        _PERSISTENT[key] = bool(_lib.lib().ocrk_lstm_fwd_persistent_supported(B, H))
+    return _PERSISTENT[key]
+
+
+_ERR = {}
+
+
+def lstm_error_word(device):
+    """u32 device word the persistent kernels set when a hand-off wait times out."""
+    if device not in _ERR:
+        _ERR[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _ERR[device]
+
+
 def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
     _chk(gx, whT, seq_len)
     dev = gx.device
+    if lstm_persistent_ok(B, H, dtype):
+        out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+        hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+        cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
+        acts = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
+        nb = _lib.lib().ocrk_lstm_fwd_persistent_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        call("ocrk_lstm_fwd_persistent", ptr(gx), ptr(whT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
+             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(ws), nb, _stream(gx))
+        return out, hprev, cprev, acts
     h_state = torch.zeros(2, 2, B, H, dtype=dtype, device=dev)
     c_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
     out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)

@@ -140,6 +140,17 @@ int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void*
 int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* dc_state, const int* seq_len,
                        int s, int T, int B, int H, const void* dout, const float* cprev_t,
                        const void* acts_t, void* dG_t, int dtype, void* stream);
+/* Persistent forward time loop (bf16, H in {256, 512}, B % 32 == 0): ONE launch
+ * runs all T steps of both directions; W_h stays in registers, h is exchanged
+ * between co-resident workgroups through write-through stores and per-group
+ * counters. Same outputs as ocrk_lstm_fwd (h_state/c_state not needed).
+ * _supported() says whether the grid fits co-resident on this device; err
+ * (u32, device) is set non-zero if a hand-off wait timed out. */
+int ocrk_lstm_fwd_persistent_supported(int B, int H);
+size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
+int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const int* seq_len, int T, int B, int H,
+                             void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err, void* ws,
+                             size_t ws_bytes, void* stream);
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
  * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
 int ocrk_lstm_debug_stamps(long long* buf);

@@ -53,3 +53,56 @@ if "--stamps" in sys.argv:
     d = st[:, 1:] - st[:, :-1]
     for i in range(5):
         print(f"  {names[i]} -> {names[i+1]}: median {np.median(d[:, i]):8.0f} ns")
+
+if "--persistent" in sys.argv:
+    import numpy as np
+    for B in (64, 256):
+        H, T = 512, 125
+        dev = torch.device("cuda")
+        gx = torch.randn(T * B, 8 * H, device=dev)
+        whT = (torch.randn(2, 4 * H, H, device=dev) * 0.05).bfloat16()
+        seq = torch.randint(T // 2, T + 1, (B,), dtype=torch.int32, device=dev)
+        os.environ["OCRK_LSTM_PERSISTENT"] = "0"
+        K._PERSISTENT.clear()
+        ref = K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+        os.environ["OCRK_LSTM_PERSISTENT"] = "1"
+        K._PERSISTENT.clear()
+        print("persistent supported:", K.lstm_persistent_ok(B, H, torch.bfloat16))
+        got = K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+        torch.cuda.synchronize()
+        print("err word:", K.lstm_error_word(dev).item())
+        for name, a, b in zip(("out", "hprev", "cprev", "acts"), ref, got):
+            d = (a.float() - b.float()).abs().max().item()
+            print(f"  {name}: max |step-kernel - persistent| = {d:.3e}")
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record()
+        for _ in range(5):
+            K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+        e[1].record()
+        torch.cuda.synchronize()
+        print(f"B={B}: persistent fwd {e[0].elapsed_time(e[1]) / 5 / T * 1e3:.2f} us/step, err={K.lstm_error_word(dev).item()}")
+
+if "--pstamps" in sys.argv:
+    import numpy as np
+    os.environ["OCRK_LSTM_PERSISTENT"] = "1"
+    K._PERSISTENT.clear()
+    B, H, T = 256, 512, 125
+    dev = torch.device("cuda")
+    gx = torch.randn(T * B, 8 * H, device=dev)
+    whT = (torch.randn(2, 4 * H, H, device=dev) * 0.05).bfloat16()
+    seq = torch.full((B,), T, dtype=torch.int32, device=dev)
+    K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+    dbg = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", _lib.ptr(dbg))
+    K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", None)
+    st = dbg.view(-1, 8)[:, :7].cpu().numpy().astype(np.float64) * 10.0
+    names = ["top", "poll done", "h staged", "mfma done", "epilogue done", "drained", "signalled"]
+    t0 = st[:, 0].min()
+    for i, n in enumerate(names):
+        print(f"  {n:16s} median {np.median(st[:, i] - t0):8.0f}  max {np.max(st[:, i] - t0):8.0f} ns")
+    d = np.diff(st, axis=1)
+    for i in range(6):
+        print(f"  {names[i]:>14s} -> {names[i+1]:14s}: median {np.median(d[:, i]):7.0f} ns  max {np.max(d[:, i]):7.0f}")
