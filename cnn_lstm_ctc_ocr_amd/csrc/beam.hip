@@ -1,0 +1,381 @@
+// a11 -- CTC prefix beam search, tf.nn.ctc_beam_search_decoder with the
+// default scorer (src/weinman/test.py:84-88 beam 128 merge_repeated=True;
+// src/weinman/client.py:227-231 merge_repeated=False). [TF1]
+// ctc_beam_search.h Step()/TopPaths() semantics, restated in
+// oracle/ref_graph.py:ctc_beam_search_single.
+//
+// One 256-thread workgroup per sequence; the beam lives in LDS.
+//   * A prefix is identified by a 64-bit hash of its label sequence (TF keeps
+//     one tree node per prefix; "parent active" and "child already in the
+//     beam" are hash lookups against the current beam).
+//   * TF's bounded top-N with strict '>' against the bottom and the
+//     parent-candidate gate is exactly "top-K of {beams with updated
+//     probabilities} U {new children}, ordered by total desc, ties by TF's
+//     insertion order (beams in rank order, then children by parent rank and
+//     label)". Each item gets a 47-bit key (total desc : insertion order) and
+//     a block radix-select finds the K-th smallest key; no candidate list is
+//     materialised.
+//   * Children of a parent are enumerated over the labels sorted by logit
+//     (only the best K can matter) plus the parent's own label, whose
+//     probability extends from the parent's blank-ending probability.
+//   * Emitted prefixes are appended to a per-sequence arena (parent id,
+//     label) in global memory; TopPaths walks it back with LabelSeq's merge.
+#include "common.h"
+
+namespace {
+
+constexpr int BEAM_MAX_K = 128;
+constexpr int BEAM_MAX_C = 128;
+constexpr int BEAM_THREADS = 256;
+constexpr int ORDER_BITS = 15;          // insertion order < n + n*C <= 16512
+constexpr uint64_t ROOT_HASH = 0x6a09e667f3bcc909ull;
+
+__device__ __forceinline__ uint64_t child_hash(uint64_t parent, int label) {
+    uint64_t z = parent ^ ((uint64_t)(label + 1) * 0x9E3779B97F4A7C15ull);
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// [TF1] ctc_loss_util.h LogSumExp.
+__device__ __forceinline__ float log_sum_exp(float a, float b) {
+    if (a == -INFINITY) return b;
+    if (b == -INFINITY) return a;
+    return a > b ? a + log1pf(expf(b - a)) : b + log1pf(expf(a - b));
+}
+
+// Larger float -> smaller key.
+__device__ __forceinline__ uint64_t desc_bits(float f) {
+    uint32_t u = __float_as_uint(f);
+    uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return (uint64_t)(~ord);
+}
+
+struct BeamLds {
+    float x[BEAM_MAX_C];                 // log-softmax row
+    int slot_label[BEAM_MAX_C];          // labels sorted by x desc (stable)
+    int label_slot[BEAM_MAX_C];
+    // current beam (sorted by total desc); o* = newp of the previous step
+    uint64_t h[BEAM_MAX_K], ph[BEAM_MAX_K];
+    int lab[BEAM_MAX_K], id[BEAM_MAX_K], pidx[BEAM_MAX_K];
+    float ot[BEAM_MAX_K], ob[BEAM_MAX_K], ol[BEAM_MAX_K];
+    float nt[BEAM_MAX_K], nb[BEAM_MAX_K], nl[BEAM_MAX_K];   // loop-1 updates
+    uint32_t act[BEAM_MAX_K][BEAM_MAX_C / 32];             // child label already a beam
+    // next beam staging
+    uint64_t h2[BEAM_MAX_K], ph2[BEAM_MAX_K];
+    int lab2[BEAM_MAX_K], id2[BEAM_MAX_K];
+    float t2[BEAM_MAX_K], b2[BEAM_MAX_K], l2[BEAM_MAX_K];
+    uint64_t sel[BEAM_MAX_K];
+    uint32_t hist[BEAM_THREADS / 64][256];
+    uint32_t wsum[BEAM_THREADS / 64];
+    float red[BEAM_THREADS / 64];
+    uint64_t prefix;
+    uint32_t kk, n_sel, n_valid;
+    int n, next_id;
+    float tau;
+};
+
+__device__ __forceinline__ int block_sync_max_f(BeamLds& s, float v, float* out) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s.red[w] = v;
+    __syncthreads();
+    float m = s.red[0];
+#pragma unroll
+    for (int i = 1; i < BEAM_THREADS / 64; ++i) m = fmaxf(m, s.red[i]);
+    *out = m;
+    __syncthreads();
+    return 0;
+}
+
+// Item i of the candidate set: beams [0, n), then n*M children (parent r,
+// slot q): slot q < Ls is the q-th best label, slot Ls is the parent's label.
+__device__ __forceinline__ bool beam_item(const BeamLds& s, int i, int n, int M, int Ls, int C,
+                                          uint64_t* key) {
+    if (i < n) {
+        *key = (desc_bits(s.nt[i]) << ORDER_BITS) | (uint64_t)i;
+        return true;
+    }
+    const int q = i - n;
+    const int r = q / M, slot = q - r * M;
+    const int pl = s.lab[r];
+    int l;
+    if (slot < Ls) {
+        l = s.slot_label[slot];
+    } else {
+        if (pl < 0 || s.label_slot[pl] < Ls) return false;
+        l = pl;
+    }
+    if ((s.act[r][l >> 5] >> (l & 31)) & 1u) return false;
+    const float v = s.x[l] + (l == pl ? s.ob[r] : s.ot[r]);
+    if (!(v > s.tau)) return false;
+    *key = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + r * C + l);
+    return true;
+}
+
+__global__ void __launch_bounds__(BEAM_THREADS)
+ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_len, int T, int B, int C,
+                int K, int top_paths, int merge_repeated, int64_t* __restrict__ out,
+                int* __restrict__ out_len, float* __restrict__ log_probs, int2* __restrict__ arena_all) {
+    __shared__ BeamLds s;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int L = min(max(seq_len[b], 0), T);
+    const int blank = C - 1;
+    const int Ls = min(K, C - 1);
+    const int M = Ls + 1;
+    int2* arena = arena_all + (size_t)b * (1 + (size_t)T * K);
+
+    if (tid == 0) {
+        s.h[0] = ROOT_HASH; s.ph[0] = 0; s.lab[0] = -1; s.id[0] = 0;
+        s.ot[0] = 0.f; s.ob[0] = 0.f; s.ol[0] = -INFINITY;
+        s.n = 1; s.next_id = 1;
+        arena[0] = make_int2(-1, -1);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < L; ++t) {
+        // ---- input row -> log-softmax (Step(): max removed, then norm_offset)
+        const float* row = logits + ((size_t)t * B + b) * C;
+        float v = tid < C ? row[tid] : -INFINITY;
+        float m;
+        block_sync_max_f(s, v, &m);
+        float e = tid < C ? expf(v - m) : 0.f;
+        e = wave_sum(e);
+        if (lane == 0) s.red[w] = e;
+        __syncthreads();
+        float z = 0.f;
+#pragma unroll
+        for (int i = 0; i < BEAM_THREADS / 64; ++i) z += s.red[i];
+        const float norm = logf(z);
+        if (tid < C) s.x[tid] = (v - m) - norm;
+        const int n = s.n;
+        __syncthreads();
+
+        // ---- label order, parent lookup, clear child tables
+        if (tid < C && tid != blank) {
+            const float xl = s.x[tid];
+            int rank = 0;
+            for (int j = 0; j < C; ++j) {
+                if (j == blank) continue;
+                const float xj = s.x[j];
+                rank += (xj > xl) || (xj == xl && j < tid);
+            }
+            s.slot_label[rank] = tid;
+            s.label_slot[tid] = rank;
+        }
+        if (tid < n) {
+            int p = -1;
+            if (s.lab[tid] >= 0) {
+                const uint64_t want = s.ph[tid];
+                for (int j = 0; j < n; ++j)
+                    if (s.h[j] == want) { p = j; break; }
+            }
+            s.pidx[tid] = p;
+#pragma unroll
+            for (int q = 0; q < BEAM_MAX_C / 32; ++q) s.act[tid][q] = 0u;
+        }
+        __syncthreads();
+
+        // ---- loop 1: extend every beam by blank / its own label
+        float my_nt = INFINITY;
+        if (tid < n) {
+            const int l = s.lab[tid], p = s.pidx[tid];
+            float nl = s.ol[tid];
+            if (l >= 0) {
+                if (p >= 0) {
+                    const float prev = (l == s.lab[p]) ? s.ob[p] : s.ot[p];
+                    nl = log_sum_exp(nl, prev);
+                }
+                nl += s.x[l];
+                if (p >= 0) atomicOr(&s.act[p][l >> 5], 1u << (l & 31));
+            }
+            const float nb = s.ot[tid] + s.x[blank];
+            my_nt = log_sum_exp(nb, nl);
+            s.nl[tid] = nl; s.nb[tid] = nb; s.nt[tid] = my_nt;
+        }
+        // tau: with a full beam no child at or below the weakest updated beam
+        // can enter (the beam wins the tie on insertion order).
+        float mn = -wave_max(-my_nt);
+        if (lane == 0) s.red[w] = mn;
+        __syncthreads();
+        if (tid == 0) {
+            float q = s.red[0];
+#pragma unroll
+            for (int i = 1; i < BEAM_THREADS / 64; ++i) q = fminf(q, s.red[i]);
+            s.tau = (n == K) ? q : -INFINITY;
+            s.prefix = 0; s.kk = 0; s.n_sel = 0;
+        }
+        __syncthreads();
+
+        // ---- radix select of the K-th smallest key (47 bits, 8-bit digits)
+        const int n_items = n + n * M;
+        uint64_t pmask = 0;
+        bool take_all = false;
+        for (int shift = 40; shift >= 0; shift -= 8) {
+            for (int i = tid; i < (BEAM_THREADS / 64) * 256; i += BEAM_THREADS) (&s.hist[0][0])[i] = 0u;
+            __syncthreads();
+            const uint64_t prefix = s.prefix;
+            for (int i = tid; i < n_items; i += BEAM_THREADS) {
+                uint64_t key;
+                if (beam_item(s, i, n, M, Ls, C, &key) && (key & pmask) == prefix)
+                    atomicAdd(&s.hist[w][(key >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            uint32_t c = 0;
+#pragma unroll
+            for (int q = 0; q < BEAM_THREADS / 64; ++q) c += s.hist[q][tid];
+            // block inclusive scan over the 256 digits
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                uint32_t u = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += u;
+            }
+            if (lane == 63) s.wsum[w] = incl;
+            __syncthreads();
+            uint32_t base = 0;
+            for (int q = 0; q < w; ++q) base += s.wsum[q];
+            incl += base;
+            const uint32_t excl = incl - c;
+            uint32_t total = 0;
+#pragma unroll
+            for (int q = 0; q < BEAM_THREADS / 64; ++q) total += s.wsum[q];
+            if (shift == 40) {
+                if (total <= (uint32_t)K) take_all = true;   // uniform across the block
+                if (tid == 0) { s.n_valid = total; s.kk = min(total, (uint32_t)K); }
+                __syncthreads();
+            }
+            if (take_all) break;
+            const uint32_t kk = s.kk;
+            __syncthreads();
+            if (c > 0 && excl < kk && kk <= incl) {
+                s.prefix = prefix | ((uint64_t)tid << shift);
+                s.kk = kk - excl;
+            }
+            pmask |= (uint64_t)255u << shift;
+            __syncthreads();
+        }
+        const uint64_t theta = take_all ? ~0ull : s.prefix;
+
+        // ---- gather the selected keys and rank them
+        for (int i = tid; i < n_items; i += BEAM_THREADS) {
+            uint64_t key;
+            if (beam_item(s, i, n, M, Ls, C, &key) && key <= theta) {
+                uint32_t pos = atomicAdd(&s.n_sel, 1u);
+                if (pos < (uint32_t)BEAM_MAX_K) s.sel[pos] = key;
+            }
+        }
+        __syncthreads();
+        const int n_sel = min((int)s.n_sel, K);
+        uint64_t my_key = ~0ull;
+        int my_rank = 0;
+        if (tid < n_sel) {
+            my_key = s.sel[tid];
+            for (int j = 0; j < n_sel; ++j) my_rank += s.sel[j] < my_key;
+        }
+        // new prefixes get arena ids in rank order
+        const int order = tid < n_sel ? (int)(my_key & ((1u << ORDER_BITS) - 1)) : 0;
+        const bool is_new = tid < n_sel && order >= n;
+        __syncthreads();
+        if (tid < n_sel) s.sel[my_rank] = my_key;
+        __syncthreads();
+        {
+            const uint64_t k2 = tid < n_sel ? s.sel[tid] : 0;
+            const int o2 = (int)(k2 & ((1u << ORDER_BITS) - 1));
+            const bool new2 = tid < n_sel && o2 >= n;
+            const uint64_t bal = __ballot(new2);
+            const int before = __popcll(bal & ((1ull << lane) - 1ull));
+            if (lane == 0) s.wsum[w] = __popcll(bal);
+            __syncthreads();
+            int off = s.next_id;
+            for (int q = 0; q < w; ++q) off += s.wsum[q];
+            if (tid < n_sel) {
+                if (!new2) {
+                    const int j = o2;
+                    s.h2[tid] = s.h[j]; s.ph2[tid] = s.ph[j]; s.lab2[tid] = s.lab[j]; s.id2[tid] = s.id[j];
+                    s.t2[tid] = s.nt[j]; s.b2[tid] = s.nb[j]; s.l2[tid] = s.nl[j];
+                } else {
+                    const int q = o2 - n, r = q / C, l = q - r * C;
+                    const int nid = off + before;
+                    const float val = s.x[l] + (l == s.lab[r] ? s.ob[r] : s.ot[r]);
+                    s.h2[tid] = child_hash(s.h[r], l); s.ph2[tid] = s.h[r]; s.lab2[tid] = l;
+                    s.id2[tid] = nid;
+                    s.t2[tid] = val; s.b2[tid] = -INFINITY; s.l2[tid] = val;
+                    arena[nid] = make_int2(s.id[r], l);
+                }
+            }
+            (void)is_new;
+            __syncthreads();
+            if (tid == 0) {
+                int nn = 0;
+#pragma unroll
+                for (int q = 0; q < BEAM_THREADS / 64; ++q) nn += s.wsum[q];
+                s.next_id += nn;
+                s.n = n_sel;
+            }
+            if (tid < n_sel) {
+                s.h[tid] = s.h2[tid]; s.ph[tid] = s.ph2[tid]; s.lab[tid] = s.lab2[tid]; s.id[tid] = s.id2[tid];
+                s.ot[tid] = s.t2[tid]; s.ob[tid] = s.b2[tid]; s.ol[tid] = s.l2[tid];
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---- TopPaths: walk the arena back, LabelSeq(merge_repeated)
+    const int n = s.n;
+    for (int k = tid; k < top_paths; k += BEAM_THREADS) {
+        int64_t* o = out + ((size_t)k * B + b) * T;
+        int len = 0;
+        if (k < n) {
+            int e = s.id[k], prev = -1;
+            while (e > 0) {
+                const int2 a = arena[e];
+                if (!merge_repeated || a.y != prev) ++len;
+                prev = a.y;
+                e = a.x;
+            }
+            e = s.id[k]; prev = -1;
+            int pos = len;
+            while (e > 0) {
+                const int2 a = arena[e];
+                if (!merge_repeated || a.y != prev) o[--pos] = a.y;
+                prev = a.y;
+                e = a.x;
+            }
+            log_probs[(size_t)b * top_paths + k] = s.ot[k];
+        } else {
+            log_probs[(size_t)b * top_paths + k] = -INFINITY;
+        }
+        for (int i = len; i < T; ++i) o[i] = -1;
+        out_len[(size_t)k * B + b] = len;
+    }
+}
+
+}  // namespace
+
+extern "C" size_t ocrk_ctc_beam_workspace_size(int T, int B, int beam_width) {
+    if (T < 0 || B < 0 || beam_width < 1) return 0;
+    return (size_t)B * (1 + (size_t)T * beam_width) * sizeof(int2);
+}
+
+extern "C" int ocrk_ctc_beam_decode(const float* logits, const int* seq_len, int T, int B, int C,
+                                    int beam_width, int top_paths, int merge_repeated, int64_t* out,
+                                    int* out_len, float* log_probs, void* ws, size_t ws_bytes,
+                                    void* stream) {
+    OCRK_REQUIRE(T > 0 && B >= 0 && C >= 2 && C <= BEAM_MAX_C,
+                 "ocrk_ctc_beam_decode: bad sizes T=%d B=%d C=%d (C <= %d)", T, B, C, BEAM_MAX_C);
+    OCRK_REQUIRE(beam_width >= 1 && beam_width <= BEAM_MAX_K,
+                 "ocrk_ctc_beam_decode: beam_width %d not in [1, %d]", beam_width, BEAM_MAX_K);
+    OCRK_REQUIRE(top_paths >= 1 && top_paths <= beam_width,
+                 "ocrk_ctc_beam_decode: top_paths %d not in [1, beam_width]", top_paths);
+    if (B == 0) return OCRK_OK;
+    OCRK_REQUIRE(logits && seq_len && out && out_len && log_probs && ws,
+                 "ocrk_ctc_beam_decode: null pointer");
+    OCRK_REQUIRE(ws_bytes >= ocrk_ctc_beam_workspace_size(T, B, beam_width),
+                 "ocrk_ctc_beam_decode: workspace too small");
+    ctc_beam_kernel<<<B, BEAM_THREADS, 0, ocrk::as_stream(stream)>>>(
+        logits, seq_len, T, B, C, beam_width, top_paths, merge_repeated, out, out_len, log_probs,
+        reinterpret_cast<int2*>(ws));
+    return ocrk::launch_status("ocrk_ctc_beam_decode");
+}

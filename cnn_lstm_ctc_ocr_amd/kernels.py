@@ -355,3 +355,36 @@ def ctc_greedy_decode(logits, seq_len, merge_repeated=True):
     call("ocrk_ctc_greedy_decode", ptr(logits), ptr(seq_len), T, B, C, int(bool(merge_repeated)),
          ptr(out), ptr(out_len), ptr(neg), _stream(logits))
     return out, out_len, neg
+
+
+def ctc_beam_decode(logits, seq_len, beam_width=100, top_paths=1, merge_repeated=True):
+    """Prefix beam search. Returns (out i64 [top_paths,B,T] -1 padded,
+    out_len i32 [top_paths,B], log_probs f32 [B,top_paths])."""
+    if logits.dtype != torch.float32:
+        raise TypeError("ctc_beam_decode takes float32 logits")
+    _chk(logits, seq_len)
+    T, B, C = logits.shape
+    dev = logits.device
+    out = torch.empty(top_paths, B, T, dtype=torch.int64, device=dev)
+    out_len = torch.empty(top_paths, B, dtype=torch.int32, device=dev)
+    logp = torch.empty(B, top_paths, dtype=torch.float32, device=dev)
+    nb = _lib.lib().ocrk_ctc_beam_workspace_size(T, B, int(beam_width))
+    ws = _ws(nb, dev)
+    call("ocrk_ctc_beam_decode", ptr(logits), ptr(seq_len), T, B, C, int(beam_width), int(top_paths),
+         int(bool(merge_repeated)), ptr(out), ptr(out_len), ptr(logp), ptr(ws), nb, _stream(logits))
+    return out, out_len, logp
+
+
+def edit_distance(hyp, hyp_len, labels, label_len, totals=None):
+    """Levenshtein distance per row (tf.edit_distance normalize=False).
+    hyp i64 [B,S] with hyp_len i32 [B]; labels i32 [B,L] with label_len i32 [B].
+    Returns dist f32 [B]; accumulates {sum, nonzero, sum label_len} into
+    `totals` (i32 [3]) when given."""
+    _chk(hyp, hyp_len, labels, label_len)
+    B = hyp.shape[0]
+    dist = torch.empty(B, dtype=torch.float32, device=hyp.device)
+    if totals is not None:
+        _chk(totals)
+    call("ocrk_edit_distance", ptr(hyp), ptr(hyp_len), hyp.shape[1], ptr(labels), ptr(label_len),
+         labels.shape[1], B, ptr(dist), ptr(totals) if totals is not None else None, _stream(hyp))
+    return dist

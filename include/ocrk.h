@@ -70,6 +70,25 @@ int ocrk_ctc_greedy_decode(const float* logits, const int* seq_len, int T, int B
                            void* stream);
 
 
+/* a11 -- tf.nn.ctc_beam_search_decoder(logits, seq_len, beam_width, top_paths, merge_repeated)
+ * with the default scorer (src/weinman/test.py:84-88 beam 128, merge_repeated=1;
+ * src/weinman/client.py:227-231 merge_repeated=0). logits f32 [T, B, C] (blank = C-1, C <= 128),
+ * beam_width <= 128, top_paths <= beam_width. out i64 [top_paths][B][T] (labels then -1),
+ * out_len i32 [top_paths][B], log_probs f32 [B][top_paths] (log-softmax path scores).
+ * ws >= ocrk_ctc_beam_workspace_size(T, B, beam_width) bytes. */
+size_t ocrk_ctc_beam_workspace_size(int T, int B, int beam_width);
+int ocrk_ctc_beam_decode(const float* logits, const int* seq_len, int T, int B, int C, int beam_width,
+                         int top_paths, int merge_repeated, int64_t* out, int* out_len, float* log_probs,
+                         void* ws, size_t ws_bytes, void* stream);
+
+/* a14 -- tf.edit_distance(hypothesis, label, normalize=False) (src/weinman/test.py:90) per row:
+ * hyp i64 [B][hyp_stride] with hyp_len i32 [B]; label i32 [B][label_stride] (<= 256) with
+ * label_len i32 [B]. dist f32 [B] (or NULL); totals i32[3] (or NULL) accumulates
+ * {sum edit, count(edit > 0), sum label_len} -- label_error / sequence_error of test.py:91-99. */
+int ocrk_edit_distance(const int64_t* hyp, const int* hyp_len, int hyp_stride, const int* label,
+                       const int* label_len, int label_stride, int B, float* dist, int* totals,
+                       void* stream);
+
 /* ------------------------------------------------------------- conv tower
  * a1+a2 conv1 -- conv_layer(layer_params[0]) (src/weinman/model.py:84-109,134):
  * 3x3 'valid', Cin = 1, bias + ReLU, fused with the uint8 preprocess of

@@ -496,3 +496,118 @@ def adam_update(p, g, m, v, lr, t, beta1=0.9, beta2=0.999, eps=1e-8):
     v = v + (g * g - v) * (1 - beta2)
     p = p - lr_t * m / (np.sqrt(v) + eps)
     return p, m, v
+
+
+# --------------------------------------------------------- a11 beam decode
+class _BeamEntry:
+    """[TF1] ctc_beam_search.h BeamEntry: prefix-tree node with (total, blank,
+    label) log-probabilities at t-1 (oldp) and t (newp)."""
+    __slots__ = ("parent", "label", "children", "oldp", "newp")
+
+    def __init__(self, parent, label):
+        self.parent, self.label, self.children = parent, label, None
+        self.oldp = [-np.inf, -np.inf, -np.inf]     # total, blank, label
+        self.newp = [-np.inf, -np.inf, -np.inf]
+
+    def active(self):
+        return self.newp[0] != -np.inf
+
+    def label_seq(self, merge_repeated):
+        out, prev, e = [], -1, self
+        while e.parent is not None:
+            if not merge_repeated or e.label != prev:
+                out.append(e.label)
+            prev = e.label
+            e = e.parent
+        return out[::-1]
+
+
+def _lse(a, b):
+    if a == -np.inf:
+        return b
+    if b == -np.inf:
+        return a
+    m = max(a, b)
+    return m + np.log1p(np.exp(-abs(a - b)))
+
+
+def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True, blank=None):
+    """One sequence of [TF1] CTCBeamSearchDecoder with the default scorer
+    (test.py:84-88 beam 128; client.py:227-231 merge_repeated=False).
+    logits [T, C] (already cut to seq_len). Step() subtracts the row max only
+    (no log-softmax); leaves are a bounded top-N by newp.total with strict '>'
+    against the bottom; ties keep the earlier insertion. Returns (paths,
+    log_probs)."""
+    T, C = logits.shape
+    blank = C - 1 if blank is None else blank
+    root = _BeamEntry(None, -1)
+    root.newp = [0.0, 0.0, -np.inf]
+    leaves = [root]                        # kept sorted by newp.total desc (stable)
+
+    def bottom():
+        return leaves[-1]
+
+    def push(e):                           # TopN push: insert keeping descending, stable
+        i = len(leaves)
+        while i > 0 and leaves[i - 1].newp[0] < e.newp[0]:
+            i -= 1
+        leaves.insert(i, e)
+        if len(leaves) > beam_width:
+            leaves.pop()
+
+    for t in range(T):
+        x = logits[t].astype(np.float64)
+        x = x - x.max()
+        x = x - np.log(np.exp(x).sum())
+        branches = list(leaves)            # Extract(): descending newp.total
+        leaves = []
+        for b in branches:
+            b.oldp = list(b.newp)
+        for b in branches:
+            if b.parent is not None:
+                if b.parent.active():
+                    prev = b.parent.oldp[1] if b.label == b.parent.label else b.parent.oldp[0]
+                    b.newp[2] = _lse(b.newp[2], prev)
+                b.newp[2] += x[b.label]
+            b.newp[1] = b.oldp[0] + x[blank]
+            b.newp[0] = _lse(b.newp[1], b.newp[2])
+            push(b)
+
+        def is_candidate(p):
+            return p[0] > -np.inf and (len(leaves) < beam_width or p[0] > bottom().newp[0])
+
+        for b in branches:
+            if not is_candidate(b.oldp):
+                continue
+            if b.children is None:
+                b.children = [_BeamEntry(b, l) for l in range(C) if l != blank]
+            for c in b.children:
+                if c.active():
+                    continue
+                c.newp[1] = -np.inf
+                prev = b.oldp[1] if c.label == b.label else b.oldp[0]
+                c.newp[2] = x[c.label] + prev
+                c.newp[0] = c.newp[2]
+                if is_candidate(c.newp):
+                    if len(leaves) == beam_width:
+                        bottom().newp = [-np.inf, -np.inf, -np.inf]
+                    push(c)
+                else:
+                    c.oldp = [-np.inf, -np.inf, -np.inf]
+                    c.newp = [-np.inf, -np.inf, -np.inf]
+    top = leaves[:top_paths]
+    return [e.label_seq(merge_repeated) for e in top], [e.newp[0] for e in top]
+
+
+def ctc_beam_search_decode(logits, seq_len, beam_width=100, top_paths=1, merge_repeated=True):
+    """Batched tf.nn.ctc_beam_search_decoder: per path k a list of B label
+    sequences, and log_probabilities [B, top_paths]."""
+    T, B, C = logits.shape
+    paths = [[None] * B for _ in range(top_paths)]
+    logp = np.full((B, top_paths), -np.inf)
+    for b in range(B):
+        ps, lps = ctc_beam_search_single(logits[:int(seq_len[b]), b], beam_width, top_paths, merge_repeated)
+        for k in range(top_paths):
+            paths[k][b] = ps[k] if k < len(ps) else []
+            logp[b, k] = lps[k] if k < len(lps) else -np.inf
+    return paths, logp

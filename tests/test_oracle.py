@@ -296,6 +296,52 @@ def test_greedy_all_zero_logits_emit_label_zero():
     assert seqs == [[0]]
 
 
+def _best_labeling(logits, blank):
+    import itertools
+    T, C = logits.shape
+    best = None
+    for L in range(T + 1):
+        for lab in itertools.product([c for c in range(C) if c != blank], repeat=L):
+            if G.ctc_required_time(lab) > T:
+                continue
+            lp = -G.ctc_loss_single(logits, list(lab), blank)[0]
+            if best is None or lp > best[0]:
+                best = (lp, list(lab))
+    return best
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_beam_search_exhaustive_is_exact_argmax(seed):
+    """With a beam wider than every prefix, prefix beam search is exact: the
+    top path is the most probable labeling and its score is log p(labeling)."""
+    rng = np.random.default_rng(seed)
+    lg = rng.standard_normal((5, 3)) * 2
+    lp, lab = _best_labeling(lg, 2)
+    paths, lps = G.ctc_beam_search_single(lg, beam_width=64, merge_repeated=False)
+    assert paths[0] == lab
+    assert abs(lps[0] - lp) < 1e-9
+
+
+def test_beam_search_labelseq_merge_quirk():
+    """[TF1] LabelSeq(merge_repeated=True) also merges equal labels separated
+    by a blank in the prefix (A B * B -> A B); merge_repeated=False keeps them."""
+    hi, lo = 8.0, -8.0
+    lg = np.full((4, 3), lo)
+    lg[0, 0] = lg[1, 1] = lg[2, 2] = lg[3, 1] = hi          # A B blank B
+    assert G.ctc_beam_search_single(lg, 8, merge_repeated=False)[0][0] == [0, 1, 1]
+    assert G.ctc_beam_search_single(lg, 8, merge_repeated=True)[0][0] == [0, 1]
+    assert G.ctc_greedy_decode(lg[:, None, :], np.array([4]), blank=2)[0] == [[0, 1, 1]]
+
+
+def test_beam_search_top_paths_sorted_and_empty_sequence():
+    rng = np.random.default_rng(3)
+    lg = rng.standard_normal((6, 5))
+    paths, lps = G.ctc_beam_search_single(lg, 10, top_paths=4)
+    assert len(paths) == 4 and all(a >= b for a, b in zip(lps, lps[1:]))
+    paths, lps = G.ctc_beam_search_single(lg[:0], 10)
+    assert paths == [[]] and lps == [0.0]
+
+
 def test_edit_distance_kat():
     assert G.edit_distance([1, 2, 3], [1, 2, 3]) == 0
     assert G.edit_distance([1, 3], [1, 2, 3]) == 1
