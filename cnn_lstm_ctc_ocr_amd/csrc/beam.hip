@@ -8,16 +8,20 @@
 //   * A prefix is identified by a 64-bit hash of its label sequence (TF keeps
 //     one tree node per prefix; "parent active" and "child already in the
 //     beam" are hash lookups against the current beam).
-//   * TF's bounded top-N with strict '>' against the bottom and the
-//     parent-candidate gate is exactly "top-K of {beams with updated
-//     probabilities} U {new children}, ordered by total desc, ties by TF's
-//     insertion order (beams in rank order, then children by parent rank and
-//     label)". Each item gets a 47-bit key (total desc : insertion order) and
-//     a block radix-select finds the K-th smallest key; no candidate list is
-//     materialised.
-//   * Children of a parent are enumerated over the labels sorted by logit
-//     (only the best K can matter) plus the parent's own label, whose
-//     probability extends from the parent's blank-ending probability.
+//   * TF's bounded top-N with strict '>' against the bottom is "top-K of
+//     {beams with updated probabilities} U {new children}, ordered by total
+//     desc, ties by TF's insertion order (beams in rank order, then children
+//     by parent rank and label)" -- except for one order-dependent effect:
+//     when beam j has been pushed out of the top-N before its parent p (ranked
+//     above j) reaches label(j) in its child loop, TF re-offers j as a new
+//     child, rejects it and resets j.oldp, so j's own children are never
+//     expanded this step ("wiped"). A wave-0 pass over parent ranks decides
+//     the wiped beams by counting, for each such (p, j), the items offered
+//     before that moment that beat j (sorted-logit binary searches per
+//     branch); the gate "p.oldp.total > bottom" is the same count.
+//   * The selection itself gives each item a 47-bit key (total desc :
+//     insertion order) and a block radix-select finds the K-th smallest key;
+//     no candidate list is materialised.
 //   * Emitted prefixes are appended to a per-sequence arena (parent id,
 //     label) in global memory; TopPaths walks it back with LabelSeq's merge.
 #include "common.h"
@@ -54,11 +58,11 @@ __device__ __forceinline__ uint64_t desc_bits(float f) {
 
 struct BeamLds {
     float x[BEAM_MAX_C];                 // log-softmax row
-    int slot_label[BEAM_MAX_C];          // labels sorted by x desc (stable)
-    int label_slot[BEAM_MAX_C];
+    float xs[BEAM_MAX_C];                // non-blank x sorted desc (wipe-pass counts)
     // current beam (sorted by total desc); o* = newp of the previous step
     uint64_t h[BEAM_MAX_K], ph[BEAM_MAX_K];
     int lab[BEAM_MAX_K], id[BEAM_MAX_K], pidx[BEAM_MAX_K];
+    int has_kid[BEAM_MAX_K], wiped[BEAM_MAX_K];
     float ot[BEAM_MAX_K], ob[BEAM_MAX_K], ol[BEAM_MAX_K];
     float nt[BEAM_MAX_K], nb[BEAM_MAX_K], nl[BEAM_MAX_K];   // loop-1 updates
     uint32_t act[BEAM_MAX_K][BEAM_MAX_C / 32];             // child label already a beam
@@ -89,29 +93,70 @@ __device__ __forceinline__ int block_sync_max_f(BeamLds& s, float v, float* out)
     return 0;
 }
 
-// Item i of the candidate set: beams [0, n), then n*M children (parent r,
-// slot q): slot q < Ls is the q-th best label, slot Ls is the parent's label.
-__device__ __forceinline__ bool beam_item(const BeamLds& s, int i, int n, int M, int Ls, int C,
-                                          uint64_t* key) {
+// Item i of the candidate set: beams [0, n), then n*(C-1) children
+// (parent r, label l) -- skipped when l is already a beam, r was wiped, or
+// the total cannot beat tau.
+__device__ __forceinline__ bool beam_item(const BeamLds& s, int i, int n, int C, uint64_t* key) {
     if (i < n) {
         *key = (desc_bits(s.nt[i]) << ORDER_BITS) | (uint64_t)i;
         return true;
     }
     const int q = i - n;
-    const int r = q / M, slot = q - r * M;
-    const int pl = s.lab[r];
-    int l;
-    if (slot < Ls) {
-        l = s.slot_label[slot];
-    } else {
-        if (pl < 0 || s.label_slot[pl] < Ls) return false;
-        l = pl;
-    }
+    const int r = q / (C - 1), l = q - r * (C - 1);
+    if (s.wiped[r]) return false;
     if ((s.act[r][l >> 5] >> (l & 31)) & 1u) return false;
-    const float v = s.x[l] + (l == pl ? s.ob[r] : s.ot[r]);
+    const float v = s.x[l] + (l == s.lab[r] ? s.ob[r] : s.ot[r]);
     if (!(v > s.tau)) return false;
     *key = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + r * C + l);
     return true;
+}
+
+// Wave-0 helper: number of offered items that beat `thr` (total >= thr when
+// ge, else > thr; beams i < j_rank win a tie at equal totals) among: every
+// beam's updated entry, all children of the unwiped branches ranked before
+// p, and p's children with label < l_lim.
+__device__ int count_better(const BeamLds& s, float thr, bool ge, int j_rank, int p, int l_lim, int n,
+                            int C, int lane) {
+    const int nl = C - 1;
+    int c = 0;
+    for (int i = lane; i < n; i += 64) {
+        const float v = s.nt[i];
+        c += ge ? (v >= thr) : (v > thr || (v == thr && i < j_rank));
+        // active child i of an earlier branch is counted above as a beam, not as a child
+        const int r = s.pidx[i];
+        if (r >= 0 && r < p && !s.wiped[r] && s.lab[i] != s.lab[r]) {
+            const float cv = s.x[s.lab[i]] + s.ot[r];
+            c -= ge ? (cv >= thr) : (cv > thr);
+        }
+    }
+    for (int r = lane; r < p; r += 64) {
+        if (s.wiped[r]) continue;
+        const float o = s.ot[r];
+        int lo = 0, hi = nl;                               // first slot failing the predicate
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const float v = s.xs[mid] + o;
+            if (ge ? (v >= thr) : (v > thr)) lo = mid + 1; else hi = mid;
+        }
+        c += lo;
+        const int pl = s.lab[r];
+        if (pl >= 0) {                                     // own label extends from the blank-ending prob
+            const float vo = s.x[pl] + o;
+            c -= ge ? (vo >= thr) : (vo > thr);
+            if (!((s.act[r][pl >> 5] >> (pl & 31)) & 1u)) {
+                const float vb = s.x[pl] + s.ob[r];
+                c += ge ? (vb >= thr) : (vb > thr);
+            }
+        }
+    }
+    for (int l = lane; l < l_lim; l += 64) {
+        if ((s.act[p][l >> 5] >> (l & 31)) & 1u) continue;
+        const float v = s.x[l] + (l == s.lab[p] ? s.ob[p] : s.ot[p]);
+        c += ge ? (v >= thr) : (v > thr);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    return c;
 }
 
 __global__ void __launch_bounds__(BEAM_THREADS)
@@ -122,8 +167,6 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int L = min(max(seq_len[b], 0), T);
     const int blank = C - 1;
-    const int Ls = min(K, C - 1);
-    const int M = Ls + 1;
     int2* arena = arena_all + (size_t)b * (1 + (size_t)T * K);
 
     if (tid == 0) {
@@ -152,7 +195,7 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
         const int n = s.n;
         __syncthreads();
 
-        // ---- label order, parent lookup, clear child tables
+        // ---- sorted logits, parent lookup, clear per-step flags
         if (tid < C && tid != blank) {
             const float xl = s.x[tid];
             int rank = 0;
@@ -161,8 +204,7 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
                 const float xj = s.x[j];
                 rank += (xj > xl) || (xj == xl && j < tid);
             }
-            s.slot_label[rank] = tid;
-            s.label_slot[tid] = rank;
+            s.xs[rank] = xl;
         }
         if (tid < n) {
             int p = -1;
@@ -172,6 +214,8 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
                     if (s.h[j] == want) { p = j; break; }
             }
             s.pidx[tid] = p;
+            s.has_kid[tid] = 0;
+            s.wiped[tid] = 0;
 #pragma unroll
             for (int q = 0; q < BEAM_MAX_C / 32; ++q) s.act[tid][q] = 0u;
         }
@@ -189,6 +233,7 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
                 }
                 nl += s.x[l];
                 if (p >= 0) atomicOr(&s.act[p][l >> 5], 1u << (l & 31));
+                if (p >= 0 && p < tid) s.has_kid[p] = 1;
             }
             const float nb = s.ot[tid] + s.x[blank];
             my_nt = log_sum_exp(nb, nl);
@@ -208,8 +253,27 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
         }
         __syncthreads();
 
+        // ---- wipe pass (wave 0), in parent rank order
+        if (w == 0) {
+            for (int p = 0; p < n; ++p) {
+                if (!s.has_kid[p] || s.wiped[p]) continue;
+                if (count_better(s, s.ot[p], true, 0, p, 0, n, C, lane) >= K) continue;   // p gated
+                for (int j0 = p + 1; j0 < n; j0 += 64) {
+                    const int jj = j0 + lane;
+                    uint64_t kids = __ballot(jj < n && s.pidx[jj] == p);
+                    while (kids) {
+                        const int j = j0 + __builtin_ctzll(kids);
+                        kids &= kids - 1;
+                        const int c = count_better(s, s.nt[j], false, j, p, s.lab[j], n, C, lane);
+                        if (lane == 0 && c >= K) s.wiped[j] = 1;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
         // ---- radix select of the K-th smallest key (47 bits, 8-bit digits)
-        const int n_items = n + n * M;
+        const int n_items = n + n * (C - 1);
         uint64_t pmask = 0;
         bool take_all = false;
         for (int shift = 40; shift >= 0; shift -= 8) {
@@ -218,7 +282,7 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
             const uint64_t prefix = s.prefix;
             for (int i = tid; i < n_items; i += BEAM_THREADS) {
                 uint64_t key;
-                if (beam_item(s, i, n, M, Ls, C, &key) && (key & pmask) == prefix)
+                if (beam_item(s, i, n, C, &key) && (key & pmask) == prefix)
                     atomicAdd(&s.hist[w][(key >> shift) & 255u], 1u);
             }
             __syncthreads();
@@ -261,7 +325,7 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
         // ---- gather the selected keys and rank them
         for (int i = tid; i < n_items; i += BEAM_THREADS) {
             uint64_t key;
-            if (beam_item(s, i, n, M, Ls, C, &key) && key <= theta) {
+            if (beam_item(s, i, n, C, &key) && key <= theta) {
                 uint32_t pos = atomicAdd(&s.n_sel, 1u);
                 if (pos < (uint32_t)BEAM_MAX_K) s.sel[pos] = key;
             }

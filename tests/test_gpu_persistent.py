@@ -19,8 +19,8 @@ def test_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch):
     seq = rng.integers(1, T + 1, B).astype(np.int32)
     seq[:3] = [T, 1, T - 1]
     ref = np.concatenate([G.lstm_dir_fwd(x, seq, ks[d], bs[d], d == 1)[0] for d in range(2)], axis=2)
-    wxT = np.concatenate([k[:n_in].T for k in ks], 0)
-    whT = np.stack([k[n_in:].T for k in ks])
+    wxT = np.ascontiguousarray(np.concatenate([k[:n_in].T for k in ks], 0))
+    whT = np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))
     gx = K.gemm(torch.from_numpy(x.reshape(T * B, n_in)).to(cuda).bfloat16(),
                 torch.from_numpy(wxT).to(cuda).bfloat16(), trans_b=True,
                 bias=torch.from_numpy(np.concatenate(bs)).to(cuda))
