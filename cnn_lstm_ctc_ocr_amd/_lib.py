@@ -39,6 +39,9 @@ SIGNATURES = {
     "ocrk_ctc_loss": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _f32, _p, _p, _p, _p, _sz, _p],
     "ocrk_ctc_greedy_decode": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
     "ocrk_ctc_beam_workspace_size": [_i32, _i32, _i32],
+    "ocrk_gru_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_gru_fwd": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
+    "ocrk_gru_bwd": [_p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_ctc_beam_decode": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _sz, _p],
     "ocrk_edit_distance": [_p, _p, _i32, _p, _p, _i32, _i32, _p, _p, _p],
     "ocrk_conv1_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _p],

@@ -20,141 +20,9 @@
 // Backward step (reverse s): dh = dout + dG_{s+1} . W_h^T (K = 4H, same
 // streaming core), then the gate gradients; dG is published for the next
 // step and scattered into time order for the dW_x / dW_h / dX GEMMs.
-#include "common.h"
-#include "mfma_util.h"
+#include "recur.h"
 
 using namespace ocrk;
-
-template <typename CT, int BR, int NC, int KC>
-struct RecurCore {
-    using RT = typename RawT<CT>::T;
-    static constexpr int LDK = KC + 8;
-    static constexpr int NVA = (BR * KC / 8 + 255) / 256;
-    static constexpr int NVB = (NC * KC / 8 + 255) / 256;
-    static constexpr int TILES = (BR / 16) * (NC / 16);
-    static constexpr int TPW = TILES >= 4 ? TILES / 4 : 1;
-    static constexpr int STAGE_BYTES = 2 * (BR + NC) * LDK * (int)sizeof(RT);
-    static constexpr int EPI_BYTES = BR * (NC + 1) * 4;
-    static constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-    static_assert(TILES % 4 == 0 || TILES < 4, "tile split");
-    static constexpr bool FULL_A = (BR * KC / 8) % 256 == 0;
-    static constexpr bool FULL_B = (NC * KC / 8) % 256 == 0;
-
-    template <typename BCol>
-    __device__ __forceinline__ static void load(V8<CT> (&ra)[NVA], V8<CT> (&rb)[NVB], const CT* __restrict__ a_rows,
-                                                int64_t lda, const BCol& bcol, int k0) {
-        const int tid = threadIdx.x;
-#pragma unroll
-        for (int v = 0; v < NVA; ++v) {
-            int idx = tid + 256 * v;
-            if (FULL_A || idx < BR * KC / 8) {
-                int r = idx / (KC / 8), kq = idx % (KC / 8);
-                vload(ra[v], a_rows + (int64_t)r * lda + k0 + 8 * kq);
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < NVB; ++v) {
-            int idx = tid + 256 * v;
-            if (FULL_B || idx < NC * KC / 8) {
-                int n = idx / (KC / 8), kq = idx % (KC / 8);
-                vload(rb[v], bcol(n) + k0 + 8 * kq);
-            }
-        }
-    }
-    __device__ __forceinline__ static void store(const V8<CT> (&ra)[NVA], const V8<CT> (&rb)[NVB], RT* sA, RT* sB,
-                                                 int buf) {
-        const int tid = threadIdx.x;
-#pragma unroll
-        for (int v = 0; v < NVA; ++v) {
-            int idx = tid + 256 * v;
-            if (FULL_A || idx < BR * KC / 8)
-                vstore_lds(sA + buf * BR * LDK + (idx / (KC / 8)) * LDK + 8 * (idx % (KC / 8)), ra[v]);
-        }
-#pragma unroll
-        for (int v = 0; v < NVB; ++v) {
-            int idx = tid + 256 * v;
-            if (FULL_B || idx < NC * KC / 8)
-                vstore_lds(sB + buf * NC * LDK + (idx / (KC / 8)) * LDK + 8 * (idx % (KC / 8)), rb[v]);
-        }
-    }
-    __device__ __forceinline__ static void compute(floatx4 (&acc)[TPW], const RT* sA, const RT* sB, int buf) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-            int q = wave + 4 * i;
-            if (q >= TILES) break;
-            int tm = q / (NC / 16), tn = q % (NC / 16);
-            const RT* a = sA + buf * BR * LDK + (tm * 16 + (lane & 15)) * LDK + 8 * (lane >> 4);
-            const RT* b = sB + buf * NC * LDK + (tn * 16 + (lane & 15)) * LDK + 8 * (lane >> 4);
-#pragma unroll
-            for (int ks = 0; ks < KC / 32; ++ks) {
-                if constexpr (sizeof(CT) == 2) {
-                    bf16x8 af = *reinterpret_cast<const bf16x8*>(a + ks * 32);
-                    bf16x8 bfr = *reinterpret_cast<const bf16x8*>(b + ks * 32);
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i], 0, 0, 0);
-                } else {
-                    V8<float> af, bfr;
-                    vload_lds(af, a + ks * 32);
-                    vload_lds(bfr, b + ks * 32);
-#pragma unroll
-                    for (int kk = 0; kk < 8; ++kk)
-                        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af.e(kk), bfr.e(kk), acc[i], 0, 0, 0);
-                }
-            }
-        }
-    }
-
-    // acc <- A[BR, K] . Bcols[NC, K]^T ; A rows at a_rows + r*lda, B col n at bcol(n).
-    // begin() issues the loads of chunks 0 and 1 (so the caller can overlap
-    // other loads with them); finish() runs the pipeline: two register sets
-    // in flight while one chunk is on MFMA.
-    V8<CT> ra0[NVA], rb0[NVB], ra1[NVA], rb1[NVB];
-
-    template <typename BCol>
-    __device__ __forceinline__ void begin(const CT* __restrict__ a_rows, int64_t lda, const BCol& bcol, int K) {
-        load(ra0, rb0, a_rows, lda, bcol, 0);
-        if (K / KC > 1) load(ra1, rb1, a_rows, lda, bcol, KC);
-    }
-
-    template <typename BCol>
-    __device__ __forceinline__ void finish(const CT* __restrict__ a_rows, int64_t lda, const BCol& bcol, int K,
-                                           char* lds, floatx4 (&acc)[TPW]) {
-        RT* sA = reinterpret_cast<RT*>(lds);
-        RT* sB = sA + 2 * BR * LDK;
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-        const int nch = K / KC;
-        store(ra0, rb0, sA, sB, 0);
-        __syncthreads();
-        for (int c = 0; c < nch; c += 2) {
-            if (c + 2 < nch) load(ra0, rb0, a_rows, lda, bcol, (c + 2) * KC);
-            compute(acc, sA, sB, 0);
-            if (c + 1 < nch) store(ra1, rb1, sA, sB, 1);
-            __syncthreads();
-            if (c + 1 >= nch) break;
-            if (c + 3 < nch) load(ra1, rb1, a_rows, lda, bcol, (c + 3) * KC);
-            compute(acc, sA, sB, 1);
-            if (c + 2 < nch) store(ra0, rb0, sA, sB, 0);
-            __syncthreads();
-        }
-    }
-
-    // accumulators -> LDS [BR][NC+1] f32 (call after run(); ends with a barrier)
-    __device__ __forceinline__ static void spill(const floatx4 (&acc)[TPW], char* lds) {
-        float* sG = reinterpret_cast<float*>(lds);
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-            int q = wave + 4 * i;
-            if (q >= TILES) break;
-            int tm = q / (NC / 16), tn = q % (NC / 16);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                sG[(tm * 16 + (lane >> 4) * 4 + r) * (NC + 1) + tn * 16 + (lane & 15)] = acc[i][r];
-        }
-        __syncthreads();
-    }
-};
 
 // Diagnostic stamps (tools/bench_lstm.py --stamps): thread 0 of every
 // workgroup writes s_memrealtime (100 MHz) at fixed points into dbg.
@@ -163,35 +31,6 @@ __device__ __forceinline__ void stamp(long long* dbg, int i) {
         long long t = __builtin_amdgcn_s_memrealtime();
         dbg[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + i] = t;
     }
-}
-
-// 4 consecutive elements of CT (8 B for bf16, 16 B for f32)
-template <typename CT> struct V4;
-template <> struct V4<bf16> { typedef unsigned int u32x2 __attribute__((ext_vector_type(2))); u32x2 q; };
-template <> struct V4<float> { f32x4 q; };
-__device__ __forceinline__ void ld4(float (&v)[4], const bf16* p) {
-    V4<bf16>::u32x2 q = *reinterpret_cast<const V4<bf16>::u32x2*>(p);
-    v[0] = __builtin_bit_cast(float, q[0] << 16); v[1] = __builtin_bit_cast(float, q[0] & 0xffff0000u);
-    v[2] = __builtin_bit_cast(float, q[1] << 16); v[3] = __builtin_bit_cast(float, q[1] & 0xffff0000u);
-}
-__device__ __forceinline__ void ld4(float (&v)[4], const float* p) {
-    f32x4 q = *reinterpret_cast<const f32x4*>(p);
-    v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
-}
-__device__ __forceinline__ void st4(bf16* p, const float (&v)[4]) {
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    bf16x4 q = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-    *reinterpret_cast<bf16x4*>(p) = q;
-}
-__device__ __forceinline__ void st4(float* p, const float (&v)[4]) {
-    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
-}
-// exp-based gate nonlinearities (one v_exp each)
-__device__ __forceinline__ float sig_fast(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_fast(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
-
-__device__ __forceinline__ int step_time(int dir, int s, int len) {
-    return (dir == 0 || s >= len) ? s : len - 1 - s;
 }
 
 // --------------------------------------------------------------- forward

@@ -256,6 +256,37 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
     return dG
 
 
+# ------------------------------------------------------------------- GRU
+def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
+    """Returns out [T,B,2H], hprev_t, rh_t [T,B,2,H], acts_t [T,B,2,3H] (dtype)."""
+    _chk(gx, whgT, whcT, seq_len)
+    dev = gx.device
+    h = torch.zeros(2, B, H, dtype=dtype, device=dev)
+    rh = torch.empty(2, B, H, dtype=dtype, device=dev)
+    out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+    hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+    rh_t = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+    acts = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
+    call("ocrk_gru_fwd", ptr(gx), ptr(whgT), ptr(whcT), ptr(h), ptr(rh), ptr(seq_len), T, B, H, ptr(out),
+         ptr(hprev), ptr(rh_t), ptr(acts), dtype_code(dtype), _stream(gx))
+    return out, hprev, rh_t, acts
+
+
+def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H):
+    """Returns dG_t [T,B,2,3H] = (dz_r, dz_u, dz_c) per direction."""
+    _chk(whg, whc, seq_len, dout, hprev, acts)
+    dtype = dout.dtype
+    dev = dout.device
+    dzg = torch.empty(2, B, 2 * H, dtype=dtype, device=dev)
+    dzc = torch.empty(2, B, H, dtype=dtype, device=dev)
+    dh_tot = torch.empty(2, B, H, dtype=torch.float32, device=dev)
+    direct = torch.empty(2, B, H, dtype=torch.float32, device=dev)
+    dG = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
+    call("ocrk_gru_bwd", ptr(whg), ptr(whc), ptr(dzg), ptr(dzc), ptr(dh_tot), ptr(direct), ptr(seq_len), T, B, H,
+         ptr(dout), ptr(hprev), ptr(acts), ptr(dG), dtype_code(dtype), _stream(dout))
+    return dG
+
+
 # ----------------------------------------------------------------- misc
 def cast(x, dtype, out=None):
     _chk(x)

@@ -205,6 +205,57 @@ class _BiLSTM(torch.autograd.Function):
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 
+class _BiGRU(torch.autograd.Function):
+    """rnn_layer with GRUCell (src/weinman/model.py:167-199)."""
+
+    @staticmethod
+    def forward(ctx, x, seq_len, store, layer, *variables):
+        dt = store.cfg.dtype
+        T, B, n_in = x.shape
+        H = store.cfg.rnn_sizes[layer - 1]
+        wxT, _wx, whgT, whcT, _whg, _whc, bias = store.gru_images(layer, dt)
+        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias)          # [T*B, 6H] f32
+        out, hprev, rh, acts = K.gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dt)
+        ctx.store, ctx.layer, ctx.H = store, layer, H
+        ctx.save_for_backward(x, seq_len, hprev, rh, acts)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        store, layer, H = ctx.store, ctx.layer, ctx.H
+        x, seq_len, hprev, rh, acts = ctx.saved_tensors
+        dt = store.cfg.dtype
+        T, B, n_in = x.shape
+        G2, G3 = 2 * H, 3 * H
+        dout = dout.contiguous()
+        if dout.dtype != dt:
+            dout = K.cast(dout, dt)
+        _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt)
+        dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H)            # [T,B,2,3H]
+        pre = f"rnn/bdrnn{layer}"
+        R = T * B
+        for d, dn in enumerate(("fw", "bw")):
+            gk = store.grads[f"{pre}/{dn}/gru_cell/gates/kernel"]               # [In+H, 2H]
+            ck = store.grads[f"{pre}/{dn}/gru_cell/candidate/kernel"]           # [In+H, H]
+            dgg = dG.view(R, 2 * G3)[:, d * G3:]                                 # (dz_r, dz_u), ld 6H
+            dgc = dG.view(R, 2 * G3)[:, d * G3 + G2:]                            # dz_c, ld 6H
+            hp = hprev.view(R, 2 * H)[:, d * H:]
+            rhd = rh.view(R, 2 * H)[:, d * H:]
+            K.gemm(x, dgg, trans_a=True, out=gk, accumulate=True, M=n_in, N=G2, K=R, lda=n_in,
+                   ldb=2 * G3, ldc=G2, splits=_splits(n_in, G2, R))
+            K.gemm(hp, dgg, trans_a=True, out=gk[n_in:], accumulate=True, M=H, N=G2, K=R, lda=2 * H,
+                   ldb=2 * G3, ldc=G2, splits=_splits(H, G2, R))
+            K.gemm(x, dgc, trans_a=True, out=ck, accumulate=True, M=n_in, N=H, K=R, lda=n_in,
+                   ldb=2 * G3, ldc=H, splits=_splits(n_in, H, R))
+            K.gemm(rhd, dgc, trans_a=True, out=ck[n_in:], accumulate=True, M=H, N=H, K=R, lda=2 * H,
+                   ldb=2 * G3, ldc=H, splits=_splits(H, H, R))
+        K.colsum(dG, R, 2 * G3, store.gru_bias_cat_grad(layer))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(dG.view(R, 2 * G3), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
+        return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
+
+
 def _splits(M, N, Kdim):
     tiles = -(-M // 128) * -(-N // 128)
     return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
@@ -249,8 +300,6 @@ def rnn_layers(features, sequence_length, num_classes, store=None):
     cfg = store.cfg
     if num_classes != cfg.num_classes:
         raise ValueError(f"store was built for {cfg.num_classes} classes, got {num_classes}")
-    if cfg.cell != "lstm":
-        raise NotImplementedError("GRU recurrent kernels are not in libocrk yet (cell='lstm', model_bu.py)")
     x = features.transpose(0, 1)                                                  # model.py:212
     if not x.is_contiguous():
         x = x.contiguous()
@@ -262,8 +311,11 @@ def rnn_layers(features, sequence_length, num_classes, store=None):
         variables = []
         if track:
             pre = f"rnn/bdrnn{layer}"
-            variables = [store.params[f"{pre}/{d}/lstm_cell/{v}"] for d in ("fw", "bw") for v in ("kernel", "bias")]
-        x = _BiLSTM.apply(x, sequence_length, store, layer, *variables)
+            leaves = ("lstm_cell/kernel", "lstm_cell/bias") if cfg.cell == "lstm" else \
+                ("gru_cell/gates/kernel", "gru_cell/gates/bias", "gru_cell/candidate/kernel", "gru_cell/candidate/bias")
+            variables = [store.params[f"{pre}/{d}/{v}"] for d in ("fw", "bw") for v in leaves]
+        op = _BiLSTM if cfg.cell == "lstm" else _BiGRU
+        x = op.apply(x, sequence_length, store, layer, *variables)
     variables = [store.params["rnn/logits/kernel"], store.params["rnn/logits/bias"]] if track else []
     return _Logits.apply(x, store, *variables)
 

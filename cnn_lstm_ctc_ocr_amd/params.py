@@ -44,13 +44,33 @@ def param_shapes(cfg):
         else:
             for d in ("fw", "bw"):
                 out.append((f"{pre}/{d}/gru_cell/gates/kernel", (n_in + H, 2 * H), True))
-                out.append((f"{pre}/{d}/gru_cell/gates/bias", (2 * H,), True))
                 out.append((f"{pre}/{d}/gru_cell/candidate/kernel", (n_in + H, H), True))
+            # [fw r|u, fw c, bw r|u, bw c] = the bias of the fused input projection
+            for d in ("fw", "bw"):
+                out.append((f"{pre}/{d}/gru_cell/gates/bias", (2 * H,), True))
                 out.append((f"{pre}/{d}/gru_cell/candidate/bias", (H,), True))
         n_in = 2 * H
     out.append(("rnn/logits/kernel", (n_in, cfg.num_classes + 1), True))
     out.append(("rnn/logits/bias", (cfg.num_classes + 1,), True))
     return out
+
+
+def creation_order(cfg):
+    """Variable names in the order the reference graph creates them (what a
+    seeded initialiser walks; the buffer order above differs for biases)."""
+    names = [n for n, _s, _t in param_shapes(cfg)]
+    out = [n for n in names if not n.startswith("rnn/bdrnn")]
+    rnn = []
+    for li in range(1, len(cfg.rnn_sizes) + 1):
+        pre = f"rnn/bdrnn{li}"
+        for d in ("fw", "bw"):
+            if cfg.cell == "lstm":
+                rnn += [f"{pre}/{d}/lstm_cell/kernel", f"{pre}/{d}/lstm_cell/bias"]
+            else:
+                rnn += [f"{pre}/{d}/gru_cell/{v}" for v in
+                        ("gates/kernel", "gates/bias", "candidate/kernel", "candidate/bias")]
+    i = out.index("rnn/logits/kernel")
+    return out[:i] + rnn + out[i:]
 
 
 def _trunc_normal(rng, shape, std):
@@ -72,7 +92,9 @@ def reference_init(cfg, seed=0):
     (model.py:170-180)."""
     rng = np.random.default_rng(seed)
     vals = {}
-    for name, shape, _tr in param_shapes(cfg):
+    shapes = {n: sh for n, sh, _t in param_shapes(cfg)}
+    for name in creation_order(cfg):
+        shape = shapes[name]
         leaf = name.rsplit("/", 1)[1]
         if name.startswith("convnet") and leaf == "kernel":
             v = _trunc_normal(rng, shape, np.sqrt(2.6 / (shape[0] * shape[1] * shape[2])))
@@ -208,6 +230,58 @@ class ParamStore:
         _, off, _ = self.offsets[f"{pre}/fw/lstm_cell/bias"]
         n = self.params[f"{pre}/fw/lstm_cell/bias"].numel()
         return self.flat_grad[off:off + 2 * n]
+
+    def gru_images(self, layer, dtype):
+        """GRU layer `layer`: WxT_cat [6H][In] and Wx_cat [In][6H] (per direction
+        columns r|u|c), whgT [2][2H][H], whcT [2][H][H] (forward), whg [2][H][2H],
+        whc [2][H][H] (backward), all in dtype; bias_cat f32 [6H] (a flat view)."""
+        def build():
+            pre = f"rnn/bdrnn{layer}"
+            gk = self.params[f"{pre}/fw/gru_cell/gates/kernel"]
+            rows, G2 = gk.shape
+            H = G2 // 2
+            n_in = rows - H
+            G3 = 3 * H
+            dev = gk.device
+            wxT = torch.empty(2 * G3, n_in, dtype=dtype, device=dev)
+            wx = torch.empty(n_in, 2 * G3, dtype=dtype, device=dev)
+            whgT = torch.empty(2, G2, H, dtype=dtype, device=dev)
+            whcT = torch.empty(2, H, H, dtype=dtype, device=dev)
+            whg = torch.empty(2, H, G2, dtype=dtype, device=dev)
+            whc = torch.empty(2, H, H, dtype=dtype, device=dev)
+            for d, dn in enumerate(("fw", "bw")):
+                g = self.params[f"{pre}/{dn}/gru_cell/gates/kernel"]
+                c = self.params[f"{pre}/{dn}/gru_cell/candidate/kernel"]
+                K.strided_copy(g, n_in, G2, G2, 1, wxT, 1, n_in, out_offset=d * G3 * n_in)
+                K.strided_copy(c, n_in, H, H, 1, wxT, 1, n_in, out_offset=(d * G3 + G2) * n_in)
+                K.strided_copy(g, n_in, G2, G2, 1, wx, 2 * G3, 1, out_offset=d * G3)
+                K.strided_copy(c, n_in, H, H, 1, wx, 2 * G3, 1, out_offset=d * G3 + G2)
+                K.strided_copy(g, H, G2, G2, 1, whgT, 1, H, out_offset=d * G2 * H, in_offset=n_in * G2)
+                K.strided_copy(c, H, H, H, 1, whcT, 1, H, out_offset=d * H * H, in_offset=n_in * H)
+                K.strided_copy(g, H, G2, G2, 1, whg, G2, 1, out_offset=d * H * G2, in_offset=n_in * G2)
+                K.strided_copy(c, H, H, H, 1, whc, H, 1, out_offset=d * H * H, in_offset=n_in * H)
+            return wxT, wx, whgT, whcT, whg, whc, self.gru_bias_cat(layer)
+        return self.images(("gru", layer, dtype), build)
+
+    def _gru_bias_span(self, layer):
+        pre = f"rnn/bdrnn{layer}"
+        names = [f"{pre}/{d}/gru_cell/{v}" for d in ("fw", "bw") for v in ("gates/bias", "candidate/bias")]
+        _, off, _ = self.offsets[names[0]]
+        pos = off
+        for n in names:
+            if self.offsets[n][1] != pos:
+                raise RuntimeError("GRU biases must be adjacent in the flat buffer")
+            pos += self.params[n].numel()
+        return off, pos
+
+    def gru_bias_cat(self, layer):
+        """[6H] view: [fw r|u, fw c, bw r|u, bw c] biases of GRU layer `layer`."""
+        a, b = self._gru_bias_span(layer)
+        return self.flat[a:b]
+
+    def gru_bias_cat_grad(self, layer):
+        a, b = self._gru_bias_span(layer)
+        return self.flat_grad[a:b]
 
     def logits_image(self, dtype):
         def build():

@@ -173,6 +173,25 @@ int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const int* seq_le
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
  * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
 int ocrk_lstm_debug_stamps(long long* buf);
+/* a7 -- rnn_layer with tf.contrib.rnn.GRUCell (src/weinman/model.py:167-199; [TF1] GRUCell:
+ * [r, u] = sig([x, h] Wg + bg), c = tanh([x, r*h] Wc + bc), h' = u h + (1 - u) c) under
+ * bidirectional_dynamic_rnn(time_major, sequence_length). gx f32 [T][B][2][3H] = x . [Wg_x | Wc_x]
+ * + [bg | bc] per direction (one GEMM). whgT dtype [2][2H][H], whcT [2][H][H] (h-parts,
+ * transposed). State h [2][B][H] and rh [2][B][H] (zeroed h). Outputs: out [T][B][2H] (zeroed by
+ * the caller; rows past seq_len stay 0), time-order hprev_t, rh_t [T][B][2][H], acts_t
+ * [T][B][2][3H] = (r, u, c). One step = two launches (gate, candidate) for both directions. */
+int ocrk_gru_fwd_step(const float* gx, const void* whgT, const void* whcT, void* h, void* rh,
+                      const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t, void* rh_t,
+                      void* acts_t, int dtype, void* stream);
+int ocrk_gru_fwd(const float* gx, const void* whgT, const void* whcT, void* h, void* rh, const int* seq_len,
+                 int T, int B, int H, void* out, void* hprev_t, void* rh_t, void* acts_t, int dtype,
+                 void* stream);
+/* GRU BPTT: whg dtype [2][H][2H], whc [2][H][H] (h-parts, untransposed); scratch dzg [2][B][2H],
+ * dzc [2][B][H] (dtype), dh_tot, direct f32 [2][B][H]; dout dtype [T][B][2H]. dG_t dtype
+ * [T][B][2][3H] = (dz_r, dz_u, dz_c) in time order, for the dW / dx GEMMs. */
+int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* dzc, float* dh_tot, float* direct,
+                 const int* seq_len, int T, int B, int H, const void* dout, const void* hprev_t,
+                 const void* acts_t, void* dG_t, int dtype, void* stream);
 int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
                   int T, int B, int H, void* out, void* hprev_t, float* cprev_t, void* acts_t, int dtype,
                   void* stream);

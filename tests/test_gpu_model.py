@@ -12,12 +12,12 @@ pytestmark = pytest.mark.gpu
 SIZES = (64, 64)
 
 
-def _setup(cuda, dtype, B=32, W=64, seed=0, scale_rnn=20.0, sizes=SIZES):
+def _setup(cuda, dtype, B=32, W=64, seed=0, scale_rnn=20.0, sizes=SIZES, cell="lstm"):
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
     rng = np.random.default_rng(seed)
-    vals = M.init_params(seed=seed, cell="lstm", rnn_sizes=sizes)
+    vals = M.init_params(seed=seed, cell=cell, rnn_sizes=sizes)
     for k in vals:
-        if "lstm_cell/kernel" in k:
+        if "_cell/" in k and "kernel" in k:
             vals[k] = (vals[k] * scale_rnn).astype(np.float32)     # non-trivial recurrent signal
     img = rng.integers(0, 256, (B, 32, W, 1)).astype(np.uint8)
     widths = rng.integers(W - 12, W + 1, B).astype(np.int32)
@@ -31,15 +31,18 @@ def _setup(cuda, dtype, B=32, W=64, seed=0, scale_rnn=20.0, sizes=SIZES):
             if G.ctc_required_time(lab) <= tl:
                 break
         labels.append(lab)
-    store = ParamStore(ModelConfig(rnn_sizes=sizes, dtype=dtype), device=cuda, values=vals)
+    store = ParamStore(ModelConfig(cell=cell, rnn_sizes=sizes, dtype=dtype), device=cuda, values=vals)
     return store, vals, img, widths, labels, T
 
 
-def test_forward_train_mode_loss_and_grads_fp32(cuda):
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_forward_train_mode_loss_and_grads_fp32(cuda, cell):
     from cnn_lstm_ctc_ocr_amd import model
-    store, vals, img, widths, labels, T = _setup(cuda, torch.float32)
-    ref = M.RefModel(vals, "lstm", SIZES)
-    x = G.preprocess(img)
+    store, vals, img, widths, labels, T = _setup(cuda, torch.float32, cell=cell)
+    # float64 oracle: an fp32 oracle's own rounding reaches 2e-3 on the conv-tower
+    # gradients behind the GRU (measured against float64); the HIP path is closer than that
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, cell, SIZES)
+    x = G.preprocess(img).astype(np.float64)
     loss_ref, grads_ref, _, logits_ref, seq_ref = ref.loss_and_grads(x, widths, labels)
     store.zero_grad()
     feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN, store)
@@ -52,14 +55,16 @@ def test_forward_train_mode_loss_and_grads_fp32(cuda):
     assert np.linalg.norm(lg - logits_ref) / np.linalg.norm(logits_ref) < 1e-4
     # north_star: CTC loss within 1e-3 relative (fp32)
     assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-3
+    errs = {}
     for name, g in grads_ref.items():
         got = store.grads[name].cpu().numpy()
         scale = np.linalg.norm(g)
         if name.endswith("/bias") and name.split("/")[1] in ("conv2", "conv4", "conv6", "conv8"):
             # a bias in front of BatchNorm has an exactly-zero gradient: both sides are rounding noise
             scale = max(scale, 1e-3 * np.linalg.norm(grads_ref[name.replace("/bias", "/kernel")]))
-        err = np.linalg.norm(got - g) / max(scale, 1e-12)
-        assert err < 2e-3, (name, err)
+        errs[name] = float(np.linalg.norm(got - g) / max(scale, 1e-12))
+    print("relative gradient errors:", errs)
+    assert max(errs.values()) < 5e-4, errs
     # BN moving averages were updated exactly like the reference UPDATE_OPS
     for name, v in ref.bn_moving_updates().items():
         np.testing.assert_allclose(store.stats[name].cpu().numpy(), v, rtol=1e-4, atol=1e-6)
@@ -105,14 +110,28 @@ def test_trainer_step_fp32_matches_oracle_adam(cuda):
         assert np.linalg.norm(delta - delta_ref) <= 2e-2 * np.linalg.norm(delta_ref) + 1e-9, name
 
 
-def test_bf16_train_step_close_to_fp32(cuda):
+@pytest.mark.parametrize("cell,sizes", [("lstm", (256, 256)), ("gru", (512, 256))])
+def test_bf16_train_step_close_to_fp32(cuda, cell, sizes):
     from cnn_lstm_ctc_ocr_amd.train import Trainer
     losses = []
     for dt in (torch.float32, torch.bfloat16):
-        store, vals, img, widths, labels, T = _setup(cuda, dt, B=64, seed=5, sizes=(256, 256))
+        store, vals, img, widths, labels, T = _setup(cuda, dt, B=64, seed=5, sizes=sizes, cell=cell)
         tr = Trainer(store)
         l0 = tr.step(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), labels).item()
         l1 = tr.step(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), labels).item()
         assert np.isfinite(l0) and np.isfinite(l1)
         losses.append((l0, l1))
     assert abs(losses[1][0] - losses[0][0]) / losses[0][0] < 2e-2
+
+
+def test_gru_infer_matches_oracle(cuda):
+    """model.py's shipped configuration: GRU (512, 256), INFER mode, fp32."""
+    from cnn_lstm_ctc_ocr_amd import model
+    store, vals, img, widths, labels, T = _setup(cuda, torch.float32, seed=6, sizes=(512, 256), cell="gru")
+    ref = M.RefModel(vals, "gru", (512, 256))
+    logits_ref, seq_ref = ref.forward(G.preprocess(img), widths, training=False)
+    with torch.no_grad():
+        feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.INFER, store)
+        logits = model.rnn_layers(feats, seq, 95, store)
+    lg = logits.cpu().numpy()
+    assert np.linalg.norm(lg - logits_ref) / np.linalg.norm(logits_ref) < 1e-4

@@ -359,6 +359,19 @@ def test_adam_kat():
 
 
 # ------------------------------------------------------------ whole graph
+@pytest.mark.parametrize("cell,sizes", [("gru", (512, 256)), ("lstm", (512, 512))])
+def test_store_init_equals_oracle_init(cell, sizes):
+    """ParamStore's reference initialisers walk variables in the reference's
+    creation order, so a seed gives the oracle's values whatever the buffer layout."""
+    from cnn_lstm_ctc_ocr_amd.config import ModelConfig
+    from cnn_lstm_ctc_ocr_amd.params import reference_init
+    a = reference_init(ModelConfig(cell=cell, rnn_sizes=sizes), seed=3)
+    b = M.init_params(seed=3, cell=cell, rnn_sizes=sizes)
+    assert set(a) == set(b)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
 def test_param_counts_match_survey():
     n = lambda shapes: sum(int(np.prod(s)) for k, s in shapes.items() if M.is_trainable(k))
     conv = sum(int(np.prod(s)) for k, s in M.param_shapes().items()
