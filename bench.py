@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--breakdown", action="store_true", help="per-entry-point event timing table on stderr")
     ap.add_argument("--cpu-sample", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
+                    help="PMC summary (tools/pmc_traffic.py) for roofline.traffic of the conv roofline kernel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,6 +197,12 @@ def main():
                      "algorithmic_flop_per_launch": work / max(len(ms), 1)},
         "loss": round(float(loss.item()), 4),
     }
+    if args.roofline == "conv" and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as fh:
+            pmc = json.load(fh)
+        result["roofline"]["traffic"] = pmc["bytes_per_launch"]
+        result["roofline"]["traffic_unit"] = "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+        result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample)
     if rank == 0:

@@ -1,0 +1,64 @@
+"""Per-launch HBM traffic of one kernel class from two rocprofv3 PMC passes.
+
+    python tools/pmc_traffic.py --fetch DIR --write DIR --match SUBSTR --out FILE.json
+
+FETCH_SIZE and WRITE_SIZE come from separate passes (they do not fit one TCC
+pass on gfx950). Both are in KiB. MI355X_MICROARCH.md (HBM section): on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so the
+read side is doubled; WRITE_SIZE is exact for 16-B/lane stores.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def per_dispatch(root, counter, match):
+    files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {root}")
+    vals = defaultdict(float)
+    for f in files:
+        with open(f, newline="") as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter or match not in row.get("Kernel_Name", ""):
+                    continue
+                vals[(f, row.get("Dispatch_Id"))] += float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--match", required=True, help="substring of the kernel name")
+    ap.add_argument("--desc", default="")
+    ap.add_argument("--command", default="")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.match)
+    write = per_dispatch(a.write, "WRITE_SIZE", a.match)
+    if not fetch or not write:
+        raise SystemExit(f"no dispatches matching {a.match!r}")
+    f_kib = sum(fetch) / len(fetch)
+    w_kib = sum(write) / len(write)
+    res = {
+        "kernel_match": a.match,
+        "kernel": a.desc,
+        "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
+        "fetch_size_kib_avg": round(f_kib, 2),
+        "write_size_kib_avg": round(w_kib, 2),
+        "read_bytes_per_launch": round(2 * f_kib * 1024),        # gfx950 FETCH_SIZE x2 correction
+        "write_bytes_per_launch": round(w_kib * 1024),
+        "bytes_per_launch": round((2 * f_kib + w_kib) * 1024),
+        "command": a.command,
+    }
+    with open(a.out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

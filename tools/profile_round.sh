@@ -1,0 +1,23 @@
+#!/bin/bash
+# Kernel-time stats and HBM traffic of the bench step, for profiles/.
+# Run on the GPU box from the repo root:  bash tools/profile_round.sh r1
+# Three separate rocprofv3 runs: --kernel-trace --stats, then one --pmc pass
+# per TCC counter (FETCH_SIZE, WRITE_SIZE); every GPU step has its own limit.
+set -o pipefail
+tag=${1:?tag}
+out=gpurun_out/prof_$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+cmd=(python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline)
+pmc=(python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- "${cmd[@]}" \
+    > "$out/trace.log" 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- "${pmc[@]}" \
+    > "$out/fetch.log" 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- "${pmc[@]}" \
+    > "$out/write.log" 2>&1 || exit $?
+python3 tools/pmc_traffic.py --fetch "$out/fetch" --write "$out/write" --match "gemm_kernelIDF16bLi2ELi0" \
+    --desc "conv2-conv8 forward implicit-GEMM (gemm_kernel<bf16, A_IM2COL, B_NK>)" \
+    --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- ${pmc[*]}" --out "$out/pmc_conv.json" || exit $?
+find "$out/trace" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
+grep '^{' "$out/trace.log" | tail -1 > "$out/bench_under_trace.json"
