@@ -1,0 +1,201 @@
+"""Drop-in for the width-bucketed recognise service of src/processing/server.py
+(Bucket, LocalServer) on the libocrk GPU path.
+
+Semantics kept from the reference:
+  * 31 buckets, width ranges (w, w+32] for w = 32, 64, ..., 992 (server.py:63-64);
+    a crop is zero-padded (uint8 0, i.e. -0.5 after preprocessing) on the right
+    to the bucket's upper width (server.py:29-34);
+  * a bucket releases a batch when it holds MORE than batchsize crops or its
+    oldest crop waited longer than maxtime (server.py:45);
+  * a short batch is topped up with zero crops whose width is widths[0]
+    (server.py:123-128); their results are dropped (clientid '-1');
+  * one result per crop: (imgid, text) on the client's output queue, text =
+    validate._get_string of the -1-filtered labels (server.py:130-141).
+Known reference edge cases, reproduced unless fixed deliberately:
+  * a crop exactly 32 px wide fits no (w, w+32] bucket; the reference's
+    assert(success_count == 1) fails (server.py:114). Here addImage raises
+    ValueError; LocalServer(accept_narrow=True) adds a (0, 32] bucket.
+  * a 3-channel crop: the reference keeps channel 1 and drops the channel
+    axis (server.py:33-35); here channel 1 is kept WITH the axis so the batch
+    stays [bs, 32, W, 1].
+The model step runs on the GPU: convnet_layers(INFER) -> rnn_layers ->
+ctc_greedy_decoder (server.py:83-89), or the beam-search decoder when the
+service is built with decoder="beam" (BASELINE config C5, beam 16).
+"""
+import queue
+import time
+
+import numpy as np
+import torch
+
+from . import decode, validate
+from .config import INFER
+from .model import convnet_layers, rnn_layers
+from .mjsynth import num_classes
+
+BUCKET_STEP = 32
+BUCKET_MAX_WIDTH = 1000
+
+
+class Bucket:
+    """server.py:17-57."""
+
+    def __init__(self, maxtime, batchsize, widthrange):
+        self.maxtime = maxtime
+        self.batchsize = batchsize
+        self.widthrange = widthrange
+        self.imgs = []
+        self.widths = []
+        self.infos = []
+        self.oldesttime = None
+
+    def addImgToBucket(self, clientid, imgid, imgtime, img):
+        w = img.shape[1]
+        if not (self.widthrange[0] < w <= self.widthrange[1]):
+            return False
+        img = np.asarray(img)
+        if img.ndim == 3:
+            img = img[:, :, 1:2] if img.shape[2] > 1 else img
+        else:
+            img = img[:, :, None]
+        padded = np.zeros((img.shape[0], self.widthrange[1], 1), np.uint8)
+        padded[:, :w] = img
+        self.imgs.append(padded)
+        self.widths.append(w)
+        self.infos.append((clientid, imgid))
+        if self.oldesttime is None or imgtime < self.oldesttime:
+            self.oldesttime = imgtime
+        return True
+
+    def getBatch(self, now=None):
+        if not self.imgs:
+            return None
+        now = time.time() if now is None else now
+        if len(self.imgs) > self.batchsize or (now - self.oldesttime) > self.maxtime:
+            batch = np.stack(self.imgs[:self.batchsize])
+            widths = np.array(self.widths[:self.batchsize], np.int32)
+            infos = self.infos[:self.batchsize]
+            del self.imgs[:self.batchsize], self.widths[:self.batchsize], self.infos[:self.batchsize]
+            self.oldesttime = now          # as the reference (server.py:52)
+            return infos, batch, widths
+        return None
+
+
+def fill_batch(infos, batch, widths, bucket_size):
+    """server.py:123-128: top a short batch up with zero crops of width widths[0]."""
+    n = batch.shape[0]
+    if n >= bucket_size:
+        return infos, batch, widths
+    extra = bucket_size - n
+    batch = np.concatenate([batch, np.zeros((extra,) + batch.shape[1:], batch.dtype)])
+    widths = np.concatenate([widths, np.full(extra, widths[0], np.int32)])
+    return list(infos) + [("-1", "0")] * extra, batch, widths
+
+
+class Recognizer:
+    """The per-batch model step of LocalServer.run (server.py:80-89, 132-138):
+    uint8 [bs, 32, W, 1] + widths -> one string per crop. Holds the variables
+    (a ParamStore) on one GPU."""
+
+    def __init__(self, store, decoder="greedy", beam_width=16, merge_repeated=True):
+        if decoder not in ("greedy", "beam"):
+            raise ValueError("decoder is 'greedy' or 'beam'")
+        self.store = store
+        self.decoder = decoder
+        self.beam_width = beam_width
+        self.merge_repeated = merge_repeated
+
+    def labels(self, batch, widths):
+        """Dense int64 [bs, max_len] (-1 padded) device tensor."""
+        dev = self.store.device
+        with torch.no_grad():
+            image = torch.from_numpy(np.ascontiguousarray(batch, dtype=np.uint8)).to(dev, non_blocking=True)
+            width = torch.from_numpy(np.asarray(widths, np.int32)).to(dev, non_blocking=True)
+            features, seq_len = convnet_layers(image, width, INFER, self.store)
+            logits = rnn_layers(features, seq_len, num_classes(), self.store)
+            if self.decoder == "greedy":
+                return validate._get_output(logits, seq_len, self.merge_repeated)[0]
+            out, _ = decode.ctc_beam_search_decoder(logits, seq_len, self.beam_width, 1, self.merge_repeated)
+            return out[0]
+
+    def __call__(self, batch, widths):
+        return validate.decode_strings(self.labels(batch, widths))
+
+
+class LocalServer:
+    """server.py:59-145. `recognizer` is a Recognizer (or any callable
+    (batch, widths) -> list of strings); queues come from `manager` (a
+    multiprocessing Manager, or None for in-process queue.Queue)."""
+
+    def __init__(self, recognizer, manager=None, bucket_size=16, bucket_max_time=1.0, accept_narrow=False):
+        self.client_inputs = {}
+        self.client_outputs = {}
+        self.recognizer = recognizer
+        self.manager = manager
+        self.bucket_size = bucket_size
+        self.buckets = [Bucket(bucket_max_time, bucket_size, (w, w + BUCKET_STEP))
+                        for w in range(BUCKET_STEP, BUCKET_MAX_WIDTH, BUCKET_STEP)]
+        if accept_narrow:
+            self.buckets.insert(0, Bucket(bucket_max_time, bucket_size, (0, BUCKET_STEP)))
+        self.maxclientid = 0
+        self.batches_run = 0
+
+    def _queue(self):
+        return self.manager.Queue() if self.manager is not None else queue.Queue()
+
+    def register(self):
+        clientid = str(self.maxclientid)
+        self.maxclientid += 1
+        self.client_inputs[clientid] = self._queue()
+        self.client_outputs[clientid] = self._queue()
+        return clientid, self.client_inputs[clientid], self.client_outputs[clientid]
+
+    def addImage(self, clientid, imgid, imgtime, img):
+        hits = sum(b.addImgToBucket(clientid, imgid, imgtime, img) for b in self.buckets)
+        if hits != 1:                                   # server.py:114 assert(success_count == 1)
+            raise ValueError(f"crop of width {img.shape[1]} fits {hits} buckets (needs exactly 1)")
+
+    def poll_inputs(self, idle_sleep=0.0):
+        got = False
+        for clientid, q in list(self.client_inputs.items()):
+            try:
+                imgid, imgtime, img = q.get(block=False)
+            except queue.Empty:
+                if idle_sleep:
+                    time.sleep(idle_sleep)
+                continue
+            self.addImage(clientid, imgid, imgtime, img)
+            got = True
+        return got
+
+    def flush_buckets(self, now=None):
+        """Run every bucket that is ready; returns the number of batches run."""
+        n = 0
+        for bucket in self.buckets:
+            b = bucket.getBatch(now)
+            if b is None:
+                continue
+            infos, batch, widths = fill_batch(*b, self.bucket_size)
+            texts = self.recognizer(batch, widths)
+            for (clientid, imgid), txt in zip(infos, texts):
+                if clientid == "-1":
+                    continue
+                self.client_outputs[clientid].put((imgid, txt), block=False)
+            n += 1
+        self.batches_run += n
+        return n
+
+    def run(self, states=None, logger=None, stop=None, idle_sleep=0.1):
+        """server.py:94-145 main loop; returns when `stop()` is true."""
+        if states is not None:
+            states["server_started"] = True
+        if logger is not None:
+            logger.info("server started, waiting image ...")
+        while stop is None or not stop():
+            try:
+                self.poll_inputs(idle_sleep)
+                self.flush_buckets()
+            except Exception:
+                if logger is None:
+                    raise
+                logger.exception("SERVER ERROR")

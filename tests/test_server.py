@@ -1,0 +1,90 @@
+"""Width-bucketed recognise service (src/processing/server.py, linepredictor.py):
+bucket semantics on CPU with a stand-in recogniser; the GPU recogniser in
+tests/test_gpu_server.py."""
+import threading
+
+import numpy as np
+import pytest
+
+from cnn_lstm_ctc_ocr_amd.linepredictor import BatchLinePredictor
+from cnn_lstm_ctc_ocr_amd.server import Bucket, LocalServer, fill_batch
+
+
+def _crop(w, v=7):
+    return np.full((32, w), v, np.uint8)
+
+
+def test_bucket_ranges_and_right_zero_padding():
+    b = Bucket(1.0, 4, (64, 96))
+    assert not b.addImgToBucket("0", "a", 0.0, _crop(64))        # (64, 96] excludes 64
+    assert b.addImgToBucket("0", "a", 0.0, _crop(65))
+    assert b.addImgToBucket("0", "b", 0.0, _crop(96))
+    assert not b.addImgToBucket("0", "c", 0.0, _crop(97))
+    img = b.imgs[0]
+    assert img.shape == (32, 96, 1) and img.dtype == np.uint8
+    assert (img[:, :65] == 7).all() and (img[:, 65:] == 0).all()
+    assert b.widths == [65, 96]
+
+
+def test_bucket_releases_only_above_batchsize_or_after_maxtime():
+    b = Bucket(1.0, 2, (32, 64))
+    for i in range(2):
+        b.addImgToBucket("0", str(i), 10.0, _crop(40))
+    assert b.getBatch(now=10.5) is None               # exactly batchsize: waits (server.py:45 uses '>')
+    b.addImgToBucket("0", "2", 10.2, _crop(50))
+    infos, batch, widths = b.getBatch(now=10.5)
+    assert [i for _, i in infos] == ["0", "1"] and batch.shape == (2, 32, 64, 1)
+    assert widths.tolist() == [40, 40] and len(b.imgs) == 1
+    assert b.getBatch(now=11.0) is None               # oldest reset to the release time
+    assert b.getBatch(now=11.6) is not None           # maxtime elapsed
+
+
+def test_fill_batch_uses_first_width_and_marks_fillers():
+    infos, batch, widths = fill_batch([("0", "a")], np.ones((1, 32, 64, 1), np.uint8), np.array([50], np.int32), 3)
+    assert infos == [("0", "a"), ("-1", "0"), ("-1", "0")]
+    assert widths.tolist() == [50, 50, 50] and (batch[1:] == 0).all()
+
+
+def test_width_32_fits_no_bucket_unless_fixed():
+    srv = LocalServer(lambda b, w: [""] * len(w))
+    with pytest.raises(ValueError):
+        srv.addImage("0", "x", 0.0, _crop(32))
+    LocalServer(lambda b, w: [""] * len(w), accept_narrow=True).addImage("0", "x", 0.0, _crop(32))
+
+
+def test_three_channel_crop_keeps_channel_one():
+    b = Bucket(1.0, 4, (32, 64))
+    img = np.zeros((32, 40, 3), np.uint8)
+    img[:, :, 1] = 9
+    b.addImgToBucket("0", "a", 0.0, img)
+    assert b.imgs[0].shape == (32, 64, 1) and (b.imgs[0][:, :40] == 9).all()
+
+
+def test_service_round_trip_with_stand_in_recogniser():
+    """Crops of many widths from two clients come back to the right client and
+    index; filler rows never reach a client."""
+    seen = []
+
+    def recog(batch, widths):
+        seen.append((batch.shape, widths.tolist()))
+        return [f"w{w}" for w in widths]
+
+    srv = LocalServer(recog, bucket_size=4, bucket_max_time=0.0)
+    p1, p2 = BatchLinePredictor(srv), BatchLinePredictor(srv)
+    rng = np.random.default_rng(0)
+    w1 = rng.integers(33, 600, 11).tolist()
+    w2 = rng.integers(33, 600, 5).tolist()
+    stop = threading.Event()
+    th = threading.Thread(target=srv.run, kwargs={"stop": stop.is_set, "idle_sleep": 0.001})
+    th.start()
+    try:
+        r1 = p1.predict_batch("b1", [_crop(w) for w in w1], give_up_after=20000)
+        r2 = p2.predict_batch("b2", [_crop(w) for w in w2], give_up_after=20000)
+    finally:
+        stop.set()
+        th.join()
+    assert r1 == {i: f"w{w}" for i, w in enumerate(w1)}
+    assert r2 == {i: f"w{w}" for i, w in enumerate(w2)}
+    for shape, widths in seen:
+        assert shape[0] == 4 and len(widths) == 4
+        assert shape[2] % 32 == 0 and all(shape[2] - 32 < w <= shape[2] for w in widths)
