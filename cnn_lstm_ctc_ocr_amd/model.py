@@ -306,6 +306,14 @@ def rnn_layers(features, sequence_length, num_classes, store=None):
     if x.dtype != cfg.dtype:
         x = K.cast(x, cfg.dtype)
     sequence_length = sequence_length.to(device=x.device, dtype=torch.int32).contiguous()
+    # the recurrent step kernels tile the batch by 64 (bf16) / 32 (fp32) rows:
+    # pad with zero-length sequences (zero outputs, zero gradients), slice after
+    B = x.shape[1]
+    mult = 64 if cfg.dtype == torch.bfloat16 else 32
+    Bp = -(-B // mult) * mult
+    if Bp != B:
+        x = torch.cat([x, x.new_zeros(x.shape[0], Bp - B, x.shape[2])], dim=1)
+        sequence_length = torch.cat([sequence_length, sequence_length.new_zeros(Bp - B)])
     track = torch.is_grad_enabled() and x.requires_grad
     for layer in range(1, len(cfg.rnn_sizes) + 1):
         variables = []
@@ -317,7 +325,8 @@ def rnn_layers(features, sequence_length, num_classes, store=None):
         op = _BiLSTM if cfg.cell == "lstm" else _BiGRU
         x = op.apply(x, sequence_length, store, layer, *variables)
     variables = [store.params["rnn/logits/kernel"], store.params["rnn/logits/bias"]] if track else []
-    return _Logits.apply(x, store, *variables)
+    logits = _Logits.apply(x, store, *variables)
+    return logits if Bp == B else logits[:, :B]
 
 
 # ---------------------------------------------------------------------- CTC

@@ -135,3 +135,42 @@ def test_gru_infer_matches_oracle(cuda):
         logits = model.rnn_layers(feats, seq, 95, store)
     lg = logits.cpu().numpy()
     assert np.linalg.norm(lg - logits_ref) / np.linalg.norm(logits_ref) < 1e-4
+
+
+def test_ragged_batch_pads_inside_rnn_layers(cuda):
+    """B not a multiple of the step kernels' row tile (serving one crop, a
+    short last batch), fp32: loss, logits and grads match the oracle."""
+    from cnn_lstm_ctc_ocr_amd import model
+    store, vals, img, widths, labels, T = _setup(cuda, torch.float32, B=5, seed=8)
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", SIZES)
+    loss_ref, grads_ref, _, logits_ref, _ = ref.loss_and_grads(G.preprocess(img).astype(np.float64), widths, labels)
+    store.zero_grad()
+    feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN, store)
+    logits = model.rnn_layers(feats, seq, 95, store)
+    assert logits.shape[1] == 5
+    loss = model.ctc_loss_layer(logits, labels, seq)
+    loss.backward()
+    lg = logits.detach().cpu().numpy()
+    assert np.linalg.norm(lg - logits_ref) / np.linalg.norm(logits_ref) < 1e-4
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-4
+    # conv grads sit behind train-mode BN over only 5 crops: fp32 noise is amplified there
+    for name, tol in (("rnn/bdrnn1/fw/lstm_cell/kernel", 5e-4), ("rnn/logits/bias", 5e-4),
+                      ("convnet/conv3/kernel", 2e-3)):
+        g, gr = store.grads[name].cpu().numpy(), grads_ref[name]
+        assert np.linalg.norm(g - gr) / np.linalg.norm(gr) < tol, name
+
+
+def test_ragged_batch_bf16_rows_independent_of_padding(cuda):
+    """bf16 INFER: 5 crops alone (padded to 64 rows inside rnn_layers) give the
+    same logits as the same crops inside a full 64-crop batch."""
+    from cnn_lstm_ctc_ocr_amd import model
+    store, vals, img, widths, labels, T = _setup(cuda, torch.bfloat16, B=64, seed=9, sizes=(256, 256))
+    with torch.no_grad():
+        outs = []
+        for n in (64, 5):
+            feats, seq = model.convnet_layers(torch.from_numpy(img[:n]).to(cuda), torch.from_numpy(widths[:n]),
+                                              model.INFER, store)
+            outs.append(model.rnn_layers(feats, seq, 95, store).float().cpu().numpy())
+    full, alone = outs
+    assert alone.shape[1] == 5
+    np.testing.assert_allclose(alone, full[:, :5], rtol=0, atol=1e-6)
