@@ -43,6 +43,7 @@ SIGNATURES = {
     "ocrk_gru_fwd": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_gru_bwd": [_p, _p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_ctc_beam_decode": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _sz, _p],
+    "ocrk_crc32c": [_p, _sz, ctypes.c_uint32],
     "ocrk_edit_distance": [_p, _p, _i32, _p, _p, _i32, _i32, _p, _p, _p],
     "ocrk_conv1_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _p],
     "ocrk_conv1_wgrad_workspace_size": [_i32, _i32, _i32, _i32],
@@ -84,6 +85,7 @@ SIGNATURES = {
 _RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
 _RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspace_size")})
 _RESTYPE["ocrk_conv_stats_tiles"] = ctypes.c_size_t
+_RESTYPE["ocrk_crc32c"] = ctypes.c_uint32
 
 
 class OcrkError(RuntimeError):

@@ -1,6 +1,7 @@
 // libocrk runtime plumbing: version, thread-local error string, launch status.
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include "common.h"
 
 namespace ocrk {
@@ -32,3 +33,46 @@ int ocrk_version(void) { return OCRK_ABI_VERSION; }
 const char* ocrk_last_error(void) { return ocrk::g_err; }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ host CRC32C
+// Castagnoli CRC (TFRecord framing, TensorBundle checksums): SSE4.2 crc32
+// instruction when the host has it, else a byte table.
+namespace {
+uint32_t crc_table[256];
+bool crc_table_ready = false;
+
+void build_crc_table() {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+        crc_table[i] = c;
+    }
+    crc_table_ready = true;
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t c, const unsigned char* p, size_t n) {
+    uint64_t c64 = c;
+    while (n >= 8) {
+        uint64_t v;
+        memcpy(&v, p, 8);
+        c64 = __builtin_ia32_crc32di(c64, v);
+        p += 8;
+        n -= 8;
+    }
+    c = (uint32_t)c64;
+    while (n--) c = __builtin_ia32_crc32qi(c, *p++);
+    return c;
+}
+}  // namespace
+
+extern "C" uint32_t ocrk_crc32c(const void* data, size_t n, uint32_t crc) {
+    const unsigned char* p = static_cast<const unsigned char*>(data);
+    uint32_t c = ~crc;
+    if (__builtin_cpu_supports("sse4.2")) {
+        c = crc32c_hw(c, p, n);
+    } else {
+        if (!crc_table_ready) build_crc_table();
+        for (size_t i = 0; i < n; ++i) c = crc_table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    }
+    return ~c;
+}

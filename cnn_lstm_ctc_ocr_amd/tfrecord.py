@@ -24,7 +24,30 @@ def _crc32c_table():
     return _CRC_TABLE
 
 
+_NATIVE = []
+
+
+def _native_crc():
+    """libocrk's host CRC32C (SSE4.2), or None when the library is absent."""
+    if not _NATIVE:
+        try:
+            from . import _lib
+            fn = _lib.lib().ocrk_crc32c
+            _NATIVE.append(lambda b: int(fn(b, len(b), 0)))
+        except Exception:                               # library not built: pure Python
+            _NATIVE.append(None)
+    return _NATIVE[0]
+
+
 def crc32c(data):
+    data = bytes(data)
+    native = _native_crc()
+    if native is not None:
+        return native(data)
+    return crc32c_py(data)
+
+
+def crc32c_py(data):
     tbl = _crc32c_table()
     c = 0xFFFFFFFF
     for b in data:

@@ -235,6 +235,11 @@ int ocrk_mean(const float* x, int n, float* out, void* stream);
 /* model.py:152-163: seq_len = floor((width - 2) / 2) - 2 */
 int ocrk_seq_len(const int* widths, int n, int* out, void* stream);
 
+/* Host-side CRC32C (Castagnoli) of n bytes continuing from `crc` (0 to start):
+ * TFRecord framing and TensorBundle checksums for the input pipeline and the
+ * checkpoint reader/writer (src/weinman/mjsynth.py:148-172, train.py:152-165). */
+uint32_t ocrk_crc32c(const void* data, size_t n, uint32_t crc);
+
 #ifdef __cplusplus
 }
 #endif
