@@ -13,7 +13,7 @@ def _declarations():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"^(int|size_t|const char\*)\s+(ocrk_\w+)\(([^;]*)\);", text, re.M):
+    for m in re.finditer(r"^(int|size_t|uint32_t|const char\*)\s+(ocrk_\w+)\(([^;]*)\);", text, re.M):
         args = m.group(3).strip()
         n = 0 if args in ("", "void") else len(args.split(","))
         decls[m.group(2)] = (m.group(1), n)
