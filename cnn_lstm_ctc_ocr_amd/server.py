@@ -199,3 +199,22 @@ class LocalServer:
                 if logger is None:
                     raise
                 logger.exception("SERVER ERROR")
+
+
+def predict_signature(store, images, width, beam_width=128, top_paths=3, merge_repeated=False):
+    """The serving signature src/weinman/client.py consumes (model 'clreceipt',
+    inputs 'images' u8 [bs, 32, W, 1] and 'width' i32 [bs]; client.py:101-123):
+    'output0' = beam log-probabilities [bs, top_paths], 'output1'..'output<top_paths>'
+    = the decoded paths as dense int64 [bs, len] (-1 padded), from
+    ctc_beam_search_decoder(beam_width=128, merge_repeated=False) (client.py:222-233)."""
+    dev = store.device
+    with torch.no_grad():
+        image = torch.as_tensor(np.asarray(images, np.uint8)).to(dev)
+        w = torch.as_tensor(np.asarray(width, np.int32)).to(dev)
+        features, seq_len = convnet_layers(image, w, INFER, store)
+        logits = rnn_layers(features, seq_len, num_classes(), store)
+        paths, logp = decode.ctc_beam_search_decoder(logits, seq_len, beam_width, top_paths, merge_repeated)
+    out = {"output0": logp.cpu().numpy()}
+    for k, p in enumerate(paths, start=1):
+        out[f"output{k}"] = p.cpu().numpy()
+    return out
