@@ -333,6 +333,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmParams p) 
     }
 }
 
+static int splitk_finish(const GemmParams& p, hipStream_t stream) {
+    if (p.splits <= 1) return OCRK_OK;
+    int64_t MN = (int64_t)p.M * p.N;
+    dim3 rg((unsigned)std::min<int64_t>(cdiv(MN, 256), 4096), (unsigned)p.batch);
+    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(p);
+    return launch_status("gemm splitk reduce");
+}
+
 size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
     return splits > 1 ? (size_t)batch * splits * M * N * sizeof(float) : 0;
 }
@@ -346,11 +354,8 @@ static int launch_tiles(const GemmParams& p0, hipStream_t stream) {
     else if (TBN == 64) gemm_kernel<CT, AM, BMD, 128, 64><<<grid, 256, 0, stream>>>(p);
     else gemm_kernel<CT, AM, BMD, 128, 128><<<grid, 256, 0, stream>>>(p);
     int st = launch_status("gemm");
-    if (st != OCRK_OK || p.splits <= 1) return st;
-    int64_t MN = (int64_t)p.M * p.N;
-    dim3 rg((unsigned)std::min<int64_t>(cdiv(MN, 256), 4096), (unsigned)p.batch);
-    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(p);
-    return launch_status("gemm splitk reduce");
+    if (st != OCRK_OK) return st;
+    return splitk_finish(p, stream);
 }
 
 template <typename CT>
@@ -379,6 +384,8 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     OCRK_REQUIRE(amode < A_IM2COL || p.convC % 8 == 0, "gemm: conv channels must be a multiple of 8");
     OCRK_REQUIRE(!(p.stats && (p.splits > 1 || p.batch > 1)), "gemm: stats need splits=1, batch=1");
     OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
+    int nt = gemm_nt(p, amode, bmode, dtype, stream);
+    if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     if (dtype == OCRK_BF16) return dispatch_modes<bf16>(p, amode, bmode, stream);
     if (dtype == OCRK_F32) return dispatch_modes<float>(p, amode, bmode, stream);
     set_error("gemm: unsupported dtype %d", dtype);

@@ -26,12 +26,13 @@ namespace {
 // ------------------------------------------------------------ forward gate
 template <typename CT, int BR, int HU, int KC>
 __global__ void __launch_bounds__(256)
-gru_fwd_gate_kernel(const float* __restrict__ gx, const CT* __restrict__ whgT, const CT* __restrict__ h,
+gru_fwd_gate_kernel(const CT* __restrict__ gx, const CT* __restrict__ whgT, const CT* __restrict__ h,
                     CT* __restrict__ rh, const int* __restrict__ seq_len, int s, int B, int H,
                     CT* __restrict__ rh_t, CT* __restrict__ acts_t) {
     using Core = RecurCore<CT, BR, 2 * HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G3 = 3 * H;
     constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
     constexpr bool EFULL = (BR * UQ) % 256 == 0;
@@ -51,7 +52,7 @@ gru_fwd_gate_kernel(const float* __restrict__ gx, const CT* __restrict__ whgT, c
         const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
         ld4(ph[q], h + ((int64_t)dir * B + b) * H + uu);
         const int t = step_time(dir, s, plen[q]);
-        const float* g = gx + (((int64_t)t * B + b) * 2 + dir) * G3 + uu;
+        const CT* g = gx + (((int64_t)t * B + b) * 2 + dir) * G3 + uu;
         ld4(pg[q][0], g);
         ld4(pg[q][1], g + H);
     }
@@ -95,12 +96,13 @@ gru_fwd_gate_kernel(const float* __restrict__ gx, const CT* __restrict__ whgT, c
 // ------------------------------------------------------- forward candidate
 template <typename CT, int BR, int HU, int KC>
 __global__ void __launch_bounds__(256)
-gru_fwd_cand_kernel(const float* __restrict__ gx, const CT* __restrict__ whcT, const CT* __restrict__ rh,
+gru_fwd_cand_kernel(const CT* __restrict__ gx, const CT* __restrict__ whcT, const CT* __restrict__ rh,
                     CT* __restrict__ h, const int* __restrict__ seq_len, int s, int B, int H,
                     CT* __restrict__ out, CT* __restrict__ hprev_t, CT* __restrict__ acts_t) {
     using Core = RecurCore<CT, BR, HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G3 = 3 * H;
     constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
     constexpr bool EFULL = (BR * UQ) % 256 == 0;
@@ -209,7 +211,8 @@ gru_bwd_cand_kernel(const CT* __restrict__ whc, const CT* __restrict__ dzc, cons
                     CT* __restrict__ dG_t) {
     using Core = RecurCore<CT, BR, HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G3 = 3 * H;
     constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
     constexpr bool EFULL = (BR * UQ) % 256 == 0;
@@ -282,7 +285,8 @@ gru_bwd_gate_kernel(const CT* __restrict__ whg, const CT* __restrict__ dzg, cons
                     CT* __restrict__ dG_t) {
     using Core = RecurCore<CT, BR, HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
     constexpr bool EFULL = (BR * UQ) % 256 == 0;
     int plen[EPQ4];
@@ -339,29 +343,29 @@ static int gru_check(const char* what, int B, int H, int dtype) {
     return OCRK_OK;
 }
 
-extern "C" int ocrk_gru_fwd_step(const float* gx, const void* whgT, const void* whcT, void* h, void* rh,
+extern "C" int ocrk_gru_fwd_step(const void* gx, const void* whgT, const void* whcT, void* h, void* rh,
                                  const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t,
                                  void* rh_t, void* acts_t, int dtype, void* stream) {
     if (int e = gru_check("ocrk_gru_fwd_step", B, H, dtype)) return e;
     OCRK_REQUIRE(s >= 0 && s < T, "ocrk_gru_fwd_step: step %d not in [0, %d)", s, T);
     hipStream_t st = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16) {
-        gru_fwd_gate_kernel<GATE_BF16><<<dim3(H / 16, B / 64, 2), 256, 0, st>>>(
-            gx, (const bf16*)whgT, (const bf16*)h, (bf16*)rh, seq_len, s, B, H, (bf16*)rh_t, (bf16*)acts_t);
-        gru_fwd_cand_kernel<CAND_BF16><<<dim3(H / 16, B / 64, 2), 256, 0, st>>>(
-            gx, (const bf16*)whcT, (const bf16*)rh, (bf16*)h, seq_len, s, B, H, (bf16*)out, (bf16*)hprev_t,
+        gru_fwd_gate_kernel<GATE_BF16><<<dim3(H / 16 * (B / 64) * 2), 256, 0, st>>>(
+            (const bf16*)gx, (const bf16*)whgT, (const bf16*)h, (bf16*)rh, seq_len, s, B, H, (bf16*)rh_t, (bf16*)acts_t);
+        gru_fwd_cand_kernel<CAND_BF16><<<dim3(H / 16 * (B / 64) * 2), 256, 0, st>>>(
+            (const bf16*)gx, (const bf16*)whcT, (const bf16*)rh, (bf16*)h, seq_len, s, B, H, (bf16*)out, (bf16*)hprev_t,
             (bf16*)acts_t);
     } else {
-        gru_fwd_gate_kernel<GATE_F32><<<dim3(H / 8, B / 32, 2), 256, 0, st>>>(
-            gx, (const float*)whgT, (const float*)h, (float*)rh, seq_len, s, B, H, (float*)rh_t, (float*)acts_t);
-        gru_fwd_cand_kernel<CAND_F32><<<dim3(H / 16, B / 32, 2), 256, 0, st>>>(
-            gx, (const float*)whcT, (const float*)rh, (float*)h, seq_len, s, B, H, (float*)out, (float*)hprev_t,
+        gru_fwd_gate_kernel<GATE_F32><<<dim3(H / 8 * (B / 32) * 2), 256, 0, st>>>(
+            (const float*)gx, (const float*)whgT, (const float*)h, (float*)rh, seq_len, s, B, H, (float*)rh_t, (float*)acts_t);
+        gru_fwd_cand_kernel<CAND_F32><<<dim3(H / 16 * (B / 32) * 2), 256, 0, st>>>(
+            (const float*)gx, (const float*)whcT, (const float*)rh, (float*)h, seq_len, s, B, H, (float*)out, (float*)hprev_t,
             (float*)acts_t);
     }
     return ocrk::launch_status("ocrk_gru_fwd_step");
 }
 
-extern "C" int ocrk_gru_fwd(const float* gx, const void* whgT, const void* whcT, void* h, void* rh,
+extern "C" int ocrk_gru_fwd(const void* gx, const void* whgT, const void* whcT, void* h, void* rh,
                             const int* seq_len, int T, int B, int H, void* out, void* hprev_t, void* rh_t,
                             void* acts_t, int dtype, void* stream) {
     for (int s = 0; s < T; ++s) {
@@ -384,10 +388,10 @@ extern "C" int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* d
                                                                (const bf16*)acts_t, dh_tot, (bf16*)dzc,
                                                                (bf16*)dG_t);
         for (int s = T - 1; s >= 0; --s) {
-            gru_bwd_cand_kernel<CAND_BF16><<<dim3(H / 16, B / 64, 2), 256, 0, st>>>(
+            gru_bwd_cand_kernel<CAND_BF16><<<dim3(H / 16 * (B / 64) * 2), 256, 0, st>>>(
                 (const bf16*)whc, (const bf16*)dzc, dh_tot, (bf16*)dzg, direct, seq_len, s, B, H,
                 (const bf16*)hprev_t, (const bf16*)acts_t, (bf16*)dG_t);
-            gru_bwd_gate_kernel<GATE_BF16><<<dim3(H / 16, B / 64, 2), 256, 0, st>>>(
+            gru_bwd_gate_kernel<GATE_BF16><<<dim3(H / 16 * (B / 64) * 2), 256, 0, st>>>(
                 (const bf16*)whg, (const bf16*)dzg, direct, dh_tot, (bf16*)dzc, seq_len, s, B, H,
                 (const bf16*)dout, (const bf16*)acts_t, (bf16*)dG_t);
         }
@@ -396,10 +400,10 @@ extern "C" int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* d
                                                                 (const float*)acts_t, dh_tot, (float*)dzc,
                                                                 (float*)dG_t);
         for (int s = T - 1; s >= 0; --s) {
-            gru_bwd_cand_kernel<CAND_F32><<<dim3(H / 16, B / 32, 2), 256, 0, st>>>(
+            gru_bwd_cand_kernel<CAND_F32><<<dim3(H / 16 * (B / 32) * 2), 256, 0, st>>>(
                 (const float*)whc, (const float*)dzc, dh_tot, (float*)dzg, direct, seq_len, s, B, H,
                 (const float*)hprev_t, (const float*)acts_t, (float*)dG_t);
-            gru_bwd_gate_kernel<CAND_F32><<<dim3(H / 16, B / 32, 2), 256, 0, st>>>(
+            gru_bwd_gate_kernel<CAND_F32><<<dim3(H / 16 * (B / 32) * 2), 256, 0, st>>>(
                 (const float*)whg, (const float*)dzg, direct, dh_tot, (float*)dzc, seq_len, s, B, H,
                 (const float*)dout, (const float*)acts_t, (float*)dG_t);
         }

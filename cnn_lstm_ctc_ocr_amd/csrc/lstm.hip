@@ -38,14 +38,15 @@ __device__ __forceinline__ void stamp(long long* dbg, int i) {
 // into registers at kernel entry so their HBM latency hides under the GEMM.
 template <typename CT, int BR, int HU, int KC>
 __global__ void __launch_bounds__(256)
-lstm_fwd_step_kernel(const float* __restrict__ gx, const CT* __restrict__ whT, const CT* __restrict__ h_in,
+lstm_fwd_step_kernel(const CT* __restrict__ gx, const CT* __restrict__ whT, const CT* __restrict__ h_in,
                      CT* __restrict__ h_out, float* __restrict__ c_state, const int* __restrict__ seq_len,
                      int s, int T, int B, int H, CT* __restrict__ out, CT* __restrict__ hprev_t,
                      float* __restrict__ cprev_t, CT* __restrict__ acts_t, long long* __restrict__ dbg) {
     using Core = RecurCore<CT, BR, 4 * HU, KC>;
     stamp(dbg, 0);
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G4 = 4 * H;
 
     // thread <-> (row r, 4 consecutive units u..u+3) of the epilogue
@@ -73,7 +74,7 @@ lstm_fwd_step_kernel(const float* __restrict__ gx, const CT* __restrict__ whT, c
         ld4(pc[q], c_state + st);
         ld4(ph[q], h_in + st);
         const int t = step_time(dir, s, plen[q]);
-        const float* g = gx + (((int64_t)t * B + b) * 2 + dir) * G4 + uu;
+        const CT* g = gx + (((int64_t)t * B + b) * 2 + dir) * G4 + uu;
 #pragma unroll
         for (int k = 0; k < 4; ++k) ld4(pg[q][k], g + k * H);
     }
@@ -132,7 +133,8 @@ lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT
                      const CT* __restrict__ acts_t, CT* __restrict__ dG_t) {
     using Core = RecurCore<CT, BR, HU, KC>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
-    const int u0 = blockIdx.x * HU, b0 = blockIdx.y * BR, dir = blockIdx.z;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G4 = 4 * H;
 
     constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
@@ -215,18 +217,18 @@ extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return
 #define BWD_BF16 bf16, 64, 16, 256
 #define BWD_F32 float, 32, 16, 128
 
-extern "C" int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void* h_out,
+extern "C" int ocrk_lstm_fwd_step(const void* gx, const void* whT, const void* h_in, void* h_out,
                                   float* c_state, const int* seq_len, int s, int T, int B, int H, void* out,
                                   void* hprev_t, float* cprev_t, void* acts_t, int dtype, void* stream) {
     hipStream_t st = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 256 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 256 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
-        dim3 grid(H / 16, B / 64, 2);
-        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
+        dim3 grid(H / 16 * (B / 64) * 2);
+        lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
     } else {
         OCRK_REQUIRE(H % 64 == 0 && B % 32 == 0, "ocrk_lstm_fwd_step: f32 needs H %% 64 == 0 and B %% 32 == 0 (H=%d B=%d)", H, B);
-        dim3 grid(H / 8, B / 32, 2);
-        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>(gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, (float*)acts_t, g_lstm_dbg);
+        dim3 grid(H / 8 * (B / 32) * 2);
+        lstm_fwd_step_kernel<FWD_F32><<<grid, 256, 0, st>>>((const float*)gx, (const float*)whT, (const float*)h_in, (float*)h_out, c_state, seq_len, s, T, B, H, (float*)out, (float*)hprev_t, cprev_t, (float*)acts_t, g_lstm_dbg);
     }
     return ocrk::launch_status("ocrk_lstm_fwd_step");
 }
@@ -238,18 +240,18 @@ extern "C" int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_ou
     hipStream_t st = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 64 == 0 && B % 64 == 0, "ocrk_lstm_bwd_step: bf16 needs H %% 64 == 0 and B %% 64 == 0");
-        dim3 grid(H / 16, B / 64, 2);
+        dim3 grid(H / 16 * (B / 64) * 2);
         lstm_bwd_step_kernel<BWD_BF16><<<grid, 256, 0, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, H, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t);
     } else {
         OCRK_REQUIRE(H % 32 == 0 && B % 32 == 0, "ocrk_lstm_bwd_step: f32 needs H %% 32 == 0 and B %% 32 == 0");
-        dim3 grid(H / 16, B / 32, 2);
+        dim3 grid(H / 16 * (B / 32) * 2);
         lstm_bwd_step_kernel<BWD_F32><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, (const float*)acts_t, (float*)dG_t);
     }
     return ocrk::launch_status("ocrk_lstm_bwd_step");
 }
 
 // Whole time loops (T launches each) so a binding makes one call per layer.
-extern "C" int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state /*[2 bufs][2][B][H]*/,
+extern "C" int ocrk_lstm_fwd(const void* gx, const void* whT, void* h_state /*[2 bufs][2][B][H]*/,
                              float* c_state, const int* seq_len, int T, int B, int H, void* out, void* hprev_t,
                              float* cprev_t, void* acts_t, int dtype, void* stream) {
     size_t esz = dtype == OCRK_BF16 ? 2 : 4;

@@ -57,7 +57,7 @@ extern long long* g_lstm_dbg;
 // KS = H / 32 k-steps
 template <int KS>
 __global__ void __launch_bounds__(256, 1)
-lstm_fwd_persistent_kernel(const float* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
+lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
                            const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out,
                            bf16* __restrict__ hprev_t, float* __restrict__ cprev_t, bf16* __restrict__ acts_t,
                            unsigned* __restrict__ cnt, unsigned* __restrict__ err, long long* __restrict__ dbg) {
@@ -116,9 +116,9 @@ lstm_fwd_persistent_kernel(const float* __restrict__ gx, const bf16* __restrict_
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int t = step_time_p(dir, s, plen[p]);
-            const float* gp = gx + (((int64_t)t * B + prow[p]) * 2 + dir) * G4 + my_unit;
+            const bf16* gp = gx + (((int64_t)t * B + prow[p]) * 2 + dir) * G4 + my_unit;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) pg[p][k] = gp[k * H];
+            for (int k = 0; k < 4; ++k) pg[p][k] = (float)gp[k * H];
         }
 
         floatx4 acc[2][2];
@@ -271,7 +271,7 @@ extern "C" int ocrk_lstm_fwd_persistent_supported(int B, int H) {
     return grid <= (long)cus * per_cu ? 1 : 0;
 }
 
-extern "C" int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const int* seq_len, int T, int B, int H,
+extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                                         void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
                                         void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_lstm_fwd_persistent_supported(B, H), "ocrk_lstm_fwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
@@ -283,10 +283,10 @@ extern "C" int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const 
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
     dim3 grid(H / PHU, B / PBR, 2);
     if (H == 512)
-        lstm_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
+        lstm_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                              (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
     else
-        lstm_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>(gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
+        lstm_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                             (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
     return ocrk::launch_status("ocrk_lstm_fwd_persistent");
 }

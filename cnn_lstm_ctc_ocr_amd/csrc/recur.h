@@ -167,4 +167,32 @@ __device__ __forceinline__ int step_time(int dir, int s, int len) {
     return (dir == 0 || s >= len) ? s : len - 1 - s;
 }
 
+// Workgroup -> (unit block, batch block, direction) of a recurrent step
+// launch on a 1-D grid of nU * nB * 2 workgroups. Dispatch hands consecutive
+// block ids round-robin to the 8 XCDs, so the map puts all unit blocks of one
+// (batch block, direction) group on the same XCD whenever the group count
+// allows: the group's h tile, which every one of its unit blocks reads each
+// step, then comes from MALL once per XCD and hits L2 after that, and the
+// direction's W_h slices stay in that XCD's L2 across steps. (Placement is a
+// speed choice only: nothing depends on it for correctness.)
+struct StepTile { int u, b, dir; };
+__device__ __forceinline__ StepTile step_tile(int nU, int nB) {
+    const int id = blockIdx.x, G = 2 * nB;
+    const int xcd = id & 7, slot = id >> 3;
+    int group, u;
+    if (G <= 8 && 8 % G == 0 && nU % (8 / G) == 0) {
+        const int q = 8 / G;
+        group = xcd % G;
+        u = slot * q + xcd / G;
+    } else if (G % 8 == 0) {
+        const int r = G / 8;
+        group = xcd + 8 * (slot % r);
+        u = slot / r;
+    } else {
+        group = id / nU;
+        u = id % nU;
+    }
+    return {u, group >> 1, group & 1};
+}
+
 }  // namespace ocrk

@@ -222,6 +222,8 @@ def lstm_error_word(device):
 
 def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
     _chk(gx, whT, seq_len)
+    if gx.dtype != dtype or whT.dtype != dtype:
+        raise TypeError(f"lstm_fwd: gx and whT must be {dtype} (got {gx.dtype}, {whT.dtype})")
     dev = gx.device
     if lstm_persistent_ok(B, H, dtype):
         out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
@@ -260,6 +262,8 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
 def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
     """Returns out [T,B,2H], hprev_t, rh_t [T,B,2,H], acts_t [T,B,2,3H] (dtype)."""
     _chk(gx, whgT, whcT, seq_len)
+    if gx.dtype != dtype or whgT.dtype != dtype:
+        raise TypeError(f"gru_fwd: gx and weights must be {dtype} (got {gx.dtype}, {whgT.dtype})")
     dev = gx.device
     h = torch.zeros(2, B, H, dtype=dtype, device=dev)
     rh = torch.empty(2, B, H, dtype=dtype, device=dev)

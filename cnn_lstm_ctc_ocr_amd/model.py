@@ -170,7 +170,7 @@ class _BiLSTM(torch.autograd.Function):
         T, B, n_in = x.shape
         H = store.cfg.rnn_sizes[layer - 1]
         wxT, _wx, whT, _wh, bias = store.lstm_images(layer, dt)
-        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias)          # [T*B, 8H] f32
+        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
         out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt)
         ctx.store, ctx.layer, ctx.H = store, layer, H
         ctx.save_for_backward(x, seq_len, hprev, cprev, acts)
@@ -214,7 +214,7 @@ class _BiGRU(torch.autograd.Function):
         T, B, n_in = x.shape
         H = store.cfg.rnn_sizes[layer - 1]
         wxT, _wx, whgT, whcT, _whg, _whc, bias = store.gru_images(layer, dt)
-        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias)          # [T*B, 6H] f32
+        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 6H]
         out, hprev, rh, acts = K.gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dt)
         ctx.store, ctx.layer, ctx.H = store, layer, H
         ctx.save_for_backward(x, seq_len, hprev, rh, acts)

@@ -145,7 +145,7 @@ int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, in
 /* ------------------------------------------------------------- recurrent
  * a7' -- rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199), both
  * directions, one launch per time step. Layouts (time order, d = direction):
- *   gx      f32 [T][B][2][4H]  = x . W_x + b  (ocrk_gemm, N = 8H)
+ *   gx      dtype [T][B][2][4H] = x . W_x + b  (ocrk_gemm, N = 8H; bf16 in bf16 mode)
  *   whT     dtype [2][4H][H]   (recurrent kernel rows of [In+H][4H], transposed)
  *   wh      dtype [2][H][4H]   (recurrent kernel rows as stored)
  *   h_state dtype [2 bufs][2][B][H], c_state f32 [2][B][H] (zero before s = 0)
@@ -153,7 +153,7 @@ int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, in
  *   hprev_t dtype [T][B][2][H], cprev_t f32 [T][B][2][H], acts_t dtype [T][B][2][4H] (gate activations)
  *   dout    dtype [T][B][2H]   dG_t dtype [T][B][2][4H]
  *   dg_state dtype [2 bufs][2][B][4H], dc_state f32 [2][B][H] (zero before the loop) */
-int ocrk_lstm_fwd_step(const float* gx, const void* whT, const void* h_in, void* h_out, float* c_state,
+int ocrk_lstm_fwd_step(const void* gx, const void* whT, const void* h_in, void* h_out, float* c_state,
                        const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t,
                        float* cprev_t, void* acts_t, int dtype, void* stream);
 int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* dc_state, const int* seq_len,
@@ -167,7 +167,7 @@ int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* d
  * (u32, device) is set non-zero if a hand-off wait timed out. */
 int ocrk_lstm_fwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
-int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const int* seq_len, int T, int B, int H,
+int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                              void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err, void* ws,
                              size_t ws_bytes, void* stream);
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
@@ -175,15 +175,15 @@ int ocrk_lstm_fwd_persistent(const float* gx, const void* whT, const int* seq_le
 int ocrk_lstm_debug_stamps(long long* buf);
 /* a7 -- rnn_layer with tf.contrib.rnn.GRUCell (src/weinman/model.py:167-199; [TF1] GRUCell:
  * [r, u] = sig([x, h] Wg + bg), c = tanh([x, r*h] Wc + bc), h' = u h + (1 - u) c) under
- * bidirectional_dynamic_rnn(time_major, sequence_length). gx f32 [T][B][2][3H] = x . [Wg_x | Wc_x]
+ * bidirectional_dynamic_rnn(time_major, sequence_length). gx dtype [T][B][2][3H] = x . [Wg_x | Wc_x]
  * + [bg | bc] per direction (one GEMM). whgT dtype [2][2H][H], whcT [2][H][H] (h-parts,
  * transposed). State h [2][B][H] and rh [2][B][H] (zeroed h). Outputs: out [T][B][2H] (zeroed by
  * the caller; rows past seq_len stay 0), time-order hprev_t, rh_t [T][B][2][H], acts_t
  * [T][B][2][3H] = (r, u, c). One step = two launches (gate, candidate) for both directions. */
-int ocrk_gru_fwd_step(const float* gx, const void* whgT, const void* whcT, void* h, void* rh,
+int ocrk_gru_fwd_step(const void* gx, const void* whgT, const void* whcT, void* h, void* rh,
                       const int* seq_len, int s, int T, int B, int H, void* out, void* hprev_t, void* rh_t,
                       void* acts_t, int dtype, void* stream);
-int ocrk_gru_fwd(const float* gx, const void* whgT, const void* whcT, void* h, void* rh, const int* seq_len,
+int ocrk_gru_fwd(const void* gx, const void* whgT, const void* whcT, void* h, void* rh, const int* seq_len,
                  int T, int B, int H, void* out, void* hprev_t, void* rh_t, void* acts_t, int dtype,
                  void* stream);
 /* GRU BPTT: whg dtype [2][H][2H], whc [2][H][H] (h-parts, untransposed); scratch dzg [2][B][2H],
@@ -192,7 +192,7 @@ int ocrk_gru_fwd(const float* gx, const void* whgT, const void* whcT, void* h, v
 int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* dzc, float* dh_tot, float* direct,
                  const int* seq_len, int T, int B, int H, const void* dout, const void* hprev_t,
                  const void* acts_t, void* dG_t, int dtype, void* stream);
-int ocrk_lstm_fwd(const float* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
+int ocrk_lstm_fwd(const void* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
                   int T, int B, int H, void* out, void* hprev_t, float* cprev_t, void* acts_t, int dtype,
                   void* stream);
 int ocrk_lstm_bwd(const void* wh, void* dg_state, float* dc_state, const int* seq_len, int T, int B, int H,

@@ -161,7 +161,8 @@ def test_lstm_layer_fwd_bwd(cuda, dtype):
     wh = np.stack([k[n_in:] for k in ks])                          # [2][H][4H]
     bias = np.concatenate(bs)
     seq_d = _t(seq, cuda)
-    gx = Kn.gemm(_t(x.reshape(T * B, n_in), cuda, dtype), _t(wxT, cuda, dtype), trans_b=True, bias=_t(bias, cuda))
+    gx = Kn.gemm(_t(x.reshape(T * B, n_in), cuda, dtype), _t(wxT, cuda, dtype), trans_b=True, bias=_t(bias, cuda),
+                 out_dtype=dtype)
     out, hprev, cprev, acts = Kn.lstm_fwd(gx, _t(whT, cuda, dtype), seq_d, T, B, H, dtype)
     tol = 1e-4 if dtype == torch.float32 else 3e-2
     assert _rel(out.float().cpu().numpy(), ref) < tol

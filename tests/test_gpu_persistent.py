@@ -23,7 +23,7 @@ def test_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch):
     whT = np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))
     gx = K.gemm(torch.from_numpy(x.reshape(T * B, n_in)).to(cuda).bfloat16(),
                 torch.from_numpy(wxT).to(cuda).bfloat16(), trans_b=True,
-                bias=torch.from_numpy(np.concatenate(bs)).to(cuda))
+                bias=torch.from_numpy(np.concatenate(bs)).to(cuda), out_dtype=torch.bfloat16)
     whT_d = torch.from_numpy(whT).to(cuda).bfloat16()
     seq_d = torch.from_numpy(seq).to(cuda)
     monkeypatch.setenv("OCRK_LSTM_PERSISTENT", "0")

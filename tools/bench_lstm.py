@@ -5,7 +5,7 @@ from cnn_lstm_ctc_ocr_amd import kernels as K, _lib
 
 def run(B, H=512, n_in=1024, T=125, reps=3, dt=torch.bfloat16):
     dev = torch.device("cuda")
-    gx = torch.randn(T * B, 8 * H, device=dev)
+    gx = torch.randn(T * B, 8 * H, device=dev).to(dt)
     whT = (torch.randn(2, 4 * H, H, device=dev) * 0.02).to(dt)
     wh = (torch.randn(2, H, 4 * H, device=dev) * 0.02).to(dt)
     seq = torch.full((B,), T, dtype=torch.int32, device=dev)
@@ -35,7 +35,7 @@ if "--stamps" in sys.argv:
     B, H, T = 256, 512, 8
     dev = torch.device("cuda")
     dbg = torch.zeros(2 * 4 * 32 * 8, dtype=torch.int64, device=dev)
-    gx = torch.randn(T * B, 8 * H, device=dev)
+    gx = torch.randn(T * B, 8 * H, device=dev).bfloat16()
     whT = (torch.randn(2, 4 * H, H, device=dev) * 0.02).bfloat16()
     seq = torch.full((B,), T, dtype=torch.int32, device=dev)
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
@@ -59,7 +59,7 @@ if "--persistent" in sys.argv:
     for B in (64, 256):
         H, T = 512, 125
         dev = torch.device("cuda")
-        gx = torch.randn(T * B, 8 * H, device=dev)
+        gx = torch.randn(T * B, 8 * H, device=dev).bfloat16()
         whT = (torch.randn(2, 4 * H, H, device=dev) * 0.05).bfloat16()
         seq = torch.randint(T // 2, T + 1, (B,), dtype=torch.int32, device=dev)
         os.environ["OCRK_LSTM_PERSISTENT"] = "0"
@@ -88,7 +88,7 @@ if "--pstamps" in sys.argv:
     K._PERSISTENT.clear()
     B, H, T = 256, 512, 125
     dev = torch.device("cuda")
-    gx = torch.randn(T * B, 8 * H, device=dev)
+    gx = torch.randn(T * B, 8 * H, device=dev).bfloat16()
     whT = (torch.randn(2, 4 * H, H, device=dev) * 0.05).bfloat16()
     seq = torch.full((B,), T, dtype=torch.int32, device=dev)
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
