@@ -50,8 +50,7 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
 
 // Pipelined LDS-DMA engine for bf16 A_ROWK / A_IM2COL / A_IM2COL_FLIP x B_NK
 // (gemm_nt.hip). Returns -1 when it does not cover the call (the caller then
-// uses the generic engine), else a status. Opt-in with OCRK_GEMM_NT=1 (measured
-// slower than gemm.hip so far at 1 workgroup per CU; tools/bench_gemm.py).
+// uses the generic engine), else a status. OCRK_GEMM_NT=0 disables it.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
 }  // namespace ocrk

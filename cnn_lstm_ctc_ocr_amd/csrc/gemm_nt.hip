@@ -6,16 +6,16 @@
 // projections and the dx GEMMs (gemm.h lists the modes).
 //
 // Structure (cdna_hip_programming.md section 5, "pipelining across
-// barriers"): 256 threads, BM x BN x 64 tiles, a 3-stage LDS ring filled by
-// LDS-DMA (buffer_load_dwordx4 ... lds) so loads for stages k+1 and k+2 are in
-// flight while stage k is on MFMA; one raw s_barrier per k-step, counted
-// s_waitcnt vmcnt (never __syncthreads inside the loop: its fence would drain
-// the DMA queue).
-// LDS images are lane-linear: one wave instruction writes 8 rows x 128 B.
-// The 16-B chunk index of each row is XOR-swizzled with (row & 7) on the
-// GLOBAL side (lane L of a row loads chunk (L & 7) ^ (L >> 3)), so the MFMA
-// fragment reads (16 rows, one chunk each) hit 8 distinct chunk slots per
-// 8 lanes: conflict-free ds_read_b128.
+// barriers"): 256 threads, BM x BN x BK tiles, an S-stage LDS ring filled by
+// LDS-DMA (buffer_load_dwordx4 ... lds) so the loads of the next S-1 stages
+// are in flight while one stage is on MFMA; one raw s_barrier per k-step,
+// counted s_waitcnt vmcnt (never __syncthreads inside the loop: its fence
+// would drain the DMA queue).
+// LDS images are lane-linear: one wave instruction writes 1 KB = 8 rows of
+// 128 B (BK = 64) or 16 rows of 64 B (BK = 32). The 16-B chunk index of each
+// row is XOR-swizzled on the GLOBAL side (BK=64: slot = chunk ^ (row & 7);
+// BK=32: slot = chunk ^ ((row >> 2) & 3)) so every 8 lanes of an MFMA
+// fragment read (16 rows, one chunk each) hit 8 distinct 16-B bank groups.
 // Zero fill (im2col padding taps, rows >= M / N, k >= K): the lane's buffer
 // offset is pushed past the resource's num_records, which returns 0.
 #include "gemm.h"
@@ -25,30 +25,42 @@ namespace ocrk {
 
 namespace {
 
-constexpr int NT_BK = 64;            // k per stage (128 B per row)
-constexpr int NT_STAGES = 3;
 constexpr unsigned NT_OOB = 0x80000000u;
 
-template <int AM>
-struct ARow {                         // per-lane precomputed row geometry of one A instruction
-    int64_t base;                     // ROWK: element offset of the row; IM2COL: of pixel (b,h,w) channel 0
-    int h, w;                         // IM2COL only
-    bool ok;
-};
+constexpr unsigned NT_BADROW = 0xFFFFFFFFu;        // row outside the matrix
 
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int BM, int BN, int WAVES_M, int AM>
-__global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
-    constexpr int WAVES_N = 4 / WAVES_M;
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at bits 15:14; expcnt, lgkmcnt left at max)
+    __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
+    // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
+    // (its second pass over the accumulators would spill); launch_nt routes
+    // calls with stats to a 4-wave tile.
+    constexpr bool ST = NW == 4;
+    constexpr int WAVES_N = NW / WAVES_M;
     constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
     constexpr int TM = WM / 16, TN = WN / 16;
-    constexpr int ROWB = NT_BK * 2;                       // 128 B per row
+    constexpr int ROWB = BK * 2;                          // bytes per LDS row
+    constexpr int RPI = 1024 / ROWB;                      // rows per wave instruction
+    constexpr int CPR = ROWB / 16;                        // 16-B chunks per row
     constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-    constexpr int NA = BM / 32, NB = BN / 32;             // DMA instructions per thread per stage
-    static_assert(BM % 32 == 0 && BN % 32 == 0 && TM >= 1 && TN >= 1, "tile");
+    // DMA instructions per thread per stage. Every wave issues the same count
+    // (the vmcnt arithmetic relies on it): when BN < 4 * RPI the spare waves
+    // repeat another wave's B instruction (same bytes to the same LDS rows).
+    constexpr int NA = BM / (NW * RPI), NB = BN >= NW * RPI ? BN / (NW * RPI) : 1;
+    constexpr int BBLK = BN / RPI;                        // B row blocks per stage
+    constexpr int NPS = NA + NB;
+    static_assert((BK == 32 || BK == 64) && S >= 2, "BK 32 or 64, >= 2 stages");
+    static_assert(BM % (NW * RPI) == 0 && BN % RPI == 0 && (BN < NW * RPI || BN % (NW * RPI) == 0), "tile");
+    static_assert(TM >= 1 && TN >= 1, "wave tile");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -59,7 +71,7 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
     const bf16* B = reinterpret_cast<const bf16*>(p.B) + zb * p.strideB;
     const int kbeg = zs * p.k_chunk;
     const int kend = min(p.K, kbeg + p.k_chunk);
-    const int nk = max(0, (kend - kbeg + NT_BK - 1) / NT_BK);
+    const int nk = max(0, (kend - kbeg + BK - 1) / BK);
 
     // buffer resources (num_records = bytes; anything beyond reads as 0)
     int64_t a_elems, b_elems = (int64_t)p.N * p.ldb;
@@ -68,70 +80,67 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min<int64_t>(a_elems * 2, 0x7fffffff), 0x00020000);
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min<int64_t>(b_elems * 2, 0x7fffffff), 0x00020000);
 
-    // this lane's chunk within its row (global side of the swizzle)
-    const int lrow = lane >> 3;                           // row within the 8-row instruction
-    const int chunk = (lane & 7) ^ lrow;                  // row & 7 == lrow (instruction rows start at multiples of 8)
+    // this lane's row within its instruction and the chunk it fetches (global side of the swizzle);
+    // instruction rows start at multiples of RPI, so row & (RPI-1) == lrow
+    const int lrow = lane / CPR;
+    const int chunk = BK == 64 ? ((lane & 7) ^ lrow) : ((lane & 3) ^ ((lrow >> 2) & 3));
 
-    ARow<AM> arow[NA];
+    // per-lane row geometry of each DMA instruction, as 32-bit byte offsets
+    // (every operand here is < 2 GB) with NT_BADROW for rows past M / N
+    unsigned aoff[NA], ahw[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-        const int r = (i * 4 + wave) * 8 + lrow;
-        const int m = m0 + r;
-        arow[i].ok = m < p.M;
-        const int mm = arow[i].ok ? m : 0;
+        const int m = m0 + (i * NW + wave) * RPI + lrow;
+        ahw[i] = 0;
         if constexpr (AM == A_ROWK) {
-            arow[i].base = (int64_t)mm * p.lda;
-            arow[i].h = arow[i].w = 0;
+            aoff[i] = m < p.M ? (unsigned)((int64_t)m * p.lda * 2) : NT_BADROW;
         } else {
             const int W = p.convW, H = p.convH;
-            const int w = mm % W, t2 = mm / W, h = t2 % H;
-            arow[i].h = h;
-            arow[i].w = w;
-            arow[i].base = (int64_t)mm * p.convC;
+            const int mm = m < p.M ? m : 0;
+            const int w = mm % W, h = (mm / W) % H;
+            ahw[i] = ((unsigned)h << 16) | (unsigned)w;
+            aoff[i] = m < p.M ? (unsigned)((int64_t)mm * p.convC * 2) : NT_BADROW;
         }
     }
-    int64_t brow[NB];
-    bool bok[NB];
+    unsigned boff[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        const int n = n0 + (i * 4 + wave) * 8 + lrow;
-        bok[i] = n < p.N;
-        brow[i] = (int64_t)(bok[i] ? n : 0) * p.ldb;
+        const int n = n0 + ((i * NW + wave) % BBLK) * RPI + lrow;
+        boff[i] = n < p.N ? (unsigned)((int64_t)n * p.ldb * 2) : NT_BADROW;
     }
 
     auto issue = [&](int kt, int stage) {
-        const int k = kbeg + kt * NT_BK + 8 * chunk;
+        const int k = kbeg + kt * BK + 8 * chunk;
         const bool kok = k < kend;
         char* sa = smem + stage * STAGE;
         char* sb = sa + A_BYTES;
-        int tap_off = 0, dh = 0, dw = 0, cch = 0;
+        int tap_off = 0, dh = 0, dw = 0;
         if constexpr (AM != A_ROWK) {
             const int C = p.convC;
             const int tap = kok ? k / C : 0;
-            cch = k - tap * C;
+            const int cch = k - tap * C;
             const int kh = tap / 3, kw = tap - kh * 3;
             if constexpr (AM == A_IM2COL_FLIP) { dh = 1 - kh; dw = 1 - kw; }
             else { dh = kh - 1; dw = kw - 1; }
-            tap_off = (dh * p.convW + dw) * C + cch;
+            tap_off = ((dh * p.convW + dw) * C + cch) * 2;
         }
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
-            bool ok = kok && arow[i].ok;
-            int64_t e;
+            bool ok = kok && aoff[i] != NT_BADROW;
+            unsigned voff;
             if constexpr (AM == A_ROWK) {
-                e = arow[i].base + k;
+                voff = aoff[i] + (unsigned)(k * 2);
             } else {
-                const int hh = arow[i].h + dh, ww = arow[i].w + dw;
+                const int hh = (int)(ahw[i] >> 16) + dh, ww = (int)(ahw[i] & 0xffff) + dw;
                 ok = ok && hh >= 0 && hh < p.convH && ww >= 0 && ww < p.convW;
-                e = arow[i].base + tap_off;
+                voff = aoff[i] + (unsigned)tap_off;
             }
-            const unsigned voff = ok ? (unsigned)(e * 2) : NT_OOB;
-            lds_dma16(ra, sa + ((i * 4 + wave) * 8) * ROWB, voff);
+            lds_dma16(ra, sa + ((i * NW + wave) * RPI) * ROWB, ok ? voff : NT_OOB);
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-            const unsigned voff = (kok && bok[i]) ? (unsigned)((brow[i] + k) * 2) : NT_OOB;
-            lds_dma16(rb, sb + ((i * 4 + wave) * 8) * ROWB, voff);
+            const bool ok = kok && boff[i] != NT_BADROW;
+            lds_dma16(rb, sb + (((i * NW + wave) % BBLK) * RPI) * ROWB, ok ? boff[i] + (unsigned)(k * 2) : NT_OOB);
         }
     };
 
@@ -141,47 +150,44 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    if (nk > 0) issue(0, 0);
-    if (nk > 1) issue(1, 1);
-    const int i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+#pragma unroll
+    for (int st = 0; st < S - 1; ++st)
+        if (st < nk) issue(st, st);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int swz = BK == 64 ? (lane & 7) : ((i16 >> 2) & 3);
     for (int kt = 0; kt < nk; ++kt) {
-        // stage kt landed (stage kt+1 may still be in flight), then everyone is past stage kt-1
-        if (kt + 1 < nk) {
-            if constexpr (NA + NB == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            else if constexpr (NA + NB == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-            else if constexpr (NA + NB == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-            else if constexpr (NA + NB == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else if constexpr (NA + NB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if constexpr (NA + NB == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else if constexpr (NA + NB == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-            else if constexpr (NA + NB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else if constexpr (NA + NB == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else if constexpr (NA + NB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // stage kt landed: the stages issued after it (up to S-2 of them) may stay in flight
+        const int ahead = min(S - 2, nk - 1 - kt);
+        if constexpr (S >= 4) {
+            if (ahead >= 2) wait_vm<2 * NPS>();
+            else if (ahead == 1) wait_vm<NPS>();
+            else wait_vm<0>();
+        } else if constexpr (S == 3) {
+            if (ahead >= 1) wait_vm<NPS>();
+            else wait_vm<0>();
         } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wait_vm<0>();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();                     // everyone's stage kt is in, stage kt-1 is free
         asm volatile("" ::: "memory");
-        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NT_STAGES);
-        const char* sa = smem + (kt % NT_STAGES) * STAGE;
+        if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+        const char* sa = smem + (kt % S) * STAGE;
         const char* sb = sa + A_BYTES;
 #pragma unroll
-        for (int kk = 0; kk < NT_BK / 32; ++kk) {
-            const int slot = ((kk * 4 + g) ^ sw) * 16;
-            bf16x8 af[TM], bfr[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * WM + i * 16 + i16) * ROWB + slot);
+        for (int kk = 0; kk < BK / 32; ++kk) {
+            const int slot = ((kk * 4 + g) ^ swz) * 16;
+            bf16x8 bfr[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * WN + j * 16 + i16) * ROWB + slot);
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(sa + (wm * WM + i * 16 + i16) * ROWB + slot);
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+            }
         }
     }
     __syncthreads();                                      // LDS is reused by the stats epilogue
@@ -230,6 +236,7 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
                 acc[i][j][r] = v;
             }
     }
+    if constexpr (!ST) return;
     if (!p.stats) return;
 
     // per-column (sum, M2) over the tile's valid rows (see gemm.hip)
@@ -295,26 +302,59 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmParams p) {
     }
 }
 
-template <int BM, int BN, int WAVES_M, int AM>
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4>
 int launch_nt(const GemmParams& p, hipStream_t stream) {
-    constexpr int LDS = NT_STAGES * (BM + BN) * NT_BK * 2;
+    if constexpr (NW == 8) {
+        if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
+    }
+    constexpr int LDS = S * (BM + BN) * BK * 2;
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, WAVES_M, AM>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
         configured = true;
     }
     dim3 grid((unsigned)cdiv(p.M, BM), (unsigned)cdiv(p.N, BN), (unsigned)(p.batch * p.splits));
-    gemm_nt_kernel<BM, BN, WAVES_M, AM><<<grid, 256, LDS, stream>>>(p);
+    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");
+}
+
+// Tile configurations (OCRK_GEMM_NT_CFG picks one for experiments; by default
+// the shape decides). BM x BN x BK / stages -> LDS -> workgroups per CU:
+//   0: 256 x 128 x 64 / 3 -> 144 KB -> 1     1: 128 x 128 x 64 / 2 -> 64 KB -> 2
+//   2: 128 x 128 x 32 / 3 ->  48 KB -> 3     3: 128 x 128 x 64 / 3 -> 96 KB -> 1
+//   4: 256 x 128 x 32 / 4 ->  96 KB -> 1     5: 128 x 128 x 32 / 4 -> 64 KB -> 2
+//   6: 256 x 256 x 64 / 2, 8 waves -> 128 KB -> 1 (2 waves per SIMD)
+//   7: 256 x 128 x 64 / 2, 8 waves ->  96 KB -> 1   8: 256 x 256 x 32 / 3, 8 waves -> 96 KB
+int nt_cfg() {
+    static int c = -2;
+    if (c == -2) {
+        const char* e = getenv("OCRK_GEMM_NT_CFG");
+        c = e ? atoi(e) : -1;
+    }
+    return c;
 }
 
 template <int AM>
 int dispatch_nt(const GemmParams& p, hipStream_t s) {
-    // BM is the pixel / row dimension (large on every caller); BN follows N.
-    if (p.N <= 32) return launch_nt<256, 32, 4, AM>(p, s);
-    if (p.N <= 64) return launch_nt<256, 64, 4, AM>(p, s);
-    return launch_nt<256, 128, 2, AM>(p, s);
+    switch (nt_cfg()) {                                  // experiments (tools/gemm_sweep.sh)
+        case 0: return launch_nt<256, 128, 64, 3, 2, AM>(p, s);
+        case 1: return launch_nt<128, 128, 64, 2, 2, AM>(p, s);
+        case 2: return launch_nt<128, 128, 32, 3, 2, AM>(p, s);
+        case 3: return launch_nt<128, 128, 64, 3, 2, AM>(p, s);
+        case 4: return launch_nt<256, 128, 32, 4, 2, AM>(p, s);
+        case 5: return launch_nt<128, 128, 32, 4, 2, AM>(p, s);
+        case 6: return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
+        case 7: return launch_nt<256, 128, 64, 2, 4, AM, 8>(p, s);
+        case 8: return launch_nt<256, 256, 32, 3, 2, AM, 8>(p, s);
+        default: break;
+    }
+    // measured on MI355X (tools/bench_gemm.py): narrow N -> BK=32, 3 stages;
+    // wide N with enough row tiles -> 256 x 256 (8 waves); else 128 x 128 x 64, 2 stages
+    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM>(p, s);
+    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM>(p, s);
+    if (p.N >= 512 && p.M >= 16384) return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
+    return launch_nt<128, 128, 64, 2, 2, AM>(p, s);
 }
 
 }  // namespace
@@ -322,8 +362,8 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
 bool gemm_nt_enabled() {
     static int on = -1;
     if (on < 0) {
-        const char* e = getenv("OCRK_GEMM_NT");      // opt-in: not yet faster than gemm.hip
-        on = (e && e[0] == '1') ? 1 : 0;
+        const char* e = getenv("OCRK_GEMM_NT");      // OCRK_GEMM_NT=0: generic engine only
+        on = (e && e[0] == '0') ? 0 : 1;
     }
     return on == 1;
 }
@@ -331,7 +371,9 @@ bool gemm_nt_enabled() {
 // Runs the NT engine when it covers (mode, dtype); returns -1 when it does not.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {
     if (!gemm_nt_enabled() || dtype != OCRK_BF16 || bmode != B_NK) return -1;
-    if (p.K % 8 != 0) return -1;
+    // wide N with short K (a few k-steps: store-bound) runs better on the
+    // generic engine's three resident workgroups per CU (measured)
+    if (p.K % 8 != 0 || (p.k_chunk < 512 && p.N > 64)) return -1;
     if (amode == A_ROWK) {
         if (p.lda % 8 != 0 || p.ldb % 8 != 0) return -1;          // 16-B aligned rows
         return dispatch_nt<A_ROWK>(p, stream);

@@ -21,6 +21,7 @@ Structure of the launches (NHWC activations, compute dtype = store.cfg.dtype):
   then the CTC lattice.
 """
 import contextlib
+import os
 
 import numpy as np
 import torch
@@ -111,6 +112,7 @@ class _ConvBlock(torch.autograd.Function):
         dx = None
         if k == 1:
             K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
+            store.join()                                   # side-stream weight gradients are in
         else:
             Bo, Ho, Wo, Co = dy_odd.shape
             K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
@@ -161,6 +163,48 @@ def convnet_layers(inputs, widths, mode, store=None):
 
 
 # ---------------------------------------------------------------- recurrent
+_SIDE_STREAMS = {}
+
+
+class side_work:
+    """Run weight-gradient work on a side stream so it overlaps the next
+    (latency-bound) recurrent BPTT on the main stream: the side stream first
+    waits for everything issued so far on the main stream; the tensors it
+    reads are marked for the caching allocator; its completion event joins the
+    store's pending list (ParamStore.join, called before the gradients are
+    read: the end of backward, zero_grad, the optimizer step)."""
+
+    def __init__(self, store, *tensors):
+        self.store, self.tensors = store, tensors
+
+    def __enter__(self):
+        dev = self.store.device
+        if os.environ.get("OCRK_SIDE_STREAM", "1") == "0":        # measurement toggle
+            self.side = None
+            return self
+        side = _SIDE_STREAMS.get(dev)
+        if side is None:
+            side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+        self.side = side
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
+        side.wait_event(ready)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is None:
+            return False
+        done = torch.cuda.Event()
+        done.record(self.side)
+        self.ctx.__exit__(*exc)
+        for t in self.tensors:
+            t.record_stream(self.side)
+        self.store.pending.append(done)
+        return False
+
+
 class _BiLSTM(torch.autograd.Function):
     """rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199)."""
 
@@ -190,15 +234,16 @@ class _BiLSTM(torch.autograd.Function):
         dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H)               # [T,B,2,4H]
         pre = f"rnn/bdrnn{layer}"
         R = T * B
-        for d, dn in enumerate(("fw", "bw")):
-            gk = store.grads[f"{pre}/{dn}/lstm_cell/kernel"]                   # [In+H, 4H] f32
-            dgd = dG.view(R, 2 * G4)[:, d * G4:]                                 # view, ldb = 8H
-            # dW_x = x^T . dG_d ; dW_h = h_prev^T . dG_d  (split-K over T*B)
-            K.gemm(x, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
-                   ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R))
-            K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
-                   M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R))
-        K.colsum(dG, R, 2 * G4, store.flat_bias_pair_grad(layer))
+        with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
+            for d, dn in enumerate(("fw", "bw")):
+                gk = store.grads[f"{pre}/{dn}/lstm_cell/kernel"]               # [In+H, 4H] f32
+                dgd = dG.view(R, 2 * G4)[:, d * G4:]                             # view, ldb = 8H
+                # dW_x = x^T . dG_d ; dW_h = h_prev^T . dG_d  (split-K over T*B)
+                K.gemm(x, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
+                       ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R))
+                K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
+                       M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R))
+            K.colsum(dG, R, 2 * G4, store.flat_bias_pair_grad(layer))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
@@ -234,6 +279,8 @@ class _BiGRU(torch.autograd.Function):
         dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H)            # [T,B,2,3H]
         pre = f"rnn/bdrnn{layer}"
         R = T * B
+        side = side_work(store, x, hprev, rh, dG)
+        side.__enter__()
         for d, dn in enumerate(("fw", "bw")):
             gk = store.grads[f"{pre}/{dn}/gru_cell/gates/kernel"]               # [In+H, 2H]
             ck = store.grads[f"{pre}/{dn}/gru_cell/candidate/kernel"]           # [In+H, H]
@@ -250,6 +297,7 @@ class _BiGRU(torch.autograd.Function):
             K.gemm(rhd, dgc, trans_a=True, out=ck[n_in:], accumulate=True, M=H, N=H, K=R, lda=2 * H,
                    ldb=2 * G3, ldc=H, splits=_splits(H, H, R))
         K.colsum(dG, R, 2 * G3, store.gru_bias_cat_grad(layer))
+        side.__exit__(None, None, None)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dG.view(R, 2 * G3), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
@@ -284,9 +332,10 @@ class _Logits(torch.autograd.Function):
         C = logits.shape[-1]
         R = T * B
         dpre = K.relu_mask(dlogits.contiguous(), logits, dt)                       # [T,B,C]
-        K.gemm(x, dpre, trans_a=True, out=store.grads["rnn/logits/kernel"], accumulate=True,
-               M=D, N=C, K=R, lda=D, ldb=C, ldc=C, splits=_splits(D, C, R))
-        K.colsum(dpre, R, C, store.grads["rnn/logits/bias"])
+        with side_work(store, x, dpre):
+            K.gemm(x, dpre, trans_a=True, out=store.grads["rnn/logits/kernel"], accumulate=True,
+                   M=D, N=C, K=R, lda=D, ldb=C, ldc=C, splits=_splits(D, C, R))
+            K.colsum(dpre, R, C, store.grads["rnn/logits/bias"])
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dpre.view(R, C), store.logits_image(dt), trans_b=True, out_dtype=dt).view(T, B, D)

@@ -136,6 +136,7 @@ class ParamStore:
                 self.stats[name] = self.flat_stats[off:off + n].view(shape)
         self.version = 0
         self._images = {}
+        self.pending = []          # events of side-stream gradient work not yet joined
         self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
 
     # ------------------------------------------------------------ state
@@ -164,7 +165,17 @@ class ParamStore:
             self.load_state_dict({k.replace("__", "/"): z[k] for k in z.files})
 
     def zero_grad(self):
+        self.join()
         self.flat_grad.zero_()
+
+    def join(self):
+        """Make the current stream wait for side-stream gradient work
+        (model.side_work) so flat_grad is complete in stream order."""
+        if self.pending:
+            cur = torch.cuda.current_stream(self.device)
+            for ev in self.pending:
+                cur.wait_event(ev)
+            self.pending.clear()
 
     def bump(self):
         """The master values changed: derived weight images are stale."""

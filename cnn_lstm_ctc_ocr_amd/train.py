@@ -75,6 +75,7 @@ class Trainer:
     def reduce_gradients(self):
         """Sum the flat gradient buffer over the data-parallel ranks (one RCCL
         all-reduce); returns the factor that turns the sum into the mean."""
+        self.store.join()
         return allreduce_mean_scale(self.store.flat_grad, self.group)
 
     def apply_gradients(self):

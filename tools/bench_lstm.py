@@ -41,7 +41,7 @@ if "--stamps" in sys.argv:
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
     torch.cuda.synchronize()
     _lib.call("ocrk_lstm_debug_stamps", _lib.ptr(dbg))
-    K.lstm_fwd(gx, whT, seq, 1, B, H, torch.bfloat16)
+    K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)     # every launch overwrites: the last step remains
     torch.cuda.synchronize()
     _lib.call("ocrk_lstm_debug_stamps", None)
     st = dbg.view(-1, 8)[:, :6].cpu().numpy().astype(np.float64) * 10.0   # ns
