@@ -59,7 +59,7 @@ SIGNATURES = {
                               _p, _i32, _i32, _p],
     "ocrk_bn_bwd_workspace_size": [_i32, _i32, _i32, _i32],
     "ocrk_bn_relu_pool_bwd": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
-                              _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+                              _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],

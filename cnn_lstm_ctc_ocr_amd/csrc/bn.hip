@@ -190,16 +190,20 @@ __device__ __forceinline__ void routed_grad(const T* __restrict__ z, const T* __
         if (!(a_me[i] > 0.f)) da[i] = 0.f;
 }
 
-// pass 1: per-block partial sums of da and da*xhat per channel
+// pass 1: route the pooled gradient (first max of each window, ReLU mask) to
+// the pre-pool pixels ONCE, store it (da is dp's value or 0: exact in the
+// compute dtype) for pass 2, and reduce per-block partial sums of da and
+// da*xhat per channel.
 template <typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
                      const float* __restrict__ mean, const float* __restrict__ invstd,
                      const float* __restrict__ gamma, const float* __restrict__ beta, int kh, int kw,
-                     int sh, int sw, int dp_time_major, int64_t items_per_block, float* __restrict__ slab) {
+                     int sh, int sw, int dp_time_major, int items_per_block, float* __restrict__ slab,
+                     T* __restrict__ da_out) {
     __shared__ float red[256][17];
     const int G = C / 8;
-    const int64_t items = (int64_t)B * H * W * G;
+    const int items = B * H * W * G;                    // < 2^31 (checked by the caller)
     const int g = threadIdx.x % G;       // fixed: items_per_block % 256 == 0 and 256 % G == 0
     const int c0 = g * 8;
     float sc[8], sf[8], mu[8], is[8];
@@ -213,20 +217,22 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
     float s1[8], s2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
-    const int64_t i0 = (int64_t)blockIdx.x * items_per_block;
-    const int64_t i1 = min(items, i0 + items_per_block);
-    for (int64_t it = i0 + threadIdx.x; it < i1; it += 256) {
-        int64_t px = it / G;
-        int w = (int)(px % W);
-        int64_t t = px / W;
-        int h = (int)(t % H), b = (int)(t / H);
+    const int i0 = blockIdx.x * items_per_block;
+    const int i1 = min(items, i0 + items_per_block);
+    for (int it = i0 + threadIdx.x; it < i1; it += 256) {
+        const int px = it / G;
+        const int w = px % W, t = px / W;
+        const int h = t % H, b = t / H;
         float da[8], zc[8];
         routed_grad(z, dp, B, H, W, C, b, h, w, c0, kh, kw, sh, sw, dp_time_major, sc, sf, da, zc);
+        F8 o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             s1[i] += da[i];
             s2[i] += da[i] * ((zc[i] - mu[i]) * is[i]);
+            o.v[i] = da[i];
         }
+        store8(da_out + (int64_t)px * C + c0, o);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
@@ -239,61 +245,97 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
     }
 }
 
-// dsum[o] = sum_i slab[i][o] (o < 2C; fixed order), then dbeta = dsum[:C], dgamma = dsum[C:]
+// Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
+// accumulation, in two stages so the ~2k slab rows are spread over many
+// workgroups: stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
+constexpr int SLAB_P = 64;
+
 __global__ void __launch_bounds__(256)
-bn_bwd_sum_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ dsum,
-                  float* __restrict__ dbeta, float* __restrict__ dgamma, int accumulate) {
-    __shared__ double part[4][64];
+slab_sum_stage1(const float* __restrict__ slab, int nslab, int NC, double* __restrict__ part) {
+    __shared__ double red[4][64];
     const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int o = blockIdx.x * 64 + cl;
+    const int c = blockIdx.x * 64 + cl;
+    const int rows = (nslab + SLAB_P - 1) / SLAB_P;
+    const int r0 = blockIdx.y * rows, r1 = min(nslab, r0 + rows);
     double s = 0.0;
-    if (o < 2 * C) {
-#pragma unroll 8
-        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * 2 * C + o];
-    }
-    part[q][cl] = s;
+    if (c < NC)
+        for (int i = r0 + q; i < r1; i += 4) s += slab[(int64_t)i * NC + c];
+    red[q][cl] = s;
     __syncthreads();
-    if (q == 0 && o < 2 * C) {
-        double t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
-        dsum[o] = (float)t;
-        float* dst = o < C ? dbeta + o : dgamma + (o - C);
-        *dst = accumulate ? *dst + (float)t : (float)t;
-    }
+    if (q == 0 && c < NC) part[(int64_t)blockIdx.y * NC + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
-// pass 2: dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n)
+// res[o] = sum; then (accumulate ? += : =) into dst_lo[o] for o < split, dst_hi[o - split] above
+__global__ void __launch_bounds__(64)
+slab_sum_stage2(const double* __restrict__ part, int NC, float* __restrict__ res, float* __restrict__ dst_lo,
+                float* __restrict__ dst_hi, int split, int accumulate) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= NC) return;
+    double t = 0.0;
+    for (int y = 0; y < SLAB_P; ++y) t += part[(int64_t)y * NC + c];
+    const float v = (float)t;
+    if (res) res[c] = v;
+    float* d = c < split ? (dst_lo ? dst_lo + c : nullptr) : (dst_hi ? dst_hi + (c - split) : nullptr);
+    if (d) *d = accumulate ? *d + v : v;
+}
+
+static int slab_sum(const float* slab, int nslab, int NC, double* part, float* res, float* dst_lo,
+                    float* dst_hi, int split, int accumulate, hipStream_t s) {
+    slab_sum_stage1<<<dim3((NC + 63) / 64, SLAB_P), 256, 0, s>>>(slab, nslab, NC, part);
+    int st = ocrk::launch_status("bn slab sum 1");
+    if (st) return st;
+    slab_sum_stage2<<<(NC + 63) / 64, 64, 0, s>>>(part, NC, res, dst_lo, dst_hi, split, accumulate);
+    return ocrk::launch_status("bn slab sum 2");
+}
+
+// pass 2 (streaming): dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n),
+// plus per-block partial column sums of dz -- the gradient of the conv bias
+// in front of the BN (fused here instead of a separate pass over dz).
 template <typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
+bn_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ da_in, int npix, int C,
                     const float* __restrict__ mean, const float* __restrict__ invstd,
-                    const float* __restrict__ gamma, const float* __restrict__ beta, int kh, int kw,
-                    int sh, int sw, int dp_time_major, const float* __restrict__ dsum, T* __restrict__ dz) {
+                    const float* __restrict__ gamma, const float* __restrict__ dsum, int items_per_block,
+                    T* __restrict__ dz, float* __restrict__ bslab) {
+    __shared__ float red[256][9];
     const int G = C / 8;
-    const int64_t items = (int64_t)B * H * W * G;
-    const float inv_n = 1.f / (float)((int64_t)B * H * W);
-    for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < items; it += (int64_t)gridDim.x * 256) {
-        int g = (int)(it % G);
-        int c0 = g * 8;
-        int64_t px = it / G;
-        int w = (int)(px % W);
-        int64_t t = px / W;
-        int h = (int)(t % H), b = (int)(t / H);
-        float sc[8], sf[8];
+    const int items = npix * G;
+    const int g = threadIdx.x % G, c0 = g * 8;
+    const float inv_n = 1.f / (float)npix;
+    float sc[8], mu[8], is[8], a[8], bb[8], cs[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            sc[i] = gamma[c0 + i] * invstd[c0 + i];
-            sf[i] = beta[c0 + i] - mean[c0 + i] * sc[i];
-        }
-        float da[8], zc[8];
-        routed_grad(z, dp, B, H, W, C, b, h, w, c0, kh, kw, sh, sw, dp_time_major, sc, sf, da, zc);
+    for (int i = 0; i < 8; ++i) {
+        const int c = c0 + i;
+        is[i] = invstd[c];
+        mu[i] = mean[c];
+        sc[i] = gamma[c] * is[i];
+        a[i] = dsum[c] * inv_n;
+        bb[i] = dsum[C + c] * inv_n;
+        cs[i] = 0.f;
+    }
+    const int i0 = blockIdx.x * items_per_block;
+    const int i1 = min(items, i0 + items_per_block);
+    for (int it = i0 + threadIdx.x; it < i1; it += 256) {
+        const int64_t off = (int64_t)(it / G) * C + c0;
+        const F8 zz = load8(z + off), dd = load8(da_in + off);
         F8 out;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            int c = c0 + i;
-            float xhat = (zc[i] - mean[c]) * invstd[c];
-            out.v[i] = sc[i] * (da[i] - dsum[c] * inv_n - xhat * dsum[C + c] * inv_n);
+            const float xhat = (zz.v[i] - mu[i]) * is[i];
+            out.v[i] = sc[i] * (dd.v[i] - a[i] - xhat * bb[i]);
+            cs[i] += out.v[i];
         }
-        store8(dz + px * C + c0, out);
+        store8(dz + off, out);
+    }
+    if (!bslab) return;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[threadIdx.x][i] = cs[i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const int gg = c / 8, ci = c % 8;
+        float s = 0.f;
+        for (int q = gg; q < 256; q += G) s += red[q][ci];
+        bslab[(int64_t)blockIdx.x * C + c] = s;
     }
 }
 
@@ -335,40 +377,54 @@ extern "C" int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, 
 static int64_t bn_bwd_blocks(int64_t items) { return std::max<int64_t>(1, std::min<int64_t>(2048, ocrk::cdiv(items, 256 * 8))); }
 static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::cdiv(items, nb), 256) * 256; }
 
+// part [SLAB_P][2C] doubles | slab [nb][2C] | dsum [2C] | bias slab [nb][C] | routed da [B*H*W*C]
+// (4 B per element: any dtype)
+static size_t bn_ws_floats(int64_t nb, int C) {
+    size_t f = (size_t)SLAB_P * 2 * C * 2 + (size_t)(nb * 2 * C + 2 * C + nb * C);
+    return (f + 3) / 4 * 4;                                           // 16-B align the da image
+}
+
 extern "C" size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C) {
     int64_t items = (int64_t)B * H * W * (C / 8);
     int64_t nb = bn_bwd_blocks(items);
     nb = ocrk::cdiv(items, bn_bwd_ipb(items, nb));
-    return (size_t)(nb * 2 * C + 2 * C) * sizeof(float);
+    return bn_ws_floats(nb, C) * sizeof(float) + (size_t)B * H * W * C * sizeof(float);
 }
 
 extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C,
                                      const float* mean, const float* invstd, const float* gamma,
                                      const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
-                                     void* dz, float* dgamma, float* dbeta, int accumulate, void* ws,
-                                     size_t ws_bytes, int dtype, void* stream) {
+                                     void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                                     void* ws, size_t ws_bytes, int dtype, void* stream) {
     OCRK_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "ocrk_bn_relu_pool_bwd: C=%d unsupported", C);
     OCRK_REQUIRE(ws_bytes >= ocrk_bn_bwd_workspace_size(B, H, W, C), "ocrk_bn_relu_pool_bwd: workspace too small");
-    int64_t items = (int64_t)B * H * W * (C / 8);
+    const int64_t items = (int64_t)B * H * W * (C / 8);
+    OCRK_REQUIRE(items < (1ll << 31) && (int64_t)B * H * W < (1ll << 31), "ocrk_bn_relu_pool_bwd: tensor too large");
     if (items == 0) return OCRK_OK;
     int64_t nb = bn_bwd_blocks(items);
-    int64_t ipb = bn_bwd_ipb(items, nb);
+    const int64_t ipb = bn_bwd_ipb(items, nb);
     nb = ocrk::cdiv(items, ipb);
-    float* slab = (float*)ws;
+    double* part = (double*)ws;
+    float* slab = (float*)(part + (size_t)SLAB_P * 2 * C);
     float* dsum = slab + nb * 2 * C;
+    float* bslab = dsum + 2 * C;
+    void* da = (float*)ws + bn_ws_floats(nb, C);
+    const int npix = B * H * W;
     hipStream_t s = ocrk::as_stream(stream);
     if (dtype == OCRK_BF16)
-        bn_bwd_reduce_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, ipb, slab);
+        bn_bwd_reduce_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, (int)ipb, slab, (bf16*)da);
     else
-        bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, ipb, slab);
+        bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, (int)ipb, slab, (float*)da);
     int st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
     if (st) return st;
-    bn_bwd_sum_kernel<<<(2 * C + 63) / 64, 256, 0, s>>>(slab, (int)nb, C, dsum, dbeta, dgamma, accumulate);
-    st = ocrk::launch_status("ocrk_bn_relu_pool_bwd sum");
+    st = slab_sum(slab, (int)nb, 2 * C, part, dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
     if (st) return st;
+    float* bs = dbias ? bslab : nullptr;
     if (dtype == OCRK_BF16)
-        bn_bwd_apply_kernel<bf16><<<grid_for(items), 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dsum, (bf16*)dz);
+        bn_bwd_apply_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)da, npix, C, mean, invstd, gamma, dsum, (int)ipb, (bf16*)dz, bs);
     else
-        bn_bwd_apply_kernel<float><<<grid_for(items), 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dsum, (float*)dz);
-    return ocrk::launch_status("ocrk_bn_relu_pool_bwd apply");
+        bn_bwd_apply_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)da, npix, C, mean, invstd, gamma, dsum, (int)ipb, (float*)dz, bs);
+    st = ocrk::launch_status("ocrk_bn_relu_pool_bwd apply");
+    if (st || !dbias) return st;
+    return slab_sum(bslab, (int)nb, C, part, nullptr, dbias, nullptr, C, accumulate, s);
 }

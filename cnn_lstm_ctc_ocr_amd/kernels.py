@@ -150,15 +150,19 @@ def bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=False):
     return out
 
 
-def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True):
-    _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta)
+def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True,
+                     dbias=None):
+    """dz of BN + ReLU + max-pool; dgamma, dbeta and (optionally) dbias = column
+    sums of dz (the conv bias in front of the BN) accumulate in f32."""
+    _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta, dbias)
     B, H, W, C = z.shape
     kh, kw, sh, sw = pool
     nb = _lib.lib().ocrk_bn_bwd_workspace_size(B, H, W, C)
     ws = _ws(nb, z.device)
     dz = torch.empty_like(z)
     call("ocrk_bn_relu_pool_bwd", ptr(z), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
-         kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(ws), nb,
+         kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), ptr(dbias), int(accumulate),
+         ptr(ws), nb,
          dtype_code(z.dtype), _stream(z))
     return dz
 

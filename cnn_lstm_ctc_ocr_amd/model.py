@@ -103,10 +103,10 @@ class _ConvBlock(torch.autograd.Function):
             dp = K.cast(dp, dt)
         dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                 POOLS[even], dp_time_major=(k == 4),
-                                dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"])
+                                dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
+                                dbias=G[pe + "/bias"])                  # conv bias grad fused
         B, H, W, C = dz.shape
         K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
-        K.colsum(dz, B * H * W, C, G[pe + "/bias"])
         _, w_bwd = store.conv_images(even, dt)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd)     # ReLU of conv_{2k-1} fused
         dx = None

@@ -135,12 +135,13 @@ int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, const float
                           const float* invstd, const float* gamma, const float* beta, int kh, int kw,
                           int sh, int sw, void* out, int time_major, int dtype, void* stream);
 /* Backward of the above: dz [B,H,W,C] from dp (pooled gradient, time-major if
- * dp_time_major); dgamma/dbeta f32 (accumulate 0/1). */
+ * dp_time_major); dgamma/dbeta f32; dbias f32 or NULL = column sums of dz, the gradient
+ * of the conv bias in front of the BN (accumulate 0/1 for all three). */
 size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C);
 int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
                           const float* invstd, const float* gamma, const float* beta, int kh, int kw,
                           int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
-                          int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
+                          float* dbias, int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
 
 /* ------------------------------------------------------------- recurrent
  * a7' -- rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199), both

@@ -126,9 +126,12 @@ def test_bn_relu_pool(cuda, pool):
     dg = torch.zeros(C, device=cuda)
     db = torch.zeros(C, device=cuda)
     dp_d = _t(dp[:, 0].transpose(1, 0, 2) if tm else dp, cuda)
+    dbias = torch.full((C,), 7.0, device=cuda)
     dz = Kn.bn_relu_pool_bwd(_t(z, cuda), dp_d, mean_d, inv_d, _t(gamma, cuda), _t(beta, cuda), pool, tm, dg, db,
-                             accumulate=False)
+                             accumulate=False, dbias=dbias)
     np.testing.assert_allclose(dz.cpu().numpy(), dz_ref, rtol=1e-4, atol=1e-5)
+    # fused conv-bias gradient = column sums of dz (~0 up to rounding: BN removes the mean)
+    np.testing.assert_allclose(dbias.cpu().numpy(), dz_ref.sum(axis=(0, 1, 2)), rtol=0, atol=1e-4)
     np.testing.assert_allclose(dg.cpu().numpy(), dg_ref, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(db.cpu().numpy(), db_ref, rtol=1e-4, atol=1e-5)
 
