@@ -53,4 +53,9 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
 // uses the generic engine), else a status. OCRK_GEMM_NT=0 disables it.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
+// The same pipeline for the k-major modes A_COLK / A_IM2COL_T x B_KN (conv
+// weight gradients, recurrent / logits weight gradients), gemm_tn.hip.
+// Returns -1 when not covered. OCRK_GEMM_TN=0 disables it.
+int gemm_tn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+
 }  // namespace ocrk

@@ -385,6 +385,7 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     OCRK_REQUIRE(!(p.stats && (p.splits > 1 || p.batch > 1)), "gemm: stats need splits=1, batch=1");
     OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
     int nt = gemm_nt(p, amode, bmode, dtype, stream);
+    if (nt < 0) nt = gemm_tn(p, amode, bmode, dtype, stream);
     if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     if (dtype == OCRK_BF16) return dispatch_modes<bf16>(p, amode, bmode, stream);
     if (dtype == OCRK_F32) return dispatch_modes<float>(p, amode, bmode, stream);

@@ -53,11 +53,35 @@ def main():
         w_bwd = (torch.randn(Ci, 9 * Co, device=dev) * 0.05).to(bf)
         ms, out = timed(lambda: K.conv3x3_bwd_data(dy, w_bwd))
         rows.append((f"conv bwd-data {Co}->{Ci} {H}x{W}", ms, fl, float(out.float().abs().sum())))
+    for (H, W, Ci, Co) in CONV:
+        x = torch.randn(B, H, W, Ci, device=dev).to(bf)
+        dy = torch.randn(B, H, W, Co, device=dev).to(bf)
+        dw = torch.zeros(9 * Ci, Co, device=dev)
+        def wg():
+            dw.zero_()
+            K.conv3x3_bwd_weight(x, dy, dw)
+            return dw
+        ms, out = timed(wg)
+        rows.append((f"conv wgrad {Ci}->{Co} {H}x{W}", ms, 2.0 * B * H * W * 9 * Ci * Co,
+                     float(out.abs().sum())))
+    R = 32000
+    for (n_in, tag) in [(1024, "LSTM dW_x L2"), (512, "LSTM dW_h"), (256, "LSTM dW_x L1")]:
+        x = torch.randn(R, n_in, device=dev).to(bf)
+        dG = torch.randn(R, 4096, device=dev).to(bf)
+        gk = torch.zeros(n_in, 2048, device=dev)
+        def dwg():
+            gk.zero_()
+            K.gemm(x, dG, trans_a=True, out=gk, accumulate=True, M=n_in, N=2048, K=R, lda=n_in, ldb=4096,
+                   ldc=2048, splits=max(1, min(-(-512 // (-(-n_in // 128) * 16)), R // 2048)))
+            return gk
+        ms, out = timed(dwg)
+        rows.append((tag, ms, 2.0 * n_in * 2048 * R, float(out.abs().sum())))
     tot = 0.0
     for tag, ms, fl, chk in rows:
         tot += ms
         print(f"{tag:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s  checksum {chk:.6e}")
-    print(f"total {tot:.3f} ms  (OCRK_GEMM_NT={os.environ.get('OCRK_GEMM_NT', '1')})")
+    print(f"total {tot:.3f} ms  (OCRK_GEMM_NT={os.environ.get('OCRK_GEMM_NT', '1')}, "
+          f"OCRK_GEMM_TN={os.environ.get('OCRK_GEMM_TN', '1')})")
 
 
 if __name__ == "__main__":
