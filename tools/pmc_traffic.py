@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 
@@ -23,7 +24,7 @@ def per_dispatch(root, counter, match):
     for f in files:
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter or match not in row.get("Kernel_Name", ""):
+                if row.get("Counter_Name") != counter or not re.search(match, row.get("Kernel_Name", "")):
                     continue
                 vals[(f, row.get("Dispatch_Id"))] += float(row["Counter_Value"])
     return list(vals.values())
@@ -33,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--match", required=True, help="substring of the kernel name")
+    ap.add_argument("--match", required=True, help="regular expression on the kernel name")
     ap.add_argument("--desc", default="")
     ap.add_argument("--command", default="")
     ap.add_argument("--out", required=True)
