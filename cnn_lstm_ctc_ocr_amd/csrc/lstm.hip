@@ -34,6 +34,59 @@ __device__ __forceinline__ void stamp(long long* dbg, int i) {
 }
 
 // --------------------------------------------------------------- forward
+// The forward cell update for the (row, 4 units) pairs of this thread, from
+// the step's gate pre-activations in LDS (sG [BR][4*HU+1] f32) and the
+// operands preloaded at kernel entry.
+template <typename CT, int BR, int HU>
+__device__ __forceinline__ void lstm_fwd_epilogue(const float* __restrict__ sG, const int (&plen)[(BR * HU / 4 + 255) / 256],
+                                                  const float (&pg)[(BR * HU / 4 + 255) / 256][4][4],
+                                                  const float (&pc)[(BR * HU / 4 + 255) / 256][4],
+                                                  const float (&ph)[(BR * HU / 4 + 255) / 256][4], int s, int B, int H,
+                                                  int b0, int u0, int dir, float* __restrict__ c_state,
+                                                  CT* __restrict__ h_out, CT* __restrict__ out,
+                                                  CT* __restrict__ hprev_t, float* __restrict__ cprev_t,
+                                                  CT* __restrict__ acts_t) {
+    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+    constexpr bool EFULL = (BR * UQ) % 256 == 0;
+    const int G4 = 4 * H;
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) {
+        const int idx = threadIdx.x + 256 * q;
+        if (!EFULL && idx >= BR * UQ) continue;
+        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+        const int len = plen[q];
+        const int t = step_time(dir, s, len);
+        const int64_t st = ((int64_t)dir * B + b) * H + uu;          // state index
+        const int64_t tb = ((int64_t)t * B + b) * 2 + dir;           // time-order row
+        CT* a = acts_t + tb * G4 + uu;
+        if (s < len) {
+            const float* gl = sG + r * (4 * HU + 1) + u;
+            float ai[4], aj[4], af[4], ao[4], c[4], h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                ai[e] = sig_fast(gl[0 * HU + e] + pg[q][0][e]);
+                aj[e] = tanh_fast(gl[1 * HU + e] + pg[q][1][e]);
+                af[e] = sig_fast(gl[2 * HU + e] + pg[q][2][e] + 1.0f);   // forget_bias = 1
+                ao[e] = sig_fast(gl[3 * HU + e] + pg[q][3][e]);
+                c[e] = af[e] * pc[q][e] + ai[e] * aj[e];
+                h[e] = ao[e] * tanh_fast(c[e]);
+            }
+            st4(c_state + st, c);
+            st4(h_out + st, h);
+            st4(out + ((int64_t)t * B + b) * 2 * H + dir * H + uu, h);
+            st4(hprev_t + tb * H + uu, ph[q]);
+            st4(cprev_t + tb * H + uu, pc[q]);
+            st4(a + 0 * H, ai); st4(a + 1 * H, aj); st4(a + 2 * H, af); st4(a + 3 * H, ao);
+        } else {
+            const float z[4] = {0.f, 0.f, 0.f, 0.f};
+            st4(h_out + st, ph[q]);
+            st4(hprev_t + tb * H + uu, z);
+            st4(cprev_t + tb * H + uu, z);
+            st4(a + 0 * H, z); st4(a + 1 * H, z); st4(a + 2 * H, z); st4(a + 3 * H, z);
+        }
+    }
+}
+
 // Epilogue operands (gx, c, h, len) do not depend on the GEMM: they are loaded
 // into registers at kernel entry so their HBM latency hides under the GEMM.
 template <typename CT, int BR, int HU, int KC>
@@ -84,44 +137,110 @@ lstm_fwd_step_kernel(const CT* __restrict__ gx, const CT* __restrict__ whT, cons
     stamp(dbg, 3);
     Core::spill(acc, lds);
     stamp(dbg, 4);
-    const float* sG = reinterpret_cast<const float*>(lds);
+    lstm_fwd_epilogue<CT, BR, HU>(reinterpret_cast<const float*>(lds), plen, pg, pc, ph, s, B, H, b0, u0, dir, c_state,
+                                  h_out, out, hprev_t, cprev_t, acts_t);
+    stamp(dbg, 5);
+}
+
+// Forward step with the whole GEMM operand set in LDS (bf16, K = H <= 512):
+// 64 h rows and the 64 W_h^T rows of this tile's 16 units x 4 gates, 2H bytes
+// each, fetched in ONE burst of LDS-DMA (global_load_lds_dwordx4: no VGPR
+// round trip, every load in flight at once) while the epilogue operands load
+// into registers; then the 64 x 64 x H product on MFMA straight from LDS.
+// Rows are lane-linear with the 16-B chunk index XOR-swizzled by (row & 7) on
+// the global side, so fragment reads are conflict-free.
+template <int H_>
+__global__ void __launch_bounds__(256)
+lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, const bf16* __restrict__ h_in,
+                         bf16* __restrict__ h_out, float* __restrict__ c_state, const int* __restrict__ seq_len,
+                         int s, int T, int B, bf16* __restrict__ out, bf16* __restrict__ hprev_t,
+                         float* __restrict__ cprev_t, bf16* __restrict__ acts_t) {
+    constexpr int BR = 64, HU = 16, NC = 4 * HU, H = H_;
+    constexpr int ROWB = 2 * H, CPR = ROWB / 16, RPI = 64 / CPR;     // 16-B chunks per row, rows per wave instr
+    constexpr int NI = BR / (4 * RPI);                              // instructions per wave per operand
+    static_assert(CPR % 8 == 0 && 64 % CPR == 0, "H = 256 or 512");
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    char* sA = lds;
+    char* sB = lds + BR * ROWB;
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
+    const int G4 = 4 * H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+
+    int plen[EPQ4];
+#pragma unroll
+    for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min(tid + 256 * q, BR * UQ - 1) / UQ];
+
+    // 1. the operand burst
+    const bf16* a_rows = h_in + ((int64_t)dir * B + b0) * H;
+    const bf16* wdir = whT + (int64_t)dir * 4 * H * H;
+    const int lrow = lane / CPR, chunk = (lane % CPR) ^ 0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int r = (i * 4 + wave) * RPI + lrow;
+        const int c = (lane % CPR) ^ (r & 7);
+        __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * H + 8 * c),
+                                         (__attribute__((address_space(3))) void*)(sA + (i * 4 + wave) * RPI * ROWB),
+                                         16, 0, 0);
+        const bf16* brow = wdir + (int64_t)((r / HU) * H + u0 + (r % HU)) * H;
+        __builtin_amdgcn_global_load_lds((const void*)(brow + 8 * c),
+                                         (__attribute__((address_space(3))) void*)(sB + (i * 4 + wave) * RPI * ROWB),
+                                         16, 0, 0);
+    }
+    (void)chunk;
+    // 2. epilogue operands (do not depend on the product)
+    float pg[EPQ4][4][4], pc[EPQ4][4], ph[EPQ4][4];
 #pragma unroll
     for (int q = 0; q < EPQ4; ++q) {
-        const int idx = threadIdx.x + 256 * q;
-        if (!EFULL && idx >= BR * UQ) continue;
+        const int idx = tid + 256 * q;
         const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
-        const int len = plen[q];
-        const int t = step_time(dir, s, len);
-        const int64_t st = ((int64_t)dir * B + b) * H + uu;          // state index
-        const int64_t tb = ((int64_t)t * B + b) * 2 + dir;           // time-order row
-        CT* a = acts_t + tb * G4 + uu;
-        if (s < len) {
-            const float* gl = sG + r * (4 * HU + 1) + u;
-            float ai[4], aj[4], af[4], ao[4], c[4], h[4];
+        const int64_t st = ((int64_t)dir * B + b) * H + uu;
+        ld4(pc[q], c_state + st);
+        ld4(ph[q], h_in + st);
+        const int t = step_time(dir, s, plen[q]);
+        const bf16* g = gx + (((int64_t)t * B + b) * 2 + dir) * G4 + uu;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                ai[e] = sig_fast(gl[0 * HU + e] + pg[q][0][e]);
-                aj[e] = tanh_fast(gl[1 * HU + e] + pg[q][1][e]);
-                af[e] = sig_fast(gl[2 * HU + e] + pg[q][2][e] + 1.0f);   // forget_bias = 1
-                ao[e] = sig_fast(gl[3 * HU + e] + pg[q][3][e]);
-                c[e] = af[e] * pc[q][e] + ai[e] * aj[e];
-                h[e] = ao[e] * tanh_fast(c[e]);
-            }
-            st4(c_state + st, c);
-            st4(h_out + st, h);
-            st4(out + ((int64_t)t * B + b) * 2 * H + dir * H + uu, h);
-            st4(hprev_t + tb * H + uu, ph[q]);
-            st4(cprev_t + tb * H + uu, pc[q]);
-            st4(a + 0 * H, ai); st4(a + 1 * H, aj); st4(a + 2 * H, af); st4(a + 3 * H, ao);
-        } else {
-            const float z[4] = {0.f, 0.f, 0.f, 0.f};
-            st4(h_out + st, ph[q]);
-            st4(hprev_t + tb * H + uu, z);
-            st4(cprev_t + tb * H + uu, z);
-            st4(a + 0 * H, z); st4(a + 1 * H, z); st4(a + 2 * H, z); st4(a + 3 * H, z);
-        }
+        for (int k = 0; k < 4; ++k) ld4(pg[q][k], g + k * H);
     }
-    stamp(dbg, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // 3. 64 x 64 x H on MFMA, 2 x 2 waves of 32 x 32
+    const int wm = wave >> 1, wn = wave & 1, i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int ks = 0; ks < H / 32; ++ks) {
+        const int slot = ((ks * 4 + g) ^ sw) * 16;
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * 32 + i * 16 + i16) * ROWB + slot);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * 32 + j * 16 + i16) * ROWB + slot);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    float* sG = reinterpret_cast<float*>(lds);                      // [BR][NC+1]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sG[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * (NC + 1) + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    lstm_fwd_epilogue<bf16, BR, HU>(sG, plen, pg, pc, ph, s, B, H, b0, u0, dir, c_state, h_out, out, hprev_t,
+                                    cprev_t, acts_t);
 }
 
 // -------------------------------------------------------------- backward
@@ -211,6 +330,21 @@ long long* g_lstm_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
 
 extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return OCRK_OK; }
 
+static bool lstm_dma_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("OCRK_LSTM_DMA");
+        on = (e && e[0] == '0') ? 0 : 1;
+        if (on) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<512>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 512);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<256>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 256);
+        }
+    }
+    return on == 1;
+}
+
 // Tile shapes: bf16 BR=64 x HU=16 (fwd K-chunk 128, bwd 256); f32 BR=32 x HU=8/16.
 #define FWD_BF16 bf16, 64, 16, 256
 #define FWD_F32 float, 32, 8, 64
@@ -224,6 +358,13 @@ extern "C" int ocrk_lstm_fwd_step(const void* gx, const void* whT, const void* h
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 256 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 256 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 16 * (B / 64) * 2);
+        if (lstm_dma_enabled() && !g_lstm_dbg && (H == 512 || H == 256)) {
+            if (H == 512)
+                lstm_fwd_step_dma_kernel<512><<<grid, 256, 256 * 512, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t);
+            else
+                lstm_fwd_step_dma_kernel<256><<<grid, 256, 256 * 256, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t);
+            return ocrk::launch_status("ocrk_lstm_fwd_step");
+        }
         lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
     } else {
         OCRK_REQUIRE(H % 64 == 0 && B % 32 == 0, "ocrk_lstm_fwd_step: f32 needs H %% 64 == 0 and B %% 32 == 0 (H=%d B=%d)", H, B);
