@@ -15,36 +15,6 @@
 // (partials -> ordered sum -> apply) BN backward.
 #include "common.h"
 
-struct F8 { float v[8]; };
-
-template <typename T> __device__ __forceinline__ F8 load8(const T* p);
-template <> __device__ __forceinline__ F8 load8<float>(const float* p) {
-    F8 r;
-    float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
-    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-    return r;
-}
-template <> __device__ __forceinline__ F8 load8<bf16>(const bf16* p) {
-    union { uint4 q; bf16 e[8]; } u;
-    u.q = *reinterpret_cast<const uint4*>(p);
-    F8 r;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = (float)u.e[i];
-    return r;
-}
-template <typename T> __device__ __forceinline__ void store8(T* p, const F8& x);
-template <> __device__ __forceinline__ void store8<float>(float* p, const F8& x) {
-    reinterpret_cast<float4*>(p)[0] = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
-    reinterpret_cast<float4*>(p)[1] = make_float4(x.v[4], x.v[5], x.v[6], x.v[7]);
-}
-template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const F8& x) {
-    union { uint4 q; bf16 e[8]; } u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) u.e[i] = (bf16)x.v[i];
-    *reinterpret_cast<uint4*>(p) = u.q;
-}
-
 // --------------------------------------------------------------- finalize
 // One block per channel: Chan-merge the per-tile (sum, M2) partials.
 __global__ void __launch_bounds__(256)
@@ -245,6 +215,161 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
     }
 }
 
+// pass 1, window-centric (the pools of the path: KH == stride_h, SW <= KW).
+// Thread = (image b, pooled row ho, SEG consecutive pooled columns, 8
+// channels). It streams the KH pre-pool rows of its column range left to
+// right through a KW-column register window, evaluates each pooling window
+// ONCE ([TF1] first max, row-major scan of relu(bn(z))), adds dp to the
+// winner's register accumulator and retires a column (ReLU mask, store, sums)
+// as it leaves the window: every z element is read once, instead of once per
+// covering window plus once for itself as in bn_bwd_reduce_kernel. The
+// PRE = (KW-1)/SW windows left of the range that still reach into it are
+// re-evaluated (their own columns are not retired here). Rows below the last
+// pooling window, and columns right of it, receive no gradient: zeros.
+template <typename T, int KH, int KW, int SW, int SEG>
+__global__ void __launch_bounds__(256)
+bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
+                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                    const float* __restrict__ gamma, const float* __restrict__ beta, int dp_time_major,
+                    int nseg, int tasks_per_block, float* __restrict__ slab, T* __restrict__ da_out) {
+    static_assert(SW >= 1 && SW <= KW, "stride <= window");
+    constexpr int PRE = (KW - 1) / SW;
+    __shared__ float red[256][17];
+    const int G = C / 8;
+    const int Ho = (H - KH) / KH + 1, Wo = (W - KW) / SW + 1;
+    const int tasks = B * Ho * nseg * G;
+    const int g = threadIdx.x % G;
+    const int c0 = g * 8;
+    float sc[8], sf[8], mu[8], is[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        is[i] = invstd[c0 + i];
+        mu[i] = mean[c0 + i];
+        sc[i] = gamma[c0 + i] * is[i];
+        sf[i] = beta[c0 + i] - mu[i] * sc[i];
+    }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+    const int t0 = blockIdx.x * tasks_per_block;
+    const int t1 = min(tasks, t0 + tasks_per_block);
+    for (int task = t0 + threadIdx.x; task < t1; task += 256) {
+        int rest = task / G;
+        const int seg = rest % nseg;
+        rest /= nseg;
+        const int ho = rest % Ho, b = rest / Ho;
+        const int wa = seg * SEG, wb = min(Wo, wa + SEG);
+        const int own0 = wa * SW, own1 = (seg == nseg - 1) ? W : wb * SW;
+        const bool tail_rows = (ho == Ho - 1) && (Ho * KH < H);
+        const T* zrow = z + (((int64_t)b * H + ho * KH) * W) * C + c0;
+        T* drow = da_out + (((int64_t)b * H + ho * KH) * W) * C + c0;
+
+        float zr[KW][KH][8], dr[KW][KH][8];
+        auto retire = [&](int x, const float (&zc)[KH][8], const float (&dc)[KH][8]) {
+            if (x < own0 || x >= own1) return;
+#pragma unroll
+            for (int dh = 0; dh < KH; ++dh) {
+                F8 o;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float d = fmaf(zc[dh][i], sc[i], sf[i]) > 0.f ? dc[dh][i] : 0.f;
+                    s1[i] += d;
+                    s2[i] += d * ((zc[dh][i] - mu[i]) * is[i]);
+                    o.v[i] = d;
+                }
+                store8(drow + ((int64_t)dh * W + x) * C, o);
+            }
+            if (tail_rows) {
+                F8 zero;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) zero.v[i] = 0.f;
+                for (int h = Ho * KH; h < H; ++h) store8(da_out + (((int64_t)b * H + h) * W + x) * C + c0, zero);
+            }
+        };
+        const int wfirst = max(0, wa - PRE);
+#pragma unroll
+        for (int j = 0; j < KW; ++j)
+#pragma unroll
+            for (int dh = 0; dh < KH; ++dh) {
+                F8 v = load8(zrow + ((int64_t)dh * W + wfirst * SW + j) * C);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { zr[j][dh][i] = v.v[i]; dr[j][dh][i] = 0.f; }
+            }
+        for (int wo = wfirst; wo < wb; ++wo) {
+            const int x0 = wo * SW;
+            // next window's new columns and this window's pooled gradient in flight first
+            F8 nz[SW][KH];
+            const bool more = wo + 1 < wb;
+            if (more) {
+#pragma unroll
+                for (int j = 0; j < SW; ++j)
+#pragma unroll
+                    for (int dh = 0; dh < KH; ++dh) nz[j][dh] = load8(zrow + ((int64_t)dh * W + x0 + KW + j) * C);
+            }
+            const int64_t o = dp_time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
+                                            : (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+            const F8 gp = load8(dp + o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                float best = -INFINITY;
+                int arg = -1;
+#pragma unroll
+                for (int dh = 0; dh < KH; ++dh)
+#pragma unroll
+                    for (int j = 0; j < KW; ++j) {
+                        const float y = fmaxf(fmaf(zr[j][dh][i], sc[i], sf[i]), 0.f);
+                        if (y > best) { best = y; arg = dh * KW + j; }
+                    }
+#pragma unroll
+                for (int dh = 0; dh < KH; ++dh)
+#pragma unroll
+                    for (int j = 0; j < KW; ++j)
+                        if (arg == dh * KW + j) dr[j][dh][i] += gp.v[i];
+            }
+            // the first SW columns leave the window
+#pragma unroll
+            for (int j = 0; j < SW; ++j) retire(x0 + j, zr[j], dr[j]);
+            if (!more) break;
+#pragma unroll
+            for (int j = 0; j + SW < KW; ++j)
+#pragma unroll
+                for (int dh = 0; dh < KH; ++dh)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) { zr[j][dh][i] = zr[j + SW][dh][i]; dr[j][dh][i] = dr[j + SW][dh][i]; }
+#pragma unroll
+            for (int j = 0; j < SW; ++j)
+#pragma unroll
+                for (int dh = 0; dh < KH; ++dh)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        zr[KW - SW + j][dh][i] = nz[j][dh].v[i];
+                        dr[KW - SW + j][dh][i] = 0.f;
+                    }
+        }
+        // columns still in the last window, then the uncovered ones on the right
+        const int xl = (wb - 1) * SW;
+#pragma unroll
+        for (int j = SW; j < KW; ++j) retire(xl + j, zr[j], dr[j]);
+        for (int x = max(xl + KW, own0); x < own1; ++x) {
+            float zc[KH][8], dc[KH][8];                     // no gradient: z is not needed
+#pragma unroll
+            for (int dh = 0; dh < KH; ++dh)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) zc[dh][i] = dc[dh][i] = 0.f;
+            retire(x, zc, dc);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 2 * C; o += 256) {
+        int which = o / C, c = o % C, gg = c / 8, ci = c % 8;
+        float s = 0.f;
+        for (int q = gg; q < 256; q += G) s += red[q][which * 8 + ci];
+        slab[(int64_t)blockIdx.x * 2 * C + o] = s;
+    }
+}
+
 // Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
 // accumulation, in two stages so the ~2k slab rows are spread over many
 // workgroups: stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
@@ -377,6 +502,22 @@ extern "C" int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, 
 static int64_t bn_bwd_blocks(int64_t items) { return std::max<int64_t>(1, std::min<int64_t>(2048, ocrk::cdiv(items, 256 * 8))); }
 static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::cdiv(items, nb), 256) * 256; }
 
+// Window-centric pass 1 covers the path's pools (2x2/[2,2], 2x2/[2,1],
+// [3,1]/[3,1]); 0 = use the pixel-centric kernel. OCRK_BN_ROUTE=0 disables it.
+constexpr int BN_ROUTE_SEG = 8;
+static int bn_route_variant(int kh, int kw, int sh, int sw, int H, int W) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("OCRK_BN_ROUTE");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (!on || sh != kh || H < kh || W < kw) return 0;
+    if (kh == 2 && kw == 2 && sw == 2) return 1;
+    if (kh == 2 && kw == 2 && sw == 1) return 2;
+    if (kh == 3 && kw == 1 && sw == 1) return 3;
+    return 0;
+}
+
 // part [SLAB_P][2C] doubles | slab [nb][2C] | dsum [2C] | bias slab [nb][C] | routed da [B*H*W*C]
 // (4 B per element: any dtype)
 static size_t bn_ws_floats(int64_t nb, int C) {
@@ -411,13 +552,38 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
     void* da = (float*)ws + bn_ws_floats(nb, C);
     const int npix = B * H * W;
     hipStream_t s = ocrk::as_stream(stream);
-    if (dtype == OCRK_BF16)
+    int nr = (int)nb;                                   // slab rows of pass 1
+    const int rk = bn_route_variant(kh, kw, sh, sw, H, W);
+    if (rk) {
+        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
+        const int nseg = (int)ocrk::cdiv(Wo, BN_ROUTE_SEG);
+        const int64_t tasks = (int64_t)B * Ho * nseg * (C / 8);
+        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
+        const int tpb = (int)(ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
+        nr = (int)ocrk::cdiv(tasks, tpb);
+#define ROUTE_ARGS B, H, W, C, mean, invstd, gamma, beta, dp_time_major, nseg, tpb, slab
+        if (dtype == OCRK_BF16) {
+            const bf16 *zz = (const bf16*)z, *pp = (const bf16*)dp;
+            bf16* dd = (bf16*)da;
+            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else if (rk == 2) bn_bwd_route_kernel<bf16, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+        } else {
+            const float *zz = (const float*)z, *pp = (const float*)dp;
+            float* dd = (float*)da;
+            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else if (rk == 2) bn_bwd_route_kernel<float, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+        }
+#undef ROUTE_ARGS
+    } else if (dtype == OCRK_BF16) {
         bn_bwd_reduce_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, (int)ipb, slab, (bf16*)da);
-    else
+    } else {
         bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, (int)ipb, slab, (float*)da);
+    }
     int st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
     if (st) return st;
-    st = slab_sum(slab, (int)nb, 2 * C, part, dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
+    st = slab_sum(slab, nr, 2 * C, part, dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
     if (st) return st;
     float* bs = dbias ? bslab : nullptr;
     if (dtype == OCRK_BF16)

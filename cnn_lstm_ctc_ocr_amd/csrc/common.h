@@ -37,6 +37,46 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// 8 consecutive elements as fp32 (16-B / 32-B vector access).
+struct F8 { float v[8]; };
+
+template <typename T> __device__ __forceinline__ F8 load8(const T* p);
+template <> __device__ __forceinline__ F8 load8<float>(const float* p) {
+    F8 r;
+    float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+template <> __device__ __forceinline__ F8 load8<bf16>(const bf16* p) {
+    union { uint4 q; bf16 e[8]; } u;
+    u.q = *reinterpret_cast<const uint4*>(p);
+    F8 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (float)u.e[i];
+    return r;
+}
+template <typename T> __device__ __forceinline__ void store8(T* p, const F8& x);
+template <> __device__ __forceinline__ void store8<float>(float* p, const F8& x) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const F8& x) {
+    union { uint4 q; bf16 e[8]; } u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u.e[i] = (bf16)x.v[i];
+    *reinterpret_cast<uint4*>(p) = u.q;
+}
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at bits 15:14;
+// expcnt and lgkmcnt left at their maxima). Counted waits let LDS-DMA stages
+// land one at a time while later stages stay in flight.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
+}
+
 // 64-lane wave reductions.
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

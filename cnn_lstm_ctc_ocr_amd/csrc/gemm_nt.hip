@@ -33,12 +33,6 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, u
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at bits 15:14; expcnt, lgkmcnt left at max)
-    __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
-}
-
 template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4>
 __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
@@ -159,14 +153,14 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         // stage kt landed: the stages issued after it (up to S-2 of them) may stay in flight
         const int ahead = min(S - 2, nk - 1 - kt);
         if constexpr (S >= 4) {
-            if (ahead >= 2) wait_vm<2 * NPS>();
-            else if (ahead == 1) wait_vm<NPS>();
-            else wait_vm<0>();
+            if (ahead >= 2) vm_wait<2 * NPS>();
+            else if (ahead == 1) vm_wait<NPS>();
+            else vm_wait<0>();
         } else if constexpr (S == 3) {
-            if (ahead >= 1) wait_vm<NPS>();
-            else wait_vm<0>();
+            if (ahead >= 1) vm_wait<NPS>();
+            else vm_wait<0>();
         } else {
-            wait_vm<0>();
+            vm_wait<0>();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                     // everyone's stage kt is in, stage kt-1 is free

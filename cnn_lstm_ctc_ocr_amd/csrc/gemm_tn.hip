@@ -23,11 +23,6 @@ __device__ __forceinline__ void tn_dma16(__amdgpu_buffer_rsrc_t r, void* lds, un
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int N>
-__device__ __forceinline__ void tn_wait_vm() {
-    __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
-}
-
 template <int CPR>
 __device__ __forceinline__ int tn_swz(int r) { return CPR >= 8 ? (r & (CPR - 1)) : ((r >> 2) & (CPR - 1)); }
 
@@ -160,10 +155,10 @@ __global__ void __launch_bounds__(NW * 64) gemm_tn_kernel(const GemmParams p) {
     for (int kt = 0; kt < nk; ++kt) {
         const int ahead = min(S - 2, nk - 1 - kt);
         if constexpr (S >= 3) {
-            if (ahead >= 1) tn_wait_vm<NPS>();
-            else tn_wait_vm<0>();
+            if (ahead >= 1) vm_wait<NPS>();
+            else vm_wait<0>();
         } else {
-            tn_wait_vm<0>();
+            vm_wait<0>();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();

@@ -244,6 +244,85 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
 }
 
 // -------------------------------------------------------------- backward
+// Per-thread epilogue operands of a backward step (independent of the
+// recurrent product, so they are fetched before / while it is computed).
+template <int BR, int HU>
+struct LstmBwdOps {
+    static constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+    static constexpr bool EFULL = (BR * UQ) % 256 == 0;   // whole passes: no lane guard
+    int plen[EPQ4];
+    float pa[EPQ4][4][4], pcp[EPQ4][4], pdc[EPQ4][4], pdo[EPQ4][4];
+
+    template <typename CT>
+    __device__ __forceinline__ void load(const int* __restrict__ seq_len, const float* __restrict__ dc_state,
+                                         const CT* __restrict__ acts_t, const float* __restrict__ cprev_t,
+                                         const CT* __restrict__ dout, int s, int B, int H, int b0, int u0,
+                                         int dir) {
+#pragma unroll
+        for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min((int)threadIdx.x + 256 * q, BR * UQ - 1) / UQ];
+        const int G4 = 4 * H;
+#pragma unroll
+        for (int q = 0; q < EPQ4; ++q) {
+            const int idx = threadIdx.x + 256 * q;
+            if (!EFULL && idx >= BR * UQ) continue;
+            const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+            ld4(pdc[q], dc_state + ((int64_t)dir * B + b) * H + uu);
+            const int t = step_time(dir, s, plen[q]);
+            const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
+            const CT* a = acts_t + tb * G4 + uu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ld4(pa[q][k], a + k * H);
+            ld4(pcp[q], cprev_t + tb * H + uu);
+            ld4(pdo[q], dout + ((int64_t)t * B + b) * 2 * H + dir * H + uu);
+        }
+    }
+
+    // sG: the recurrent product dh_rec as [BR][HU + 1] fp32.
+    template <typename CT>
+    __device__ __forceinline__ void epilogue(const float* __restrict__ sG, int s, int B, int H, int b0, int u0,
+                                             int dir, float* __restrict__ dc_state, CT* __restrict__ dg_out,
+                                             CT* __restrict__ dG_t) const {
+        const int G4 = 4 * H;
+#pragma unroll
+        for (int q = 0; q < EPQ4; ++q) {
+            const int idx = threadIdx.x + 256 * q;
+            if (!EFULL && idx >= BR * UQ) continue;
+            const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
+            const int len = plen[q];
+            const int t = step_time(dir, s, len);
+            const int64_t st = ((int64_t)dir * B + b) * H + uu;
+            const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
+            CT* dgo = dg_out + ((int64_t)dir * B + b) * G4 + uu;
+            CT* dgt = dG_t + tb * G4 + uu;
+            if (s < len) {
+                float di[4], dj[4], df[4], dO[4], dcn[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float dh = sG[r * (HU + 1) + u + e] + pdo[q][e];
+                    float ai = pa[q][0][e], aj = pa[q][1][e], af = pa[q][2][e], ao = pa[q][3][e];
+                    float cp = pcp[q][e];
+                    float c = af * cp + ai * aj;
+                    float tc = tanh_fast(c);
+                    float dc = pdc[q][e] + dh * ao * (1.f - tc * tc);
+                    dO[e] = dh * tc * ao * (1.f - ao);
+                    di[e] = dc * aj * ai * (1.f - ai);
+                    dj[e] = dc * ai * (1.f - aj * aj);
+                    df[e] = dc * cp * af * (1.f - af);
+                    dcn[e] = dc * af;
+                }
+                st4(dc_state + st, dcn);
+                st4(dgo + 0 * H, di); st4(dgo + 1 * H, dj); st4(dgo + 2 * H, df); st4(dgo + 3 * H, dO);
+                st4(dgt + 0 * H, di); st4(dgt + 1 * H, dj); st4(dgt + 2 * H, df); st4(dgt + 3 * H, dO);
+            } else {
+                const float z[4] = {0.f, 0.f, 0.f, 0.f};
+                st4(dc_state + st, z);
+                st4(dgo + 0 * H, z); st4(dgo + 1 * H, z); st4(dgo + 2 * H, z); st4(dgo + 3 * H, z);
+                st4(dgt + 0 * H, z); st4(dgt + 1 * H, z); st4(dgt + 2 * H, z); st4(dgt + 3 * H, z);
+            }
+        }
+    }
+};
+
 template <typename CT, int BR, int HU, int KC>
 __global__ void __launch_bounds__(256)
 lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT* __restrict__ dg_out,
@@ -255,74 +334,94 @@ lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT
     const StepTile tl = step_tile(H / HU, B / BR);
     const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G4 = 4 * H;
-
-    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
     static_assert(HU % 4 == 0, "4-unit epilogue vectors");
-    constexpr bool EFULL = (BR * UQ) % 256 == 0;     // whole passes: no lane guard (bf16 tiles)
-    int plen[EPQ4];
-#pragma unroll
-    for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min((int)threadIdx.x + 256 * q, BR * UQ - 1) / UQ];
     const CT* a_rows = dg_in + ((int64_t)dir * B + b0) * G4;
     const CT* wdir = wh + (int64_t)dir * H * G4;
     auto bcol = [&](int n) { return wdir + (int64_t)(u0 + n) * G4; };
     Core core;
     core.begin(a_rows, G4, bcol, G4);
-    float pa[EPQ4][4][4], pcp[EPQ4][4], pdc[EPQ4][4], pdo[EPQ4][4];
-#pragma unroll
-    for (int q = 0; q < EPQ4; ++q) {
-        const int idx = threadIdx.x + 256 * q;
-        if (!EFULL && idx >= BR * UQ) continue;
-        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
-        ld4(pdc[q], dc_state + ((int64_t)dir * B + b) * H + uu);
-        const int t = step_time(dir, s, plen[q]);
-        const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
-        const CT* a = acts_t + tb * G4 + uu;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ld4(pa[q][k], a + k * H);
-        ld4(pcp[q], cprev_t + tb * H + uu);
-        ld4(pdo[q], dout + ((int64_t)t * B + b) * 2 * H + dir * H + uu);
-    }
+    LstmBwdOps<BR, HU> ops;
+    ops.load(seq_len, dc_state, acts_t, cprev_t, dout, s, B, H, b0, u0, dir);
     floatx4 acc[Core::TPW];
     core.finish(a_rows, G4, bcol, G4, lds, acc);
     Core::spill(acc, lds);
-    const float* sG = reinterpret_cast<const float*>(lds);
+    ops.epilogue(reinterpret_cast<const float*>(lds), s, B, H, b0, u0, dir, dc_state, dg_out, dG_t);
+}
+
+// bf16 backward step with the operands streamed by LDS-DMA: the 64 dG rows
+// and the 16 W_h rows (K = 4H) pass through a two-buffer ring of 512-deep
+// k-chunks (80 KB each, 1 KB per row, 16-B chunks XOR-swizzled by row), so
+// chunk c+1 is in flight while chunk c is on MFMA. Wave w owns batch rows
+// 16w..16w+15 of the 64 x 16 product.
+template <int H_>
+__global__ void __launch_bounds__(256)
+lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ dg_in, bf16* __restrict__ dg_out,
+                         float* __restrict__ dc_state, const int* __restrict__ seq_len, int s, int T, int B,
+                         const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
+                         const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t) {
+    constexpr int BR = 64, HU = 16, H = H_, G4 = 4 * H;
+    constexpr int KCH = 512, NCH = G4 / KCH, ROWB = 2 * KCH;     // one wave instruction per 1-KB row
+    constexpr int BUFB = (BR + HU) * ROWB, NPS = (BR + HU) / 4;  // DMA instructions per wave per chunk
+    static_assert(G4 % KCH == 0 && NCH >= 2, "H = 256 or 512");
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const StepTile tl = step_tile(H / HU, B / BR);
+    const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    // epilogue operands first: vmcnt retires in order, so the counted waits
+    // below also cover them
+    LstmBwdOps<BR, HU> ops;
+    ops.load(seq_len, dc_state, acts_t, cprev_t, dout, s, B, H, b0, u0, dir);
+
+    const bf16* a_rows = dg_in + ((int64_t)dir * B + b0) * G4;
+    const bf16* wdir = wh + ((int64_t)dir * H + u0) * G4;
+    auto issue = [&](int c) {
+        char* sA = lds + (c & 1) * BUFB;
+        char* sB = sA + BR * ROWB;
 #pragma unroll
-    for (int q = 0; q < EPQ4; ++q) {
-        const int idx = threadIdx.x + 256 * q;
-        if (!EFULL && idx >= BR * UQ) continue;
-        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
-        const int len = plen[q];
-        const int t = step_time(dir, s, len);
-        const int64_t st = ((int64_t)dir * B + b) * H + uu;
-        const int64_t tb = ((int64_t)t * B + b) * 2 + dir;
-        CT* dgo = dg_out + ((int64_t)dir * B + b) * G4 + uu;
-        CT* dgt = dG_t + tb * G4 + uu;
-        if (s < len) {
-            float di[4], dj[4], df[4], dO[4], dcn[4];
+        for (int i = 0; i < BR / 4; ++i) {
+            const int r = i * 4 + wave;
+            __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * G4 + c * KCH + 8 * (lane ^ (r & 7))),
+                                             (__attribute__((address_space(3))) void*)(sA + r * ROWB), 16, 0, 0);
+        }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float dh = sG[r * (HU + 1) + u + e] + pdo[q][e];
-                float ai = pa[q][0][e], aj = pa[q][1][e], af = pa[q][2][e], ao = pa[q][3][e];
-                float cp = pcp[q][e];
-                float c = af * cp + ai * aj;
-                float tc = tanh_fast(c);
-                float dc = pdc[q][e] + dh * ao * (1.f - tc * tc);
-                dO[e] = dh * tc * ao * (1.f - ao);
-                di[e] = dc * aj * ai * (1.f - ai);
-                dj[e] = dc * ai * (1.f - aj * aj);
-                df[e] = dc * cp * af * (1.f - af);
-                dcn[e] = dc * af;
-            }
-            st4(dc_state + st, dcn);
-            st4(dgo + 0 * H, di); st4(dgo + 1 * H, dj); st4(dgo + 2 * H, df); st4(dgo + 3 * H, dO);
-            st4(dgt + 0 * H, di); st4(dgt + 1 * H, dj); st4(dgt + 2 * H, df); st4(dgt + 3 * H, dO);
-        } else {
-            const float z[4] = {0.f, 0.f, 0.f, 0.f};
-            st4(dc_state + st, z);
-            st4(dgo + 0 * H, z); st4(dgo + 1 * H, z); st4(dgo + 2 * H, z); st4(dgo + 3 * H, z);
-            st4(dgt + 0 * H, z); st4(dgt + 1 * H, z); st4(dgt + 2 * H, z); st4(dgt + 3 * H, z);
+        for (int i = 0; i < HU / 4; ++i) {
+            const int n = i * 4 + wave;
+            __builtin_amdgcn_global_load_lds((const void*)(wdir + (int64_t)n * G4 + c * KCH + 8 * (lane ^ (n & 7))),
+                                             (__attribute__((address_space(3))) void*)(sB + n * ROWB), 16, 0, 0);
+        }
+    };
+    issue(0);
+    issue(1);
+
+    const int i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) vm_wait<NPS>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();                       // everyone's chunk c has landed
+        const char* sA = lds + (c & 1) * BUFB + (wave * 16 + i16) * ROWB;
+        const char* sB = lds + (c & 1) * BUFB + BR * ROWB + i16 * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < KCH / 32; ++ks) {
+            const int slot = ((ks * 4 + g) ^ sw) * 16;
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + slot);
+            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sB + slot);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc, 0, 0, 0);
+        }
+        if (c + 2 < NCH) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();                   // buffer c & 1 is free again
+            issue(c + 2);
         }
     }
+    __syncthreads();
+    float* sG = reinterpret_cast<float*>(lds);              // [BR][HU + 1]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sG[(wave * 16 + g * 4 + r) * (HU + 1) + i16] = acc[r];
+    __syncthreads();
+    ops.epilogue(sG, s, B, H, b0, u0, dir, dc_state, dg_out, dG_t);
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -340,6 +439,24 @@ static bool lstm_dma_enabled() {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 512);
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<256>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 256);
+        }
+    }
+    return on == 1;
+}
+
+// Backward ring: 2 x 80 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it.
+constexpr int LSTM_BWD_DMA_LDS = 2 * (64 + 16) * 1024;
+static bool lstm_bwd_dma_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("OCRK_LSTM_BWD_DMA");
+        on = (e && e[0] == '0') ? 0 : 1;
+        if (on) {
+            hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<512>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
+            hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<256>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
+            if (e1 != hipSuccess || e2 != hipSuccess) on = 0;
         }
     }
     return on == 1;
@@ -382,6 +499,13 @@ extern "C" int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_ou
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 64 == 0 && B % 64 == 0, "ocrk_lstm_bwd_step: bf16 needs H %% 64 == 0 and B %% 64 == 0");
         dim3 grid(H / 16 * (B / 64) * 2);
+        if (lstm_bwd_dma_enabled() && !g_lstm_dbg && (H == 512 || H == 256)) {
+            if (H == 512)
+                lstm_bwd_step_dma_kernel<512><<<grid, 256, LSTM_BWD_DMA_LDS, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t);
+            else
+                lstm_bwd_step_dma_kernel<256><<<grid, 256, LSTM_BWD_DMA_LDS, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t);
+            return ocrk::launch_status("ocrk_lstm_bwd_step");
+        }
         lstm_bwd_step_kernel<BWD_BF16><<<grid, 256, 0, st>>>((const bf16*)wh, (const bf16*)dg_in, (bf16*)dg_out, dc_state, seq_len, s, T, B, H, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t);
     } else {
         OCRK_REQUIRE(H % 32 == 0 && B % 32 == 0, "ocrk_lstm_bwd_step: f32 needs H %% 32 == 0 and B %% 32 == 0");

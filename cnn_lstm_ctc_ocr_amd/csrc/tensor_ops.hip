@@ -24,41 +24,39 @@ __global__ void __launch_bounds__(256) permute3_kernel(const TI* __restrict__ in
     }
 }
 
-// column sums of [M][N]: each block reduces a row range with 8-column vector
-// loads (TPR threads per row), combines its threads in a fixed order, and
-// writes one slab row; reduce_slabs then sums the slabs in a fixed order
-// (deterministic for a given shape).
+// column sums of [M][N]: block (x, y) reduces column block x (TPR groups of 8
+// columns, one 16-B vector per thread per row; a wave reads 64 consecutive
+// chunks of a row when N >= 512) over row range y, combines its threads in a
+// fixed order and writes slab row y; reduce_slabs then sums the slabs in a
+// fixed order (deterministic for a given shape).
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict__ in, int64_t M, int N,
                                                              int64_t rows_per_block, float* __restrict__ slab) {
     __shared__ float red[256 * 9];
     const int G = N / 8;                       // column groups of 8
-    const int TPR = G < 256 ? G : 256;         // threads per row
+    const int TPR = G < 64 ? G : 64;           // threads per row
     const int RPP = 256 / TPR;                 // rows per pass
     const int tg = threadIdx.x % TPR, tr = threadIdx.x / TPR;
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int g = blockIdx.x * TPR + tg;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
-    for (int g0 = 0; g0 < G; g0 += TPR) {
-        const int g = g0 + tg;
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (tr < RPP && g < G) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (tr < RPP && g < G) {
 #pragma unroll 4
-            for (int64_t r = r0 + tr; r < r1; r += RPP) {
-                const T* p = in + r * N + g * 8;
+        for (int64_t r = r0 + tr; r < r1; r += RPP) {
+            const F8 v = load8(in + r * N + g * 8);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) acc[i] += to_f32(p[i]);
-            }
+            for (int i = 0; i < 8; ++i) acc[i] += v.v[i];
         }
+    }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) red[threadIdx.x * 9 + i] = acc[i];
-        __syncthreads();
-        for (int o = threadIdx.x; o < TPR * 8; o += 256) {
-            int gg = o / 8, i = o % 8;
-            float sum = 0.f;
-            for (int q = 0; q < RPP; ++q) sum += red[(q * TPR + gg) * 9 + i];
-            if (g0 + gg < G) slab[(int64_t)blockIdx.x * N + (g0 + gg) * 8 + i] = sum;
-        }
-        __syncthreads();
+    for (int i = 0; i < 8; ++i) red[threadIdx.x * 9 + i] = acc[i];
+    __syncthreads();
+    for (int o = threadIdx.x; o < TPR * 8; o += 256) {
+        int gg = o / 8, i = o % 8;
+        float sum = 0.f;
+        for (int q = 0; q < RPP; ++q) sum += red[(q * TPR + gg) * 9 + i];
+        if (blockIdx.x * TPR + gg < G) slab[(int64_t)blockIdx.y * N + (blockIdx.x * TPR + gg) * 8 + i] = sum;
     }
 }
 
@@ -111,10 +109,16 @@ extern "C" int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d
     return ocrk::launch_status("ocrk_permute3");
 }
 
-static int64_t colsum_blocks(int64_t M) { return std::max<int64_t>(1, std::min<int64_t>(256, ocrk::cdiv(M, 512))); }
+// Row blocks: enough (column block x row block) workgroups to fill the chip
+// (~2048), at least 64 rows each.
+static int colsum_col_blocks(int N) { return (int)ocrk::cdiv(N / 8, 64); }
+static int64_t colsum_blocks(int64_t M, int N) {
+    const int64_t want = std::max<int64_t>(1, 2048 / colsum_col_blocks(std::max(N, 8)));
+    return std::max<int64_t>(1, std::min<int64_t>(want, ocrk::cdiv(M, 64)));
+}
 
 extern "C" size_t ocrk_colsum_workspace_size(int64_t M, int N) {
-    return (size_t)colsum_blocks(M) * N * sizeof(float);
+    return (size_t)colsum_blocks(M, N) * N * sizeof(float);
 }
 
 extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
@@ -122,12 +126,13 @@ extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* o
     OCRK_REQUIRE(ws_bytes >= ocrk_colsum_workspace_size(M, N), "ocrk_colsum: workspace too small");
     OCRK_REQUIRE(N % 8 == 0, "ocrk_colsum: N=%d must be a multiple of 8", N);
     if (N == 0) return OCRK_OK;
-    int64_t nb = colsum_blocks(M);
+    int64_t nb = colsum_blocks(M, N);
     int64_t rpb = ocrk::cdiv(M, nb);
     nb = std::max<int64_t>(1, ocrk::cdiv(M, rpb));
     hipStream_t s = ocrk::as_stream(stream);
-    if (dtype == OCRK_BF16) colsum_partial_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)in, M, N, rpb, (float*)ws);
-    else colsum_partial_kernel<float><<<nb, 256, 0, s>>>((const float*)in, M, N, rpb, (float*)ws);
+    dim3 grid(colsum_col_blocks(N), (unsigned)nb);
+    if (dtype == OCRK_BF16) colsum_partial_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)in, M, N, rpb, (float*)ws);
+    else colsum_partial_kernel<float><<<grid, 256, 0, s>>>((const float*)in, M, N, rpb, (float*)ws);
     int st = ocrk::launch_status("ocrk_colsum");
     if (st) return st;
     reduce_slabs_kernel<<<(N + 63) / 64, 256, 0, s>>>((const float*)ws, (int)nb, N, out, accumulate);

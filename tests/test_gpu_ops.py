@@ -101,11 +101,15 @@ def test_conv3x3_fwd_bwd(cuda, cin, cout, relu):
     np.testing.assert_allclose(dw.cpu().numpy(), dw_ref, rtol=1e-4, atol=1e-3)
 
 
+# W = 11 / 37: one / several 8-window column segments of the window-centric
+# routing pass, an odd width leaves an uncovered column for the 2x2/[2,2]
+# pool, H = 7 an uncovered row for the 2-row pools.
+@pytest.mark.parametrize("W", [11, 37])
 @pytest.mark.parametrize("pool", [(2, 2, 2, 2), (2, 2, 2, 1), (3, 1, 3, 1)])
-def test_bn_relu_pool(cuda, pool):
+def test_bn_relu_pool(cuda, pool, W):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    rng = np.random.default_rng(sum(pool))
-    B, H, W, C = 2, 7 if pool[0] == 2 else 3, 11, 32
+    rng = np.random.default_rng(sum(pool) + W)
+    B, H, C = 2, 7 if pool[0] == 2 else 3, 32
     z = rng.standard_normal((B, H, W, C)).astype(np.float32)
     gamma = rng.standard_normal(C).astype(np.float32)
     beta = rng.standard_normal(C).astype(np.float32)
@@ -134,6 +138,23 @@ def test_bn_relu_pool(cuda, pool):
     np.testing.assert_allclose(dbias.cpu().numpy(), dz_ref.sum(axis=(0, 1, 2)), rtol=0, atol=1e-4)
     np.testing.assert_allclose(dg.cpu().numpy(), dg_ref, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(db.cpu().numpy(), db_ref, rtol=1e-4, atol=1e-5)
+
+
+# column sums (bias gradients of the odd convs, recurrent and logits layers)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(37, 64), (5000, 24), (3001, 4096), (20000, 256)])
+def test_colsum(cuda, dtype, M, N):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(M + N)
+    x = rng.standard_normal((M, N)).astype(np.float32)
+    xd = _t(x, cuda, dtype)
+    ref = xd.double().sum(0).cpu().numpy() + 1.5
+    out = torch.full((N,), 1.5, device=cuda)
+    Kn.colsum(xd, M, N, out, accumulate=True)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=1e-5 * np.sqrt(M) + 1e-5)
+    out2 = torch.full((N,), 9.0, device=cuda)
+    Kn.colsum(xd, M, N, out2, accumulate=False)
+    np.testing.assert_allclose(out2.cpu().numpy(), ref - 1.5, rtol=0, atol=1e-5 * np.sqrt(M) + 1e-5)
 
 
 # --------------------------------------------------------------------- LSTM
