@@ -147,18 +147,20 @@ lstm_fwd_step_kernel(const CT* __restrict__ gx, const CT* __restrict__ whT, cons
 // each, fetched in ONE burst of LDS-DMA (global_load_lds_dwordx4: no VGPR
 // round trip, every load in flight at once) while the epilogue operands load
 // into registers; then the 64 x 64 x H product on MFMA straight from LDS.
-// Rows are lane-linear with the 16-B chunk index XOR-swizzled by (row & 7) on
-// the global side, so fragment reads are conflict-free.
+// Rows are lane-linear with the 16-B chunk index XOR-swizzled by (row & 15) on
+// the global side, so each 16-lane group of a ds_read_b128 fragment read covers
+// all 64 banks (conflict-free; row starts are 256-B aligned).
 template <int H_>
 __global__ void __launch_bounds__(256)
 lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, const bf16* __restrict__ h_in,
                          bf16* __restrict__ h_out, float* __restrict__ c_state, const int* __restrict__ seq_len,
                          int s, int T, int B, bf16* __restrict__ out, bf16* __restrict__ hprev_t,
-                         float* __restrict__ cprev_t, bf16* __restrict__ acts_t) {
+                         float* __restrict__ cprev_t, bf16* __restrict__ acts_t, long long* __restrict__ dbg) {
     constexpr int BR = 64, HU = 16, NC = 4 * HU, H = H_;
+    stamp(dbg, 0);
     constexpr int ROWB = 2 * H, CPR = ROWB / 16, RPI = 64 / CPR;     // 16-B chunks per row, rows per wave instr
     constexpr int NI = BR / (4 * RPI);                              // instructions per wave per operand
-    static_assert(CPR % 8 == 0 && 64 % CPR == 0, "H = 256 or 512");
+    static_assert(CPR % 16 == 0 && 64 % CPR == 0, "H = 256 or 512");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     char* sA = lds;
     char* sB = lds + BR * ROWB;
@@ -179,7 +181,7 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int r = (i * 4 + wave) * RPI + lrow;
-        const int c = (lane % CPR) ^ (r & 7);
+        const int c = (lane % CPR) ^ (r & 15);
         __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * H + 8 * c),
                                          (__attribute__((address_space(3))) void*)(sA + (i * 4 + wave) * RPI * ROWB),
                                          16, 0, 0);
@@ -189,6 +191,7 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
                                          16, 0, 0);
     }
     (void)chunk;
+    stamp(dbg, 1);
     // 2. epilogue operands (do not depend on the product)
     float pg[EPQ4][4][4], pc[EPQ4][4], ph[EPQ4][4];
 #pragma unroll
@@ -203,31 +206,22 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
 #pragma unroll
         for (int k = 0; k < 4; ++k) ld4(pg[q][k], g + k * H);
     }
+    stamp(dbg, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(dbg, 3);
 
     // 3. 64 x 64 x H on MFMA, 2 x 2 waves of 32 x 32
-    const int wm = wave >> 1, wn = wave & 1, i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+    const int wm = wave >> 1, wn = wave & 1, i16 = lane & 15, g = lane >> 4, sw = lane & 15;
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int ks = 0; ks < H / 32; ++ks) {
-        const int slot = ((ks * 4 + g) ^ sw) * 16;
-        bf16x8 af[2], bfr[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * 32 + i * 16 + i16) * ROWB + slot);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * 32 + j * 16 + i16) * ROWB + slot);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    {
+        const char* ar[2] = {sA + (wm * 32 + i16) * ROWB, sA + (wm * 32 + 16 + i16) * ROWB};
+        const char* br[2] = {sB + (wn * 32 + i16) * ROWB, sB + (wn * 32 + 16 + i16) * ROWB};
+        lds_mma_16x16x32<H / 32, 2, 2>(ar, br, g, sw, acc);
     }
     __syncthreads();
     float* sG = reinterpret_cast<float*>(lds);                      // [BR][NC+1]
@@ -239,8 +233,10 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
             for (int r = 0; r < 4; ++r)
                 sG[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * (NC + 1) + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
     __syncthreads();
+    stamp(dbg, 4);
     lstm_fwd_epilogue<bf16, BR, HU>(sG, plen, pg, pc, ph, s, B, H, b0, u0, dir, c_state, h_out, out, hprev_t,
                                     cprev_t, acts_t);
+    stamp(dbg, 5);
 }
 
 // -------------------------------------------------------------- backward
@@ -381,20 +377,20 @@ lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ d
 #pragma unroll
         for (int i = 0; i < BR / 4; ++i) {
             const int r = i * 4 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * G4 + c * KCH + 8 * (lane ^ (r & 7))),
+            __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * G4 + c * KCH + 8 * (lane ^ (r & 15))),
                                              (__attribute__((address_space(3))) void*)(sA + r * ROWB), 16, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < HU / 4; ++i) {
             const int n = i * 4 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(wdir + (int64_t)n * G4 + c * KCH + 8 * (lane ^ (n & 7))),
+            __builtin_amdgcn_global_load_lds((const void*)(wdir + (int64_t)n * G4 + c * KCH + 8 * (lane ^ (n & 15))),
                                              (__attribute__((address_space(3))) void*)(sB + n * ROWB), 16, 0, 0);
         }
     };
     issue(0);
     issue(1);
 
-    const int i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+    const int i16 = lane & 15, g = lane >> 4, sw = lane & 15;
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -403,12 +399,11 @@ lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ d
         __builtin_amdgcn_s_barrier();                       // everyone's chunk c has landed
         const char* sA = lds + (c & 1) * BUFB + (wave * 16 + i16) * ROWB;
         const char* sB = lds + (c & 1) * BUFB + BR * ROWB + i16 * ROWB;
-#pragma unroll
-        for (int ks = 0; ks < KCH / 32; ++ks) {
-            const int slot = ((ks * 4 + g) ^ sw) * 16;
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + slot);
-            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(sB + slot);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc, 0, 0, 0);
+        {
+            const char* ar[1] = {sA};
+            const char* br[1] = {sB};
+            floatx4 (&acc11)[1][1] = reinterpret_cast<floatx4 (&)[1][1]>(acc);
+            lds_mma_16x16x32<KCH / 32, 1, 1, 4>(ar, br, g, sw, acc11);
         }
         if (c + 2 < NCH) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -475,11 +470,11 @@ extern "C" int ocrk_lstm_fwd_step(const void* gx, const void* whT, const void* h
     if (dtype == OCRK_BF16) {
         OCRK_REQUIRE(H % 256 == 0 && B % 64 == 0, "ocrk_lstm_fwd_step: bf16 needs H %% 256 == 0 and B %% 64 == 0 (H=%d B=%d)", H, B);
         dim3 grid(H / 16 * (B / 64) * 2);
-        if (lstm_dma_enabled() && !g_lstm_dbg && (H == 512 || H == 256)) {
+        if (lstm_dma_enabled() && (H == 512 || H == 256)) {
             if (H == 512)
-                lstm_fwd_step_dma_kernel<512><<<grid, 256, 256 * 512, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t);
+                lstm_fwd_step_dma_kernel<512><<<grid, 256, 256 * 512, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
             else
-                lstm_fwd_step_dma_kernel<256><<<grid, 256, 256 * 256, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t);
+                lstm_fwd_step_dma_kernel<256><<<grid, 256, 256 * 256, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
             return ocrk::launch_status("ocrk_lstm_fwd_step");
         }
         lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);

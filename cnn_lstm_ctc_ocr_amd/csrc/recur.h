@@ -159,40 +159,82 @@ __device__ __forceinline__ void st4(bf16* p, const float (&v)[4]) {
 __device__ __forceinline__ void st4(float* p, const float (&v)[4]) {
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
 }
-// exp-based gate nonlinearities (one v_exp each)
-__device__ __forceinline__ float sig_fast(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_fast(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+// exp-based gate nonlinearities: one v_exp + one v_rcp each (1-ulp hardware
+// reciprocal instead of the ~10-instruction IEEE division sequence, which
+// made up ~40 % of the step epilogue's VALU work). Saturate correctly:
+// exp -> inf gives rcp(inf) = 0.
+__device__ __forceinline__ float sig_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; }
 
 __device__ __forceinline__ int step_time(int dir, int s, int len) {
     return (dir == 0 || s >= len) ? s : len - 1 - s;
 }
 
+// acc[i][j] += A_i . B_j over NKS 32-deep k-steps, both operands resident in
+// LDS as lane-linear rows whose 16-B chunks are XOR-swizzled by (row & 15):
+// arow[i] / brow[j] point at this lane's row (16-row fragment i16 = lane&15),
+// g = lane >> 4 picks the 8-element k group, sw = row & 15. Fully unrolled
+// with the fragment reads PF k-steps ahead of the MFMAs that use them (left
+// to itself the scheduler sinks every read next to its MFMA and waits on
+// it; a sched_barrier per k-step pins the order), and the chunk offsets
+// precomputed so each read is one ds_read_b128 with an immediate offset.
+template <int NKS, int TM, int TN, int PF = 2>
+__device__ __forceinline__ void lds_mma_16x16x32(const char* const (&arow)[TM], const char* const (&brow)[TN],
+                                                 int g, int sw, floatx4 (&acc)[TM][TN]) {
+    const int gs = g ^ sw;                              // (4 ks + g) ^ sw == 4 ks ^ (g ^ sw)
+    const char* pa[TM][4];
+    const char* pb[TN][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int off = ((4 * q) ^ gs) * 16;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) pa[i][q] = arow[i] + off;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) pb[j][q] = brow[j] + off;
+    }
+    constexpr int R = PF + 1;
+    bf16x8 fa[R][TM], fb[R][TN];
+    auto load = [&](int ks, int slot) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[slot][i] = *reinterpret_cast<const bf16x8*>(pa[i][ks & 3] + (ks >> 2) * 256);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[slot][j] = *reinterpret_cast<const bf16x8*>(pb[j][ks & 3] + (ks >> 2) * 256);
+    };
+#pragma unroll
+    for (int ks = 0; ks < PF && ks < NKS; ++ks) load(ks, ks);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        if (ks + PF < NKS) load(ks + PF, (ks + PF) % R);
+        // keep the scheduler from sinking the reads next to their MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        const int c = ks % R;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c][i], fb[c][j], acc[i][j], 0, 0, 0);
+    }
+}
+
 // Workgroup -> (unit block, batch block, direction) of a recurrent step
 // launch on a 1-D grid of nU * nB * 2 workgroups. Dispatch hands consecutive
-// block ids round-robin to the 8 XCDs, so the map puts all unit blocks of one
-// (batch block, direction) group on the same XCD whenever the group count
-// allows: the group's h tile, which every one of its unit blocks reads each
-// step, then comes from MALL once per XCD and hits L2 after that, and the
-// direction's W_h slices stay in that XCD's L2 across steps. (Placement is a
-// speed choice only: nothing depends on it for correctness.)
+// block ids round-robin to the 8 XCDs; the map gives each XCD a contiguous
+// range of (direction, unit block, batch block) with the batch block
+// fastest, i.e. a 1/8 slice of the direction's units for every batch block.
+// An XCD then reads only its own W_h slice (1/8 of W_h, each row slice
+// shared by the nB workgroups of that unit block) plus the direction's h,
+// instead of the whole W_h[dir] -- measured: the previous map, all unit
+// blocks of one (batch block, direction) on an XCD, re-fetched all of W_h
+// from beyond L2 every step (FETCH_SIZE ~20 MB per step at B=256, H=512;
+// L2 does not keep it across launches). Placement is a speed choice only:
+// nothing depends on it for correctness.
 struct StepTile { int u, b, dir; };
 __device__ __forceinline__ StepTile step_tile(int nU, int nB) {
-    const int id = blockIdx.x, G = 2 * nB;
-    const int xcd = id & 7, slot = id >> 3;
-    int group, u;
-    if (G <= 8 && 8 % G == 0 && nU % (8 / G) == 0) {
-        const int q = 8 / G;
-        group = xcd % G;
-        u = slot * q + xcd / G;
-    } else if (G % 8 == 0) {
-        const int r = G / 8;
-        group = xcd + 8 * (slot % r);
-        u = slot / r;
-    } else {
-        group = id / nU;
-        u = id % nU;
-    }
-    return {u, group >> 1, group & 1};
+    const int id = blockIdx.x, total = 2 * nU * nB;
+    int j = id;
+    if (total % 8 == 0) j = (id & 7) * (total >> 3) + (id >> 3);
+    const int b = j % nB, rest = j / nB;
+    return {rest % nU, b, rest / nU};
 }
 
 }  // namespace ocrk

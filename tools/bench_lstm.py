@@ -26,7 +26,7 @@ def run(B, H=512, n_in=1024, T=125, reps=3, dt=torch.bfloat16):
     b = e[1].elapsed_time(e[2]) / reps / T * 1e3
     print(f"B={B:4d} H={H}: fwd step {f:7.2f} us   bwd step {b:7.2f} us", flush=True)
 
-for B in (64, 128, 256, 512):
+for B in ([int(a) for a in sys.argv[1:] if a.isdigit()] or (64, 128, 256, 512)):
     run(B)
 
 # in-kernel stamps of one forward step (thread 0 of each workgroup, 100 MHz clock)
@@ -48,6 +48,8 @@ if "--stamps" in sys.argv:
     t0 = st[:, 0].min()
     print("stamp (ns since first WG start): median / max over workgroups")
     names = ["start", "gemm loads issued", "epilogue loads issued", "gemm done", "spill done", "end"]
+    if os.environ.get("OCRK_LSTM_DMA", "1") != "0":
+        names = ["start", "dma issued", "epilogue loads issued", "operands landed", "mfma+spill done", "end"]
     for i, n in enumerate(names):
         print(f"  {n:24s} {np.median(st[:, i] - t0):9.0f} {np.max(st[:, i] - t0):9.0f}")
     d = st[:, 1:] - st[:, :-1]
