@@ -142,14 +142,16 @@ lstm_fwd_step_kernel(const CT* __restrict__ gx, const CT* __restrict__ whT, cons
     stamp(dbg, 5);
 }
 
-// Forward step with the whole GEMM operand set in LDS (bf16, K = H <= 512):
-// 64 h rows and the 64 W_h^T rows of this tile's 16 units x 4 gates, 2H bytes
-// each, fetched in ONE burst of LDS-DMA (global_load_lds_dwordx4: no VGPR
-// round trip, every load in flight at once) while the epilogue operands load
-// into registers; then the 64 x 64 x H product on MFMA straight from LDS.
-// Rows are lane-linear with the 16-B chunk index XOR-swizzled by (row & 15) on
-// the global side, so each 16-lane group of a ds_read_b128 fragment read covers
-// all 64 banks (conflict-free; row starts are 256-B aligned).
+// Forward step with the whole operand set in LDS (bf16, K = H <= 512), moved
+// by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, all in flight at
+// once) in k-block-major order: block kc = k in [128 kc, 128 kc + 128) of the
+// 64 h rows and the 64 W_h^T rows of this tile's 16 units x 4 gates, 256 B
+// per row, 16-B chunks XOR-swizzled by (row & 15) on the global side (each
+// 16-lane group of a ds_read_b128 fragment read covers all 64 banks). The
+// MFMAs of block kc start as soon as it has landed (counted vmcnt, raw
+// s_barrier) while later blocks are in flight. The epilogue operands (gx
+// tile, c tile) ride the same DMA queue behind the GEMM blocks; h_{s-1} of
+// the tile's own units is read back from the A image.
 template <int H_>
 __global__ void __launch_bounds__(256)
 lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, const bf16* __restrict__ h_in,
@@ -157,74 +159,118 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
                          int s, int T, int B, bf16* __restrict__ out, bf16* __restrict__ hprev_t,
                          float* __restrict__ cprev_t, bf16* __restrict__ acts_t, long long* __restrict__ dbg) {
     constexpr int BR = 64, HU = 16, NC = 4 * HU, H = H_;
-    stamp(dbg, 0);
-    constexpr int ROWB = 2 * H, CPR = ROWB / 16, RPI = 64 / CPR;     // 16-B chunks per row, rows per wave instr
-    constexpr int NI = BR / (4 * RPI);                              // instructions per wave per operand
-    static_assert(CPR % 16 == 0 && 64 % CPR == 0, "H = 256 or 512");
+    constexpr int NCH = H / 128, ROWB = 256, BLK = 2 * BR * ROWB;   // k blocks, bytes per row per block, block bytes
+    constexpr int GX_OFF = NCH * BLK, C_OFF = GX_OFF + BR * 4 * HU * 2;
+    static_assert(H % 128 == 0 && NCH >= 1 && NCH <= 4, "H = 128, 256, 384 or 512");
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    char* sA = lds;
-    char* sB = lds + BR * ROWB;
+    stamp(dbg, 0);
     const StepTile tl = step_tile(H / HU, B / BR);
     const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int G4 = 4 * H;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int UQ = HU / 4, EPQ4 = (BR * UQ + 255) / 256;
+    constexpr int UQ = HU / 4;
+    static_assert(BR * UQ == 256, "one epilogue item per thread");
 
-    int plen[EPQ4];
-#pragma unroll
-    for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min(tid + 256 * q, BR * UQ - 1) / UQ];
+    // sequence lengths: SCALAR loads of the wave's row groups, issued now and
+    // waited for only after the DMA burst is out (a vector load here would
+    // be waited for with vmcnt(0) behind the whole burst: the compiler does
+    // not count LDS-DMA), then picked per lane with selects. Inline asm
+    // because the compiler turns the select chain back into a vector gather.
+    typedef int int8v __attribute__((ext_vector_type(8)));
+    typedef int int16v __attribute__((ext_vector_type(16)));
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int gr0 = (0 * 4 + wv) * 8 + (lane >> 3), gr1 = (1 * 4 + wv) * 8 + (lane >> 3);
+    int8v sl0, sl1;
+    int16v sle;
+    {
+        // byte offsets made explicitly uniform: the pointer must sit in SGPRs
+        const unsigned o0 = __builtin_amdgcn_readfirstlane((b0 + (0 * 4 + wv) * 8) * 4);
+        const unsigned o1 = __builtin_amdgcn_readfirstlane((b0 + (1 * 4 + wv) * 8) * 4);
+        const unsigned oe = __builtin_amdgcn_readfirstlane((b0 + wv * 16) * 4);
+        asm volatile("s_load_dwordx8 %0, %1, %2" : "=&s"(sl0) : "s"(seq_len), "s"(o0));
+        asm volatile("s_load_dwordx8 %0, %1, %2" : "=&s"(sl1) : "s"(seq_len), "s"(o1));
+        asm volatile("s_load_dwordx16 %0, %1, %2" : "=&s"(sle) : "s"(seq_len), "s"(oe));
+    }
 
-    // 1. the operand burst
+    // 1. GEMM operand blocks, k-block-major; 8 wave instructions per block
     const bf16* a_rows = h_in + ((int64_t)dir * B + b0) * H;
-    const bf16* wdir = whT + (int64_t)dir * 4 * H * H;
-    const int lrow = lane / CPR, chunk = (lane % CPR) ^ 0;
+    const bf16* wdir = whT + (int64_t)dir * 4 * H * H + (int64_t)u0 * H;
+    const int c16 = lane & 15;
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int r = (i * 4 + wave) * RPI + lrow;
-        const int c = (lane % CPR) ^ (r & 15);
-        __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * H + 8 * c),
-                                         (__attribute__((address_space(3))) void*)(sA + (i * 4 + wave) * RPI * ROWB),
+    for (int kc = 0; kc < NCH; ++kc)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int ii = i * 4 + wave, r = 4 * ii + (lane >> 4);     // r < 64: h row; else W^T row r - 64
+            const int n = r - BR;
+            const bf16* src = r < BR ? a_rows + (int64_t)r * H : wdir + (int64_t)((n / HU) * H + (n % HU)) * H;
+            __builtin_amdgcn_global_load_lds((const void*)(src + kc * 128 + 8 * (c16 ^ (r & 15))),
+                                             (__attribute__((address_space(3))) void*)(lds + kc * BLK + 4 * ii * ROWB),
+                                             16, 0, 0);
+        }
+    // 2. epilogue operands: gx [64 rows][4 gates][16 units] bf16 (2 instructions
+    //    per wave), c [64 rows][16] f32 (1 per wave)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(sl0), "+s"(sl1), "+s"(sle));
+    int plen[1], len0 = sl0[0], len1 = sl1[0];
+    plen[0] = sle[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        len0 = (lane >> 3) == k ? sl0[k] : len0;
+        len1 = (lane >> 3) == k ? sl1[k] : len1;
+    }
+#pragma unroll
+    for (int k = 1; k < 16; ++k) plen[0] = (lane >> 2) == k ? sle[k] : plen[0];
+    {
+        const int gate = (lane & 7) >> 1, half = lane & 1;
+        const int t0 = step_time(dir, s, len0), t1 = step_time(dir, s, len1);
+        const bf16* g0 = gx + (((int64_t)t0 * B + b0 + gr0) * 2 + dir) * G4 + gate * H + u0 + half * 8;
+        const bf16* g1 = gx + (((int64_t)t1 * B + b0 + gr1) * 2 + dir) * G4 + gate * H + u0 + half * 8;
+        __builtin_amdgcn_global_load_lds((const void*)g0,
+                                         (__attribute__((address_space(3))) void*)(lds + GX_OFF + (0 * 4 + wave) * 1024),
                                          16, 0, 0);
-        const bf16* brow = wdir + (int64_t)((r / HU) * H + u0 + (r % HU)) * H;
-        __builtin_amdgcn_global_load_lds((const void*)(brow + 8 * c),
-                                         (__attribute__((address_space(3))) void*)(sB + (i * 4 + wave) * RPI * ROWB),
+        __builtin_amdgcn_global_load_lds((const void*)g1,
+                                         (__attribute__((address_space(3))) void*)(lds + GX_OFF + (1 * 4 + wave) * 1024),
+                                         16, 0, 0);
+        const float* cs = c_state + ((int64_t)dir * B + b0 + wave * 16 + (lane >> 2)) * H + u0 + (lane & 3) * 4;
+        __builtin_amdgcn_global_load_lds((const void*)cs,
+                                         (__attribute__((address_space(3))) void*)(lds + C_OFF + wave * 1024),
                                          16, 0, 0);
     }
-    (void)chunk;
     stamp(dbg, 1);
-    // 2. epilogue operands (do not depend on the product)
-    float pg[EPQ4][4][4], pc[EPQ4][4], ph[EPQ4][4];
-#pragma unroll
-    for (int q = 0; q < EPQ4; ++q) {
-        const int idx = tid + 256 * q;
-        const int r = idx / UQ, u = 4 * (idx % UQ), b = b0 + r, uu = u0 + u;
-        const int64_t st = ((int64_t)dir * B + b) * H + uu;
-        ld4(pc[q], c_state + st);
-        ld4(ph[q], h_in + st);
-        const int t = step_time(dir, s, plen[q]);
-        const bf16* g = gx + (((int64_t)t * B + b) * 2 + dir) * G4 + uu;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ld4(pg[q][k], g + k * H);
-    }
-    stamp(dbg, 2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    stamp(dbg, 3);
 
-    // 3. 64 x 64 x H on MFMA, 2 x 2 waves of 32 x 32
+    // 3. 64 x 64 x H on MFMA, 2 x 2 waves of 32 x 32, block by block as they land
     const int wm = wave >> 1, wn = wave & 1, i16 = lane & 15, g = lane >> 4, sw = lane & 15;
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    {
-        const char* ar[2] = {sA + (wm * 32 + i16) * ROWB, sA + (wm * 32 + 16 + i16) * ROWB};
-        const char* br[2] = {sB + (wn * 32 + i16) * ROWB, sB + (wn * 32 + 16 + i16) * ROWB};
-        lds_mma_16x16x32<H / 32, 2, 2>(ar, br, g, sw, acc);
+#pragma unroll
+    for (int kc = 0; kc < NCH; ++kc) {
+        // block kc landed: the blocks after it and the 3 epilogue moves are younger
+        const int younger = 8 * (NCH - 1 - kc) + 3;     // folds under the unrolled loop
+        if (younger == 27) vm_wait<27>();
+        else if (younger == 19) vm_wait<19>();
+        else if (younger == 11) vm_wait<11>();
+        else vm_wait<3>();
+        __builtin_amdgcn_s_barrier();
+        if (kc == 0) stamp(dbg, 2);
+        const char* base = lds + kc * BLK;
+        const char* ar[2] = {base + (wm * 32 + i16) * ROWB, base + (wm * 32 + 16 + i16) * ROWB};
+        const char* br[2] = {base + (BR + wn * 32 + i16) * ROWB, base + (BR + wn * 32 + 16 + i16) * ROWB};
+        lds_mma_16x16x32<4, 2, 2, 2>(ar, br, g, sw, acc);
     }
-    __syncthreads();
-    float* sG = reinterpret_cast<float*>(lds);                      // [BR][NC+1]
+    stamp(dbg, 3);
+    // h_{s-1} of this thread's 4 units, from the A image (before the spill overwrites block 0)
+    const int er = tid / UQ, eu = 4 * (tid % UQ);
+    float pg[1][4][4], pc[1][4], ph[1][4];
+    {
+        const int k = u0 + eu;
+        const char* p = lds + (k / 128) * BLK + er * ROWB + ((((k % 128) / 8) ^ (er & 15)) * 16) + (k % 8) * 2;
+        ld4(ph[0], reinterpret_cast<const bf16*>(p));
+    }
+    vm_wait<0>();
+    __syncthreads();                                      // gx / c tiles in; every wave is done with block 0
+    float* sG = reinterpret_cast<float*>(lds);            // [BR][NC+1]
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -232,11 +278,36 @@ lstm_fwd_step_dma_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ w
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 sG[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * (NC + 1) + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        ld4(pg[0][k], reinterpret_cast<const bf16*>(lds + GX_OFF + er * 128 + k * 32 + eu * 2));
+    ld4(pc[0], reinterpret_cast<const float*>(lds + C_OFF + er * 64 + eu * 4));
     __syncthreads();
     stamp(dbg, 4);
     lstm_fwd_epilogue<bf16, BR, HU>(sG, plen, pg, pc, ph, s, B, H, b0, u0, dir, c_state, h_out, out, hprev_t,
                                     cprev_t, acts_t);
     stamp(dbg, 5);
+}
+
+// Sequence lengths of the 16 rows b0 + 16 w .. +15 of wave w by ONE scalar
+// load (inline asm: issued early and waited for late, after the LDS-DMA burst
+// is out -- a vector load would be waited for with vmcnt(0), i.e. behind
+// every DMA issued before its use, and the compiler folds a select chain on
+// plain loads back into a vector gather), then picked per lane.
+typedef int int16v_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int16v_t wave_rows_len16_issue(const int* __restrict__ seq_len, int b0, int wave) {
+    const unsigned off = __builtin_amdgcn_readfirstlane((b0 + wave * 16) * 4);
+    int16v_t v;
+    asm volatile("s_load_dwordx16 %0, %1, %2" : "=&s"(v) : "s"(seq_len), "s"(off));
+    return v;
+}
+// row 16 w + (lane >> 2): the epilogue row when 4 threads share a row
+__device__ __forceinline__ int wave_rows_len16_pick(int16v_t v, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v));
+    int len = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) len = (lane >> 2) == k ? v[k] : len;
+    return len;
 }
 
 // -------------------------------------------------------------- backward
@@ -256,6 +327,14 @@ struct LstmBwdOps {
                                          int dir) {
 #pragma unroll
         for (int q = 0; q < EPQ4; ++q) plen[q] = seq_len[b0 + min((int)threadIdx.x + 256 * q, BR * UQ - 1) / UQ];
+        load_operands(dc_state, acts_t, cprev_t, dout, s, B, H, b0, u0, dir);
+    }
+
+    // the same with plen[] already set
+    template <typename CT>
+    __device__ __forceinline__ void load_operands(const float* __restrict__ dc_state, const CT* __restrict__ acts_t,
+                                                  const float* __restrict__ cprev_t, const CT* __restrict__ dout,
+                                                  int s, int B, int H, int b0, int u0, int dir) {
         const int G4 = 4 * H;
 #pragma unroll
         for (int q = 0; q < EPQ4; ++q) {
@@ -344,11 +423,18 @@ lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT
     ops.epilogue(reinterpret_cast<const float*>(lds), s, B, H, b0, u0, dir, dc_state, dg_out, dG_t);
 }
 
-// bf16 backward step with the operands streamed by LDS-DMA: the 64 dG rows
-// and the 16 W_h rows (K = 4H) pass through a two-buffer ring of 512-deep
-// k-chunks (80 KB each, 1 KB per row, 16-B chunks XOR-swizzled by row), so
-// chunk c+1 is in flight while chunk c is on MFMA. Wave w owns batch rows
-// 16w..16w+15 of the 64 x 16 product.
+// bf16 backward step with every operand moved by LDS-DMA. The 64 dG rows and
+// the 16 W_h rows (K = 4H) stream through a three-buffer ring of 256-deep
+// k-chunks (40 KB each, 512 B per row, 16-B chunks XOR-swizzled by row & 15),
+// two chunks in flight while one is on MFMA; the epilogue operands (dc,
+// c_prev, gate activations and dout of the step's time rows) ride the same
+// queue behind the first two chunks into a region of their own. Counted
+// vmcnt waits + raw s_barrier per chunk. Wave w owns batch rows 16w..16w+15
+// of the 64 x 16 product and moves the epilogue operands of those rows.
+constexpr int LSTM_BWD_KCH = 256, LSTM_BWD_RING = 3;
+constexpr int LSTM_BWD_BUFB = (64 + 16) * 2 * LSTM_BWD_KCH;
+constexpr int LSTM_BWD_EPI = 64 * 128 + 64 * 64 + 64 * 64 + 64 * 32;   // acts | c_prev | dc | dout
+constexpr int LSTM_BWD_DMA_LDS = LSTM_BWD_RING * LSTM_BWD_BUFB + LSTM_BWD_EPI;
 template <int H_>
 __global__ void __launch_bounds__(256)
 lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ dg_in, bf16* __restrict__ dg_out,
@@ -356,63 +442,103 @@ lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ d
                          const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
                          const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t) {
     constexpr int BR = 64, HU = 16, H = H_, G4 = 4 * H;
-    constexpr int KCH = 512, NCH = G4 / KCH, ROWB = 2 * KCH;     // one wave instruction per 1-KB row
-    constexpr int BUFB = (BR + HU) * ROWB, NPS = (BR + HU) / 4;  // DMA instructions per wave per chunk
-    static_assert(G4 % KCH == 0 && NCH >= 2, "H = 256 or 512");
+    constexpr int KCH = LSTM_BWD_KCH, NCH = G4 / KCH, ROWB = 2 * KCH, RING = LSTM_BWD_RING;
+    constexpr int BUFB = LSTM_BWD_BUFB, NPS = (BR + HU) / 2 / 4;  // DMA instructions per wave per chunk (2 rows each)
+    constexpr int EPI = RING * BUFB, A_OFF = EPI, CP_OFF = A_OFF + 64 * 128, DC_OFF = CP_OFF + 64 * 64,
+                  DO_OFF = DC_OFF + 64 * 64, NEPI = 5;            // epilogue DMA instructions per wave
+    static_assert(G4 % KCH == 0 && NCH >= 2 && NPS == 10, "H = 256 or 512");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const StepTile tl = step_tile(H / HU, B / BR);
     const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    typedef __attribute__((address_space(3))) void* lds_p;
 
-    // epilogue operands first: vmcnt retires in order, so the counted waits
-    // below also cover them
-    LstmBwdOps<BR, HU> ops;
-    ops.load(seq_len, dc_state, acts_t, cprev_t, dout, s, B, H, b0, u0, dir);
+    const int16v_t lens = wave_rows_len16_issue(seq_len, b0, wave);   // rows 16w .. 16w+15
 
     const bf16* a_rows = dg_in + ((int64_t)dir * B + b0) * G4;
     const bf16* wdir = wh + ((int64_t)dir * H + u0) * G4;
     auto issue = [&](int c) {
-        char* sA = lds + (c & 1) * BUFB;
-        char* sB = sA + BR * ROWB;
+        char* buf = lds + (c % RING) * BUFB;
 #pragma unroll
-        for (int i = 0; i < BR / 4; ++i) {
-            const int r = i * 4 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(a_rows + (int64_t)r * G4 + c * KCH + 8 * (lane ^ (r & 15))),
-                                             (__attribute__((address_space(3))) void*)(sA + r * ROWB), 16, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < HU / 4; ++i) {
-            const int n = i * 4 + wave;
-            __builtin_amdgcn_global_load_lds((const void*)(wdir + (int64_t)n * G4 + c * KCH + 8 * (lane ^ (n & 15))),
-                                             (__attribute__((address_space(3))) void*)(sB + n * ROWB), 16, 0, 0);
+        for (int i = 0; i < NPS; ++i) {
+            const int ii = i * 4 + wave, r = 2 * ii + (lane >> 5);       // r < 64: dG row; else W_h row r - 64
+            const bf16* src = r < BR ? a_rows + (int64_t)r * G4 : wdir + (int64_t)(r - BR) * G4;
+            __builtin_amdgcn_global_load_lds((const void*)(src + c * KCH + 8 * ((lane & 31) ^ (r & 15))),
+                                             (lds_p)(buf + 2 * ii * ROWB), 16, 0, 0);
         }
     };
     issue(0);
     issue(1);
+    // epilogue operands of rows 16w.. (time row per sequence length)
+    int plen;
+    {
+        int16v_t v = lens;
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v));
+        auto pick = [&](int k) {
+            int x = v[0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) x = k == q ? v[q] : x;
+            return x;
+        };
+        const int rb = b0 + wave * 16;
+        // gate activations: 2 x 8 rows x 4 gates x 32 B
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int rr = i * 8 + (lane >> 3), t = step_time(dir, s, pick(rr));
+            const bf16* src = acts_t + (((int64_t)t * B + rb + rr) * 2 + dir) * G4 + ((lane & 7) >> 1) * H + u0 +
+                              (lane & 1) * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_p)(lds + A_OFF + (wave * 16 + i * 8) * 128), 16,
+                                             0, 0);
+        }
+        {   // c_prev (f32, 64 B per row) and the dc state
+            const int rr = lane >> 2, t = step_time(dir, s, pick(rr));
+            const float* src = cprev_t + (((int64_t)t * B + rb + rr) * 2 + dir) * H + u0 + (lane & 3) * 4;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_p)(lds + CP_OFF + wave * 16 * 64), 16, 0, 0);
+            const float* dsrc = dc_state + ((int64_t)dir * B + rb + rr) * H + u0 + (lane & 3) * 4;
+            __builtin_amdgcn_global_load_lds((const void*)dsrc, (lds_p)(lds + DC_OFF + wave * 16 * 64), 16, 0, 0);
+        }
+        {   // dout (bf16, 32 B per row): half a wave
+            const int rr = (lane & 31) >> 1, t = step_time(dir, s, pick(rr));
+            const bf16* src = dout + ((int64_t)t * B + rb + rr) * 2 * H + dir * H + u0 + (lane & 1) * 8;
+            if (lane < 32)
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_p)(lds + DO_OFF + wave * 16 * 32), 16, 0, 0);
+        }
+        plen = pick(lane >> 2);                         // this thread's epilogue row 16w + lane/4
+    }
 
     const int i16 = lane & 15, g = lane >> 4, sw = lane & 15;
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) vm_wait<NPS>();
+        // chunk c landed; younger: chunk c+1 (if any) and, for c <= 1, the epilogue moves
+        const int younger = (c + 1 < NCH ? NPS : 0) + (c <= 1 ? NEPI : 0);
+        if (younger == NPS + NEPI) vm_wait<NPS + NEPI>();
+        else if (younger == NPS) vm_wait<NPS>();
+        else if (younger == NEPI) vm_wait<NEPI>();
         else vm_wait<0>();
-        __builtin_amdgcn_s_barrier();                       // everyone's chunk c has landed
-        const char* sA = lds + (c & 1) * BUFB + (wave * 16 + i16) * ROWB;
-        const char* sB = lds + (c & 1) * BUFB + BR * ROWB + i16 * ROWB;
-        {
-            const char* ar[1] = {sA};
-            const char* br[1] = {sB};
-            floatx4 (&acc11)[1][1] = reinterpret_cast<floatx4 (&)[1][1]>(acc);
-            lds_mma_16x16x32<KCH / 32, 1, 1, 4>(ar, br, g, sw, acc11);
-        }
-        if (c + 2 < NCH) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();                   // buffer c & 1 is free again
-            issue(c + 2);
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                   // chunk c in for every wave; buffer (c+2)%3 is free
+        if (c + 2 < NCH) issue(c + 2);
+        const char* buf = lds + (c % RING) * BUFB;
+        const char* ar[1] = {buf + (wave * 16 + i16) * ROWB};
+        const char* br[1] = {buf + (BR + i16) * ROWB};
+        floatx4 (&acc11)[1][1] = reinterpret_cast<floatx4 (&)[1][1]>(acc);
+        lds_mma_16x16x32<KCH / 32, 1, 1, 4>(ar, br, g, sw, acc11);
     }
-    __syncthreads();
-    float* sG = reinterpret_cast<float*>(lds);              // [BR][HU + 1]
+    vm_wait<0>();
+    __syncthreads();                                    // epilogue operands in; every wave done with the ring
+    LstmBwdOps<BR, HU> ops;
+    static_assert(LstmBwdOps<BR, HU>::EPQ4 == 1 && LstmBwdOps<BR, HU>::UQ == 4, "one item per thread");
+    {
+        const int r = threadIdx.x / 4, u = 4 * (threadIdx.x % 4);
+        ops.plen[0] = plen;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ld4(ops.pa[0][k], reinterpret_cast<const bf16*>(lds + A_OFF + r * 128 + k * 32 + u * 2));
+        ld4(ops.pcp[0], reinterpret_cast<const float*>(lds + CP_OFF + r * 64 + u * 4));
+        ld4(ops.pdc[0], reinterpret_cast<const float*>(lds + DC_OFF + r * 64 + u * 4));
+        ld4(ops.pdo[0], reinterpret_cast<const bf16*>(lds + DO_OFF + r * 32 + u * 2));
+    }
+    float* sG = reinterpret_cast<float*>(lds);              // [BR][HU + 1], in ring buffer 0
 #pragma unroll
     for (int r = 0; r < 4; ++r) sG[(wave * 16 + g * 4 + r) * (HU + 1) + i16] = acc[r];
     __syncthreads();
@@ -424,6 +550,8 @@ long long* g_lstm_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
 
 extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return OCRK_OK; }
 
+// GEMM blocks (2 x 64 rows x 2H bytes) + gx tile (8 KB) + c tile (4 KB)
+static constexpr int lstm_fwd_dma_lds(int H) { return 2 * 64 * 2 * H + 64 * 64 * 2 + 64 * 16 * 4; }
 static bool lstm_dma_enabled() {
     static int on = -1;
     if (on < 0) {
@@ -431,16 +559,15 @@ static bool lstm_dma_enabled() {
         on = (e && e[0] == '0') ? 0 : 1;
         if (on) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<512>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 512);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lstm_fwd_dma_lds(512));
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<256>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 256 * 256);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lstm_fwd_dma_lds(256));
         }
     }
     return on == 1;
 }
 
-// Backward ring: 2 x 80 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it.
-constexpr int LSTM_BWD_DMA_LDS = 2 * (64 + 16) * 1024;
+// Backward ring + epilogue operands: 138 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it.
 static bool lstm_bwd_dma_enabled() {
     static int on = -1;
     if (on < 0) {
@@ -472,9 +599,9 @@ extern "C" int ocrk_lstm_fwd_step(const void* gx, const void* whT, const void* h
         dim3 grid(H / 16 * (B / 64) * 2);
         if (lstm_dma_enabled() && (H == 512 || H == 256)) {
             if (H == 512)
-                lstm_fwd_step_dma_kernel<512><<<grid, 256, 256 * 512, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
+                lstm_fwd_step_dma_kernel<512><<<grid, 256, lstm_fwd_dma_lds(512), st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
             else
-                lstm_fwd_step_dma_kernel<256><<<grid, 256, 256 * 256, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
+                lstm_fwd_step_dma_kernel<256><<<grid, 256, lstm_fwd_dma_lds(256), st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);
             return ocrk::launch_status("ocrk_lstm_fwd_step");
         }
         lstm_fwd_step_kernel<FWD_BF16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, (const bf16*)h_in, (bf16*)h_out, c_state, seq_len, s, T, B, H, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, g_lstm_dbg);

@@ -178,7 +178,9 @@ __device__ __forceinline__ int step_time(int dir, int s, int len) {
 // to itself the scheduler sinks every read next to its MFMA and waits on
 // it; a sched_barrier per k-step pins the order), and the chunk offsets
 // precomputed so each read is one ds_read_b128 with an immediate offset.
-template <int NKS, int TM, int TN, int PF = 2>
+// KSTRIDE: bytes between consecutive 128-element k blocks of a row (256 for
+// row-contiguous images, the block size for k-block-major images).
+template <int NKS, int TM, int TN, int PF = 2, int KSTRIDE = 256>
 __device__ __forceinline__ void lds_mma_16x16x32(const char* const (&arow)[TM], const char* const (&brow)[TN],
                                                  int g, int sw, floatx4 (&acc)[TM][TN]) {
     const int gs = g ^ sw;                              // (4 ks + g) ^ sw == 4 ks ^ (g ^ sw)
@@ -196,9 +198,9 @@ __device__ __forceinline__ void lds_mma_16x16x32(const char* const (&arow)[TM], 
     bf16x8 fa[R][TM], fb[R][TN];
     auto load = [&](int ks, int slot) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[slot][i] = *reinterpret_cast<const bf16x8*>(pa[i][ks & 3] + (ks >> 2) * 256);
+        for (int i = 0; i < TM; ++i) fa[slot][i] = *reinterpret_cast<const bf16x8*>(pa[i][ks & 3] + (ks >> 2) * KSTRIDE);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[slot][j] = *reinterpret_cast<const bf16x8*>(pb[j][ks & 3] + (ks >> 2) * 256);
+        for (int j = 0; j < TN; ++j) fb[slot][j] = *reinterpret_cast<const bf16x8*>(pb[j][ks & 3] + (ks >> 2) * KSTRIDE);
     };
 #pragma unroll
     for (int ks = 0; ks < PF && ks < NKS; ++ks) load(ks, ks);
