@@ -41,6 +41,26 @@ struct GemmParams {
     int convH, convW, convC;       // im2col source geometry (NHWC) for the A_IM2COL* modes
 };
 
+// XCD-aware tile order for a 1-D grid of 8 * ceil(tm * tn / 8) workgroups.
+// Dispatch deals consecutive workgroup ids round-robin to the 8 XCDs (each
+// with its own L2); this gives XCD x the contiguous tile range
+// [x * per, (x + 1) * per) of a grouped order (GM m-tiles x all n-tiles, m
+// fastest), so the ~32 tiles an XCD runs at once share A rows and B columns
+// in its L2 (and conv tiles share their im2col halo rows) instead of every
+// XCD fetching every operand block from beyond L2. Speed only: any order is
+// correct. valid = false for the padding workgroups past tm * tn.
+struct TileIdx { int bm, bn; bool valid; };
+__device__ __forceinline__ TileIdx xcd_tile(int tm, int tn) {
+    const int nT = tm * tn, per = (nT + 7) >> 3;
+    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (t >= nT) return {0, 0, false};
+    constexpr int GM = 4;
+    const int gsz = GM * tn, grp = t / gsz, first = grp * GM;
+    const int gm = min(GM, tm - first), w = t - grp * gsz;
+    return {first + w % gm, w / gm, true};
+}
+__host__ __forceinline__ unsigned xcd_grid(int tm, int tn) { return 8u * (unsigned)((tm * tn + 7) / 8); }
+
 // Launch C = A.B with the given operand modes. dtype: OCRK_F32 / OCRK_BF16
 // (type of A and B). Picks the tile shape from M, N.
 int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
@@ -52,6 +72,10 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
 // (gemm_nt.hip). Returns -1 when it does not cover the call (the caller then
 // uses the generic engine), else a status. OCRK_GEMM_NT=0 disables it.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+
+// Plain A_ROWK x B_NK bf16 GEMMs with a bf16 C and at most a bias epilogue
+// on hipBLASLt (blaslt.hip). Returns -1 when not covered. OCRK_BLASLT=0 disables it.
+int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
 // The same pipeline for the k-major modes A_COLK / A_IM2COL_T x B_KN (conv
 // weight gradients, recurrent / logits weight gradients), gemm_tn.hip.

@@ -59,7 +59,9 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const TileIdx tix = xcd_tile((p.M + BM - 1) / BM, (p.N + BN - 1) / BN);
+    if (!tix.valid) return;
+    const int m0 = tix.bm * BM, n0 = tix.bn * BN;
     const int zb = blockIdx.z / p.splits, zs = blockIdx.z - zb * p.splits;
     const bf16* A = reinterpret_cast<const bf16*>(p.A) + zb * p.strideA;
     const bf16* B = reinterpret_cast<const bf16*>(p.B) + zb * p.strideB;
@@ -288,7 +290,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
                 float m2 = 0.f;
 #pragma unroll
                 for (int q = 0; q < WAVES_M; ++q) m2 += s_red[q * BN + c];
-                float* st = p.stats + (int64_t)blockIdx.x * 2 * p.N;
+                float* st = p.stats + (int64_t)tix.bm * 2 * p.N;
                 st[n0 + c] = tsum[j];
                 st[p.N + n0 + c] = m2;
             }
@@ -308,7 +310,7 @@ int launch_nt(const GemmParams& p, hipStream_t stream) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
         configured = true;
     }
-    dim3 grid((unsigned)cdiv(p.M, BM), (unsigned)cdiv(p.N, BN), (unsigned)(p.batch * p.splits));
+    dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
     gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");
 }
@@ -320,6 +322,7 @@ int launch_nt(const GemmParams& p, hipStream_t stream) {
 //   4: 256 x 128 x 32 / 4 ->  96 KB -> 1     5: 128 x 128 x 32 / 4 -> 64 KB -> 2
 //   6: 256 x 256 x 64 / 2, 8 waves -> 128 KB -> 1 (2 waves per SIMD)
 //   7: 256 x 128 x 64 / 2, 8 waves ->  96 KB -> 1   8: 256 x 256 x 32 / 3, 8 waves -> 96 KB
+//   9: 256 x 256 x 32 / 4, 8 waves -> 128 KB       10: 256 x 128 x 32 / 4, 8 waves -> 64 KB -> 2
 int nt_cfg() {
     static int c = -2;
     if (c == -2) {
@@ -341,6 +344,8 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
         case 6: return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
         case 7: return launch_nt<256, 128, 64, 2, 4, AM, 8>(p, s);
         case 8: return launch_nt<256, 256, 32, 3, 2, AM, 8>(p, s);
+        case 9: return launch_nt<256, 256, 32, 4, 2, AM, 8>(p, s);
+        case 10: return launch_nt<256, 128, 32, 4, 4, AM, 8>(p, s);
         default: break;
     }
     // measured on MI355X (tools/bench_gemm.py): narrow N -> BK=32, 3 stages;

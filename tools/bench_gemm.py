@@ -30,6 +30,7 @@ def timed(fn, reps=10):
 
 
 def main():
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     torch.manual_seed(0)
     dev = torch.device("cuda")
     bf = torch.bfloat16
@@ -37,12 +38,14 @@ def main():
     for (M, N, Kd, tag) in [(32000, 4096, 256, "proj L1"), (32000, 4096, 1024, "proj L2"),
                             (32000, 1024, 4096, "dx L2"), (32000, 256, 4096, "dx L1"),
                             (32000, 1024, 96, "logits dx")]:
+        if only and only not in tag:
+            continue
         a = torch.randn(M, Kd, device=dev).to(bf)
         w = torch.randn(N, Kd, device=dev).to(bf) * 0.05
         bias = torch.randn(N, device=dev)
         ms, out = timed(lambda: K.gemm(a, w, trans_b=True, bias=bias, out_dtype=bf))
         rows.append((tag, ms, 2.0 * M * N * Kd, float(out.float().abs().sum())))
-    for (H, W, Ci, Co) in CONV:
+    for (H, W, Ci, Co) in ([] if only else CONV):
         x = torch.randn(B, H, W, Ci, device=dev).to(bf)
         w_nk = (torch.randn(Co, 9 * Ci, device=dev) * 0.05).to(bf)
         bias = torch.zeros(Co, device=dev)
@@ -53,7 +56,7 @@ def main():
         w_bwd = (torch.randn(Ci, 9 * Co, device=dev) * 0.05).to(bf)
         ms, out = timed(lambda: K.conv3x3_bwd_data(dy, w_bwd))
         rows.append((f"conv bwd-data {Co}->{Ci} {H}x{W}", ms, fl, float(out.float().abs().sum())))
-    for (H, W, Ci, Co) in CONV:
+    for (H, W, Ci, Co) in ([] if only else CONV):
         x = torch.randn(B, H, W, Ci, device=dev).to(bf)
         dy = torch.randn(B, H, W, Co, device=dev).to(bf)
         dw = torch.zeros(9 * Ci, Co, device=dev)
@@ -66,6 +69,8 @@ def main():
                      float(out.abs().sum())))
     R = 32000
     for (n_in, tag) in [(1024, "LSTM dW_x L2"), (512, "LSTM dW_h"), (256, "LSTM dW_x L1")]:
+        if only and only not in tag:
+            continue
         x = torch.randn(R, n_in, device=dev).to(bf)
         dG = torch.randn(R, 4096, device=dev).to(bf)
         gk = torch.zeros(n_in, 2048, device=dev)
