@@ -50,7 +50,8 @@ SIGNATURES = {
     "ocrk_conv1_bwd_weight": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv_stats_tiles": [_i64],
     "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],
-    "ocrk_conv3x3_bwd_data": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _i32, _p],
+    "ocrk_conv3x3_bwd_data_workspace_size": [_i32, _i32, _i32, _i32],
+    "ocrk_conv3x3_bwd_data": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv3x3_wgrad_workspace_size": [_i32, _i32, _i32, _i32, _i32],
     "ocrk_conv3x3_bwd_weight": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_bn_finalize": [_p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p],

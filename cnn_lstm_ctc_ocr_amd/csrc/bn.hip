@@ -14,6 +14,10 @@
 // the window), applies the ReLU mask, and a deterministic two-pass
 // (partials -> ordered sum -> apply) BN backward.
 #include "common.h"
+#include "reduce.h"
+
+using ocrk::slab_sum;
+using ocrk::SLAB_P;
 
 // --------------------------------------------------------------- finalize
 // One block per channel: Chan-merge the per-tile (sum, M2) partials.
@@ -370,48 +374,6 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
     }
 }
 
-// Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
-// accumulation, in two stages so the ~2k slab rows are spread over many
-// workgroups: stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
-constexpr int SLAB_P = 64;
-
-__global__ void __launch_bounds__(256)
-slab_sum_stage1(const float* __restrict__ slab, int nslab, int NC, double* __restrict__ part) {
-    __shared__ double red[4][64];
-    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
-    const int rows = (nslab + SLAB_P - 1) / SLAB_P;
-    const int r0 = blockIdx.y * rows, r1 = min(nslab, r0 + rows);
-    double s = 0.0;
-    if (c < NC)
-        for (int i = r0 + q; i < r1; i += 4) s += slab[(int64_t)i * NC + c];
-    red[q][cl] = s;
-    __syncthreads();
-    if (q == 0 && c < NC) part[(int64_t)blockIdx.y * NC + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-}
-
-// res[o] = sum; then (accumulate ? += : =) into dst_lo[o] for o < split, dst_hi[o - split] above
-__global__ void __launch_bounds__(64)
-slab_sum_stage2(const double* __restrict__ part, int NC, float* __restrict__ res, float* __restrict__ dst_lo,
-                float* __restrict__ dst_hi, int split, int accumulate) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= NC) return;
-    double t = 0.0;
-    for (int y = 0; y < SLAB_P; ++y) t += part[(int64_t)y * NC + c];
-    const float v = (float)t;
-    if (res) res[c] = v;
-    float* d = c < split ? (dst_lo ? dst_lo + c : nullptr) : (dst_hi ? dst_hi + (c - split) : nullptr);
-    if (d) *d = accumulate ? *d + v : v;
-}
-
-static int slab_sum(const float* slab, int nslab, int NC, double* part, float* res, float* dst_lo,
-                    float* dst_hi, int split, int accumulate, hipStream_t s) {
-    slab_sum_stage1<<<dim3((NC + 63) / 64, SLAB_P), 256, 0, s>>>(slab, nslab, NC, part);
-    int st = ocrk::launch_status("bn slab sum 1");
-    if (st) return st;
-    slab_sum_stage2<<<(NC + 63) / 64, 64, 0, s>>>(part, NC, res, dst_lo, dst_hi, split, accumulate);
-    return ocrk::launch_status("bn slab sum 2");
-}
 
 // pass 2 (streaming): dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n),
 // plus per-block partial column sums of dz -- the gradient of the conv bias

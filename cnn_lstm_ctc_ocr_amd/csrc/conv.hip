@@ -14,6 +14,7 @@
 //           weight = split-K GEMM im2col(x)^T . dy; bias = column sums of dy.
 #include "common.h"
 #include "gemm.h"
+#include "reduce.h"
 
 // ----------------------------------------------------------------- conv1 fwd
 template <typename TIn, typename TOut, int COUT>
@@ -217,8 +218,20 @@ extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, con
     return ocrk::gemm(p, ocrk::A_IM2COL, ocrk::B_NK, dtype, ocrk::as_stream(stream));
 }
 
+// Optional fused bias gradient of the producing (odd) conv: the GEMM's
+// per-128-row-tile column statistics are taken after the ReLU mask, so their
+// sums are the column sums of dx; slab_sum reduces them in a fixed order.
+// workspace: stats [tiles][2 cin] f32 | part [SLAB_P][cin] double
+static int64_t bwd_data_tiles(int B, int H, int W) { return ocrk::cdiv((int64_t)B * H * W, 128); }
+
+extern "C" size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin) {
+    return ((size_t)bwd_data_tiles(B, H, W) * 2 * cin * sizeof(float) + 7) / 8 * 8 +
+           (size_t)ocrk::SLAB_P * cin * sizeof(double);
+}
+
 extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd,
-                                     int cin, void* dx, const void* relu_mask, int dtype, void* stream) {
+                                     int cin, void* dx, const void* relu_mask, float* dbias, int accumulate,
+                                     void* ws, size_t ws_bytes, int dtype, void* stream) {
     ocrk::GemmParams p = {};
     p.M = B * H * W; p.N = cin; p.K = 9 * cout; p.batch = 1;
     p.A = dy; p.B = w_bwd; p.ldb = 9 * cout;
@@ -226,7 +239,17 @@ extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int co
     p.mask = relu_mask; p.ldmask = cin; p.alpha = 1.f;
     p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
     p.convH = H; p.convW = W; p.convC = cout;
-    return ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, ocrk::as_stream(stream));
+    if (dbias) {
+        OCRK_REQUIRE(ws && ws_bytes >= ocrk_conv3x3_bwd_data_workspace_size(B, H, W, cin),
+                     "ocrk_conv3x3_bwd_data: workspace too small for the bias gradient");
+        p.stats = (float*)ws;
+    }
+    hipStream_t s = ocrk::as_stream(stream);
+    int st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
+    if (st || !dbias) return st;
+    const int tiles = (int)bwd_data_tiles(B, H, W);
+    double* part = (double*)((char*)ws + ((size_t)tiles * 2 * cin * sizeof(float) + 7) / 8 * 8);
+    return ocrk::slab_sum((const float*)ws, tiles, cin, part, nullptr, dbias, nullptr, cin, accumulate, s, 2 * cin);
 }
 
 static int wgrad_splits(int64_t M, int cin, int cout) {

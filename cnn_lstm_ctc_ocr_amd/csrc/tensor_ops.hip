@@ -3,6 +3,7 @@
 // [Cin][kh][kw][Cout] for backward-data), deterministic column sums (bias
 // gradients) and the ReLU-mask product of the logits layer backward.
 #include "common.h"
+#include "reduce.h"
 
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
@@ -24,10 +25,59 @@ __global__ void __launch_bounds__(256) permute3_kernel(const TI* __restrict__ in
     }
 }
 
+namespace ocrk {
+namespace {
+
+// Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
+// accumulation, in two stages so the ~2k slab rows are spread over many
+// workgroups: stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
+
+__global__ void __launch_bounds__(256)
+slab_sum_stage1(const float* __restrict__ slab, int nslab, int NC, int ld, double* __restrict__ part) {
+    __shared__ double red[4][64];
+    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const int rows = (nslab + SLAB_P - 1) / SLAB_P;
+    const int r0 = blockIdx.y * rows, r1 = min(nslab, r0 + rows);
+    double s = 0.0;
+    if (c < NC)
+        for (int i = r0 + q; i < r1; i += 4) s += slab[(int64_t)i * ld + c];
+    red[q][cl] = s;
+    __syncthreads();
+    if (q == 0 && c < NC) part[(int64_t)blockIdx.y * NC + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+// res[o] = sum; then (accumulate ? += : =) into dst_lo[o] for o < split, dst_hi[o - split] above
+__global__ void __launch_bounds__(64)
+slab_sum_stage2(const double* __restrict__ part, int NC, float* __restrict__ res, float* __restrict__ dst_lo,
+                float* __restrict__ dst_hi, int split, int accumulate) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= NC) return;
+    double t = 0.0;
+    for (int y = 0; y < SLAB_P; ++y) t += part[(int64_t)y * NC + c];
+    const float v = (float)t;
+    if (res) res[c] = v;
+    float* d = c < split ? (dst_lo ? dst_lo + c : nullptr) : (dst_hi ? dst_hi + (c - split) : nullptr);
+    if (d) *d = accumulate ? *d + v : v;
+}
+
+}  // namespace
+
+int slab_sum(const float* slab, int nslab, int NC, double* part, float* res, float* dst_lo, float* dst_hi,
+             int split, int accumulate, hipStream_t s, int ld) {
+    slab_sum_stage1<<<dim3((NC + 63) / 64, SLAB_P), 256, 0, s>>>(slab, nslab, NC, ld > 0 ? ld : NC, part);
+    int st = ocrk::launch_status("slab sum 1");
+    if (st) return st;
+    slab_sum_stage2<<<(NC + 63) / 64, 64, 0, s>>>(part, NC, res, dst_lo, dst_hi, split, accumulate);
+    return ocrk::launch_status("slab sum 2");
+}
+
+}  // namespace ocrk
+
 // column sums of [M][N]: block (x, y) reduces column block x (TPR groups of 8
 // columns, one 16-B vector per thread per row; a wave reads 64 consecutive
 // chunks of a row when N >= 512) over row range y, combines its threads in a
-// fixed order and writes slab row y; reduce_slabs then sums the slabs in a
+// fixed order and writes slab row y; slab_sum then sums the slabs in a
 // fixed order (deterministic for a given shape).
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict__ in, int64_t M, int N,
@@ -57,25 +107,6 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict
         float sum = 0.f;
         for (int q = 0; q < RPP; ++q) sum += red[(q * TPR + gg) * 9 + i];
         if (blockIdx.x * TPR + gg < G) slab[(int64_t)blockIdx.y * N + (blockIdx.x * TPR + gg) * 8 + i] = sum;
-    }
-}
-
-// out[c] (+)= sum_i slab[i][c], 64 columns x 4 slab lanes per block, fixed order.
-__global__ void __launch_bounds__(256) reduce_slabs_kernel(const float* __restrict__ slab, int nslab, int N,
-                                                           float* __restrict__ out, int accumulate) {
-    __shared__ double part[4][64];
-    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
-    double s = 0.0;
-    if (c < N) {
-#pragma unroll 8
-        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * N + c];
-    }
-    part[q][cl] = s;
-    __syncthreads();
-    if (q == 0 && c < N) {
-        double t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
-        out[c] = accumulate ? out[c] + (float)t : (float)t;
     }
 }
 
@@ -117,8 +148,9 @@ static int64_t colsum_blocks(int64_t M, int N) {
     return std::max<int64_t>(1, std::min<int64_t>(want, ocrk::cdiv(M, 64)));
 }
 
+// slab [nb][N] f32 | part [SLAB_P][N] double
 extern "C" size_t ocrk_colsum_workspace_size(int64_t M, int N) {
-    return (size_t)colsum_blocks(M, N) * N * sizeof(float);
+    return ((size_t)colsum_blocks(M, N) * N * sizeof(float) + 7) / 8 * 8 + (size_t)ocrk::SLAB_P * N * sizeof(double);
 }
 
 extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
@@ -135,8 +167,8 @@ extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* o
     else colsum_partial_kernel<float><<<grid, 256, 0, s>>>((const float*)in, M, N, rpb, (float*)ws);
     int st = ocrk::launch_status("ocrk_colsum");
     if (st) return st;
-    reduce_slabs_kernel<<<(N + 63) / 64, 256, 0, s>>>((const float*)ws, (int)nb, N, out, accumulate);
-    return ocrk::launch_status("ocrk_colsum final");
+    double* part = (double*)((char*)ws + ((size_t)nb * N * sizeof(float) + 7) / 8 * 8);
+    return ocrk::slab_sum((const float*)ws, (int)nb, N, part, nullptr, out, nullptr, N, accumulate, s);
 }
 
 extern "C" int ocrk_relu_mask(const float* dy, const float* y, int64_t n, float scale, void* out, int out_dtype,

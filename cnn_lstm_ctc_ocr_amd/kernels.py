@@ -97,13 +97,19 @@ def conv3x3_fwd(x, w_nk, bias, relu, stats=None, y_dtype=None):
     return y
 
 
-def conv3x3_bwd_data(dy, w_bwd, relu_mask=None):
-    _chk(dy, w_bwd, relu_mask)
+def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True):
+    """dx = conv3x3 backward-data (ReLU mask of the producer fused); if dbias
+    is given, dbias (+)= column sums of dx (the producer's bias gradient)."""
+    _chk(dy, w_bwd, relu_mask, dbias)
     B, H, W, Cout = dy.shape
     Cin = w_bwd.shape[0]
     dx = torch.empty(B, H, W, Cin, dtype=dy.dtype, device=dy.device)
-    call("ocrk_conv3x3_bwd_data", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_mask),
-         dtype_code(dy.dtype), _stream(dy))
+    nb, ws = 0, None
+    if dbias is not None:
+        nb = _lib.lib().ocrk_conv3x3_bwd_data_workspace_size(B, H, W, Cin)
+        ws = _ws(nb, dy.device)
+    call("ocrk_conv3x3_bwd_data", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_mask), ptr(dbias),
+         int(accumulate), ptr(ws), nb, dtype_code(dy.dtype), _stream(dy))
     return dx
 
 

@@ -108,15 +108,14 @@ class _ConvBlock(torch.autograd.Function):
         B, H, W, C = dz.shape
         K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
-        dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd)     # ReLU of conv_{2k-1} fused
+        # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
+        dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None)
         dx = None
         if k == 1:
             K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
             store.join()                                   # side-stream weight gradients are in
         else:
-            Bo, Ho, Wo, Co = dy_odd.shape
             K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
-            K.colsum(dy_odd, Bo * Ho * Wo, Co, G[po + "/bias"])
             if ctx.needs_input_grad[0]:
                 _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)

@@ -112,9 +112,14 @@ int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_
                      int cout, void* y, int y_dtype, int relu, float* stats, int dtype, void* stream);
 /* dx [B,H,W,cin] = conv3x3 backward-data of dy [B,H,W,cout] with w_bwd
  * [cin][3][3][cout]; if relu_mask != NULL, dx *= (relu_mask > 0) (the ReLU of
- * the layer that produced x). */
+ * the layer that produced x). If dbias != NULL, dbias [cin] f32 (+)= the
+ * column sums of dx (the bias gradient of that layer, conv_layer bias
+ * model.py:97-104), from the GEMM's per-tile column statistics; needs ws of
+ * ocrk_conv3x3_bwd_data_workspace_size bytes (else ws may be NULL). */
+size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin);
 int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
-                          void* dx, const void* relu_mask, int dtype, void* stream);
+                          void* dx, const void* relu_mask, float* dbias, int accumulate, void* ws,
+                          size_t ws_bytes, int dtype, void* stream);
 /* dw f32 HWIO [3][3][cin][cout] (+)= im2col(x)^T . dy (split-K). */
 size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin, int cout);
 int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, int cin, int cout,

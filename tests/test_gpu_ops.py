@@ -94,8 +94,12 @@ def test_conv3x3_fwd_bwd(cuda, cin, cout, relu):
     dy = rng.standard_normal(z.shape).astype(np.float32)
     dx_ref, dw_ref, _ = G.conv2d_bwd(x, w, dy, "same")
     mask = rng.standard_normal(x.shape).astype(np.float32)
-    dx = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd, relu_mask=_t(mask, cuda))
+    dbias = torch.full((cin,), 0.25, device=cuda)
+    dx = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd, relu_mask=_t(mask, cuda), dbias=dbias, accumulate=True)
     np.testing.assert_allclose(dx.cpu().numpy(), dx_ref * (mask > 0), rtol=1e-4, atol=1e-4)
+    # fused bias gradient of the producing layer = column sums of the masked dx
+    np.testing.assert_allclose(dbias.cpu().numpy(), 0.25 + (dx_ref * (mask > 0)).reshape(-1, cin).sum(0),
+                               rtol=1e-4, atol=1e-3)
     dw = torch.zeros(3, 3, cin, cout, device=cuda)
     Kn.conv3x3_bwd_weight(_t(x, cuda), _t(dy, cuda), dw, accumulate=False)
     np.testing.assert_allclose(dw.cpu().numpy(), dw_ref, rtol=1e-4, atol=1e-3)
