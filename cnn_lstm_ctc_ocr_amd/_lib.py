@@ -66,6 +66,9 @@ SIGNATURES = {
     "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_workspace_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_lstm_bwd_persistent_supported": [_i32, _i32],
+    "ocrk_lstm_bwd_persistent_workspace_size": [_i32, _i32],
+    "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_debug_stamps": [_p],
     "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
@@ -82,6 +85,10 @@ SIGNATURES = {
     "ocrk_mul_scalar": [_p, _i64, _p, _p],
     "ocrk_mean": [_p, _i32, _p, _p],
     "ocrk_seq_len": [_p, _i32, _p, _p],
+    "ocrk_timer_create": [_p],
+    "ocrk_timer_record": [_p, _p],
+    "ocrk_timer_elapsed": [_p, _p, _p],
+    "ocrk_timer_destroy": [_p],
 }
 _RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
 _RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspace_size")})
@@ -120,9 +127,32 @@ def lib():
     return _lib
 
 
+class Timer:
+    """A HIP event owned by libocrk (ocrk_timer_*): recorded on torch's current
+    stream; inside a hipGraph capture it becomes an external event node, so it
+    keeps timestamping on every replay."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        call("ocrk_timer_create", ctypes.byref(h))
+        self.h = h
+
+    def record(self):
+        call("ocrk_timer_record", self.h, stream_ptr())
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        call("ocrk_timer_elapsed", self.h, end.h, ctypes.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        if _lib is not None and self.h:
+            _lib.ocrk_timer_destroy(self.h)
+
+
 # Optional launch probes (bench.py): name -> (work_fn(args) or None, records list).
-# A probed entry point is bracketed by HIP events on torch's current stream --
-# the stream every wrapper launches on -- and (start, end, work) is recorded.
+# A probed entry point is bracketed by Timers on torch's current stream -- the
+# stream every wrapper launches on -- and (start, end, work) is recorded.
 PROBES = {}
 
 
@@ -131,8 +161,7 @@ def call(name, *args):
     probe = PROBES.get(name)
     if probe is not None:
         work_fn, records = probe
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0, ev1 = Timer(), Timer()
         ev0.record()
         status = getattr(lib(), name)(*args)
         ev1.record()

@@ -55,6 +55,11 @@ LtState& lt() {
 void* lt_ws(LtState& s, hipStream_t st) {
     auto it = s.ws.find(st);
     if (it != s.ws.end()) return it->second;
+    // a stream's workspace is allocated on its first eager use; a stream being
+    // captured into a hipGraph must not allocate (the caller then falls back
+    // to the in-house engine)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, LT_WS_BYTES) != hipSuccess) p = nullptr;
     s.ws[st] = p;

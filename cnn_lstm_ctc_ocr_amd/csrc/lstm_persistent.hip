@@ -2,51 +2,70 @@
 // (rnn_layer, src/weinman/model_bu.py:167-199; [TF1] LSTMCell i, j, f, o,
 // forget_bias 1; bidirectional_dynamic_rnn with sequence_length).
 //
-// Work split (bf16, B = 256, H = 512): 256 workgroups = 2 directions x B/32
-// batch slices x H/32 unit slices, one per CU, all co-resident. A workgroup
-// owns 32 hidden units (x 4 gates = 128 gate columns) of one direction for 32
-// batch rows. Its W_h^T slice [128 x H] stays in VGPRs for the whole
-// sequence as MFMA B fragments (wave w: units 8w..8w+7, 4 gates = two 16-col
-// tiles, all H/32 k-steps: 128 VGPRs). Per step the workgroup
-//   1. waits until the 16 workgroups of its (direction, batch slice) group
-//      published h_{s-1} (one agent-scope counter per group, polled by one lane),
-//   2. stages h_{s-1}[32 x H] into LDS with write-through (sc1) loads,
-//   3. runs 2 x 2 tiles x H/32 k-steps of v_mfma_f32_16x16x32_bf16 per wave,
-//   4. finishes the gates wave-locally (lane l and l^8 hold the i/j and f/o
-//      halves of the same unit: two shuffles), keeps c in registers,
-//   5. writes h_s as sc1 stores (4-B pairs), the layer output and the saved
-//      tensors for the backward pass, drains, barriers, and one lane adds 1 to
-//      the group counter.
-// Hand-off form: MI355X_MICROARCH.md "Valid forms" row 1 (sc1 payload stores,
-// every storing wave drained before the barrier, one lane's agent atomic add;
-// consumer: sc1 poll, barrier, every payload load sc1). Spins are bounded: on
-// timeout the kernel records an error word and finishes (no hang).
+// Work split (bf16, H = 32 KS): 2 directions x B/32 batch slices = groups, each
+// of H/32 member workgroups (16 at H = 512, B = 256: 256 workgroups, one per
+// CU, all co-resident). A member owns 32 hidden units (x 4 gates = 128 gate
+// columns) of one direction for 32 batch rows; its W_h^T slice [128 x H] stays
+// in VGPRs for the whole sequence as MFMA B fragments (wave w: units
+// 8w..8w+7, 4 gates = two 16-column tiles, all H/32 k-steps: 128 VGPRs) and
+// its cell state c in registers. Per step a member
+//   0. issues the loads of its gx tile (independent of h) first;
+//   1. waits until the 16 members of its group have published h_{s-1}: one
+//      flag word per member (sharded), polled by 16 lanes of wave 0;
+//   2. stages h_{s-1}[32 x H] into LDS with sc1 (L1-bypassing) loads;
+//   3. runs 2 x 2 tiles x H/32 k-steps of v_mfma_f32_16x16x32_bf16 per wave;
+//   4. finishes the gates wave-locally (lanes l and l^8 hold the i/f and j/o
+//      halves of one unit: two shuffles), keeping c in registers;
+//   5. publishes h_s with sc1 stores, drains (vmcnt 0), barriers, and one lane
+//      stores its flag = s + 1 (sc1);
+//   6. only then stores the layer output and the tensors saved for the
+//      backward pass (they drain behind the next step).
+// Hand-off form: MI355X_MICROARCH.md "Valid forms", table row 1 (sc1 payload
+// stores drained by every storing wave before the barrier, one lane's sc1 flag
+// store per workgroup; consumer: sc1 poll of every shard, barrier, every
+// payload load sc1) -- correct under any placement. Placement is used for
+// speed only: the members of a group are the workgroups with equal
+// blockIdx % 8 (dealt to one XCD by the dispatcher), so the group's hand-off
+// traffic and its W_h^T slices stay on one XCD. Spins are bounded: on timeout
+// the kernel records an error word and runs to completion (no hang).
 #include "common.h"
 #include "mfma_util.h"
+#include "recur.h"
 
 using namespace ocrk;
 
 namespace {
 
 constexpr int PBR = 32, PHU = 32;          // batch rows, hidden units per workgroup
+typedef __attribute__((address_space(1))) unsigned gu32;            // hand-off words: global, never flat
+typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr unsigned SPIN_LIMIT = 1u << 22;  // polls (with s_sleep) before giving up
-
-__device__ __forceinline__ int step_time_p(int dir, int s, int len) {
-    return (dir == 0 || s >= len) ? s : len - 1 - s;
-}
-__device__ __forceinline__ float sigf(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float tanhf_(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
 
 __device__ __forceinline__ unsigned short bf16_bits(float x) {
     bf16 b = (bf16)x;
     return __builtin_bit_cast(unsigned short, b);
 }
+__device__ __forceinline__ float bits_f(unsigned short u) {
+    return __uint_as_float((unsigned)u << 16);
+}
 
-// diagnostics (ocrk_lstm_debug_stamps): thread 0 stamps step S_DBG
+// diagnostics (ocrk_lstm_debug_stamps): thread 0 stamps step 64 (slots 0-5) and the top of step 65 (slot 6)
 __device__ __forceinline__ void pstamp(long long* dbg, int s, int i) {
-    if (dbg && threadIdx.x == 0 && s == 64) {
-        dbg[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + i] =
-            __builtin_amdgcn_s_memrealtime();
+    if (dbg && threadIdx.x == 0 && (s == 64 || (s == 65 && i == 0)))
+        dbg[(int64_t)blockIdx.x * 8 + (s == 65 ? 6 : i)] = __builtin_amdgcn_s_memrealtime();
+}
+
+// workgroup -> (group, member): members of a group share blockIdx % 8 when the
+// grid allows it (speed only)
+__device__ __forceinline__ void persistent_role(int ngroups, int nu, int& group, int& member) {
+    const int id = blockIdx.x, grid = ngroups * nu;
+    if (grid % 8 == 0 && (grid / 8) % nu == 0) {
+        const int per = grid / 8, j = id / 8;
+        group = (id % 8) * (per / nu) + j / nu;
+        member = j % nu;
+    } else {
+        group = id / nu;
+        member = id % nu;
     }
 }
 
@@ -60,24 +79,27 @@ __global__ void __launch_bounds__(256, 1)
 lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
                            const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out,
                            bf16* __restrict__ hprev_t, float* __restrict__ cprev_t, bf16* __restrict__ acts_t,
-                           unsigned* __restrict__ cnt, unsigned* __restrict__ err, long long* __restrict__ dbg) {
+                           unsigned* __restrict__ flags, unsigned* __restrict__ err, long long* __restrict__ dbg) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
+    constexpr int NU = H / PHU;                         // members per group
     constexpr int LDH = H + 8;                          // padded LDS row (bf16 elements)
+    static_assert(NU <= 64, "one poll lane per member");
+    constexpr int LDG = 4 * PHU + 4;                    // padded gate row (floats)
     __shared__ __attribute__((aligned(16))) unsigned short sh[PBR * LDH];
-    // per-step output staging (row-contiguous 32-unit pieces)
-    __shared__ __attribute__((aligned(16))) unsigned short so_h[PBR * PHU], so_out[PBR * PHU], so_hp[PBR * PHU];
-    __shared__ __attribute__((aligned(16))) float so_cp[PBR * PHU];
-    __shared__ __attribute__((aligned(16))) unsigned short so_a[PBR * 4 * PHU];
-    __shared__ int s_t[PBR], s_valid[PBR], s_len[PBR];
+    __shared__ __attribute__((aligned(16))) unsigned short sgx[PBR * 4 * PHU];   // [row][gate][unit] bf16
+    __shared__ __attribute__((aligned(16))) float sG[PBR * LDG];                 // [row][gate][unit] f32
+    __shared__ int s_len[PBR];
 
-    const int us = blockIdx.x, bs = blockIdx.y, dir = blockIdx.z;
-    const int nu = gridDim.x;                           // workgroups per group
-    const int u0 = us * PHU, b0 = bs * PBR;
+    int group, member;
+    persistent_role(2 * (B / PBR), NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * PHU, b0 = bs * PBR;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
-    const int my_unit = u0 + 8 * w + (c & 7);           // the unit this lane finishes
-    unsigned* my_cnt = cnt + dir * gridDim.y + bs;
+    const int lu = 8 * w + (c & 7);                     // the unit (within the slice) this lane finishes
+    const int my_unit = u0 + lu;
+    gu32* gflags = (gu32*)(flags) + group * NU;
 
     // ---- resident B fragments: N-tile j holds gates 2j + (c >> 3) of unit my_unit
     bf16x8 bw[2][KS];
@@ -89,21 +111,22 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
         for (int ks = 0; ks < KS; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
     }
 
-    // ---- the 4 (row, unit) pairs this lane finishes: M-tile mt, register r
-    // lanes c < 8 take registers r = 0,1; lanes c >= 8 take r = 2,3
-    const int rbase = (c >= 8) ? 2 : 0;
-    int prow[4], plen[4];
-    float cst[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int mt = p >> 1, r = rbase + (p & 1);
-        prow[p] = b0 + 16 * mt + 4 * g + r;
-        plen[p] = seq_len[prow[p]];
-        cst[p] = 0.f;
-    }
-    float hst[4] = {0.f, 0.f, 0.f, 0.f};
+    // ---- the epilogue item of this thread: row er, units eu..eu+3 (all 4 gates)
+    const int er = tid >> 3, eu = 4 * (tid & 7);
+    const int elen = seq_len[b0 + er];
+    float cst[4] = {0.f, 0.f, 0.f, 0.f}, hst[4] = {0.f, 0.f, 0.f, 0.f};
     if (tid < PBR) s_len[tid] = seq_len[b0 + tid];
-    static_assert(PHU == 32 && PBR == 32, "staging index math assumes 32 x 32 tiles");
+    __syncthreads();
+
+    // gx tile loader: 32 rows x 4 gates x 4 chunks of 8 units = 512 16-B pieces, 2 per thread
+    int gx_lr[2], gx_gate[2], gx_q[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        const int id = tid + 256 * v;
+        gx_lr[v] = id >> 4;
+        gx_gate[v] = (id >> 2) & 3;
+        gx_q[v] = id & 3;
+    }
 
     // buffer resources for the sc1 hand-off traffic
     const int64_t hx_elems = (int64_t)2 * 2 * B * H;
@@ -111,14 +134,14 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
 
     for (int s = 0; s < T; ++s) {
         pstamp(dbg, s, 0);
-        // epilogue operands first: they do not depend on h
-        float pg[4][4];
+        // 0. the step's gx tile (independent of h): loads in flight across the wait
+        u32x4 gxv[2];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int t = step_time_p(dir, s, plen[p]);
-            const bf16* gp = gx + (((int64_t)t * B + prow[p]) * 2 + dir) * G4 + my_unit;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) pg[p][k] = (float)gp[k * H];
+        for (int v = 0; v < 2; ++v) {
+            const int lr = gx_lr[v];
+            const int t = step_time(dir, s, s_len[lr]);
+            const bf16* gp = gx + (((int64_t)t * B + b0 + lr) * 2 + dir) * G4 + gx_gate[v] * H + u0 + 8 * gx_q[v];
+            gxv[v] = *reinterpret_cast<const u32x4*>(gp);
         }
 
         floatx4 acc[2][2];
@@ -128,14 +151,16 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
         if (s > 0) {
-            // 1. wait for the group's h_{s-1}
-            if (tid == 0) {
-                const unsigned target = (unsigned)nu * (unsigned)s;
+            // 1. wait until every member of the group published h_{s-1} (flag >= s)
+            if (w == 0) {
                 unsigned spins = 0;
-                while (__hip_atomic_load(my_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                while (true) {
+                    unsigned f = (unsigned)s;
+                    if (lane < NU) f = __hip_atomic_load(gflags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(f >= (unsigned)s)) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > SPIN_LIMIT) {
-                        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
                     }
                 }
@@ -144,16 +169,27 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             pstamp(dbg, s, 1);
             // 2. stage h_{s-1} rows (sc1 loads: the bytes were written through by other CUs)
             const int64_t base = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
+            u32x4 hv[PBR * H / 8 / 256];
 #pragma unroll
             for (int v = 0; v < PBR * H / 8 / 256; ++v) {
                 const int idx = tid + 256 * v;
                 const int row = idx / (H / 8), kq = idx % (H / 8);
                 const int off = (int)((base + (int64_t)row * H + 8 * kq) * 2);
-                u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(hx_rsrc, off, 0, 16));
-                *reinterpret_cast<u32x4*>(&sh[row * LDH + 8 * kq]) = q;
+                hv[v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(hx_rsrc, off, 0, 16));
             }
-            __syncthreads();
-            pstamp(dbg, s, 2);
+#pragma unroll
+            for (int v = 0; v < PBR * H / 8 / 256; ++v) {
+                const int idx = tid + 256 * v;
+                const int row = idx / (H / 8), kq = idx % (H / 8);
+                *reinterpret_cast<u32x4*>(&sh[row * LDH + 8 * kq]) = hv[v];
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+            *reinterpret_cast<u32x4*>(&sgx[(gx_lr[v] * 4 + gx_gate[v]) * PHU + 8 * gx_q[v]]) = gxv[v];
+        __syncthreads();
+        pstamp(dbg, s, 2);
+        if (s > 0) {
             // 3. gates += h_{s-1} . W_h
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
@@ -167,93 +203,259 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             }
         }
 
-        pstamp(dbg, s, 3);
-        // 4. gates for (row, unit): lane c < 8 holds i (tile 0) and f (tile 1),
-        //    lane c ^ 8 holds j and o of the same unit and rows. Results go to
-        //    LDS staging rows [32 rows][32 units] so the stores leave as 16-B pieces.
+        // 4. spill the gate pre-activations: lane (c, g) of wave w holds, for N-tile j,
+        //    gate 2j + (c >> 3) of unit 8w + (c & 7), rows 16 mt + 4 g + r
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float x0 = __shfl_xor(acc[mt][0][r], 8, 64);
-                const float x1 = __shfl_xor(acc[mt][1][r], 8, 64);
-                if ((r >> 1) == (rbase >> 1)) {          // this lane's register pair
-                    const int p = mt * 2 + (r & 1);
-                    const float gi = (c < 8) ? acc[mt][0][r] : x0;
-                    const float gj = (c < 8) ? x0 : acc[mt][0][r];
-                    const float gf = (c < 8) ? acc[mt][1][r] : x1;
-                    const float go = (c < 8) ? x1 : acc[mt][1][r];
-                    const bool valid = s < plen[p];
-                    const float ai = sigf(gi + pg[p][0]);
-                    const float aj = tanhf_(gj + pg[p][1]);
-                    const float af = sigf(gf + pg[p][2] + 1.0f);      // forget_bias = 1
-                    const float ao = sigf(go + pg[p][3]);
-                    const float cn = af * cst[p] + ai * aj;
-                    const float hn = ao * tanhf_(cn);
-                    const int lr = prow[p] - b0, lu = my_unit - u0;
-                    so_h[lr * PHU + lu] = bf16_bits(valid ? hn : hst[p]);      // published state
-                    so_out[lr * PHU + lu] = bf16_bits(valid ? hn : 0.f);
-                    so_hp[lr * PHU + lu] = bf16_bits(valid ? hst[p] : 0.f);
-                    so_cp[lr * PHU + lu] = valid ? cst[p] : 0.f;
-                    so_a[(lr * 4 + 0) * PHU + lu] = bf16_bits(valid ? ai : 0.f);
-                    so_a[(lr * 4 + 1) * PHU + lu] = bf16_bits(valid ? aj : 0.f);
-                    so_a[(lr * 4 + 2) * PHU + lu] = bf16_bits(valid ? af : 0.f);
-                    so_a[(lr * 4 + 3) * PHU + lu] = bf16_bits(valid ? ao : 0.f);
-                    if (valid) { cst[p] = cn; hst[p] = hn; }
-                }
-            }
-        if (tid < PBR) {
-            const int len = s_len[tid];
-            s_t[tid] = step_time_p(dir, s, len);
-            s_valid[tid] = s < len;
-        }
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sG[(16 * mt + 4 * g + r) * LDG + (2 * j + (c >> 3)) * PHU + lu] = acc[mt][j][r];
         __syncthreads();
-        pstamp(dbg, s, 4);
+        pstamp(dbg, s, 3);
 
-        // 5. publish h_s (32 rows x 64 B, sc1), drain, barrier, one lane signals
-        const int64_t obase = (int64_t)((s & 1) * 2 + dir) * B * H;
-        if (tid < PBR * PHU / 8) {
-            const int lr = tid / (PHU / 8), q = tid % (PHU / 8);
-            const u32x4 v = *reinterpret_cast<const u32x4*>(&so_h[lr * PHU + 8 * q]);
-            const int off = (int)((obase + (int64_t)(b0 + lr) * H + u0 + 8 * q) * 2);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), hx_rsrc, off, 0, 16);
+        // 5. the cell update of (row er, units eu..eu+3), all lanes busy
+        const bool valid = s < elen;
+        const int t = step_time(dir, s, elen);
+        float a4[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f32x4 z = *reinterpret_cast<const f32x4*>(&sG[er * LDG + k * PHU + eu]);
+            typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+            const u16x4 xg = *reinterpret_cast<const u16x4*>(&sgx[(er * 4 + k) * PHU + eu]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a4[k][e] = z[e] + bits_f(xg[e]);
+        }
+        float hn[4], cp[4], hp[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float ai = sig_fast(a4[0][e]);
+            const float aj = tanh_fast(a4[1][e]);
+            const float af = sig_fast(a4[2][e] + 1.0f);       // forget_bias = 1
+            const float ao = sig_fast(a4[3][e]);
+            const float cn = af * cst[e] + ai * aj;
+            const float h = ao * tanh_fast(cn);
+            a4[0][e] = valid ? ai : 0.f; a4[1][e] = valid ? aj : 0.f;
+            a4[2][e] = valid ? af : 0.f; a4[3][e] = valid ? ao : 0.f;
+            cp[e] = valid ? cst[e] : 0.f;
+            hp[e] = valid ? hst[e] : 0.f;
+            if (valid) { cst[e] = cn; hst[e] = (float)(bf16)h; }
+            hn[e] = hst[e];                                   // published state (carried when invalid)
+        }
+
+        // 6. publish h_s (8-B sc1 stores), drain, barrier, one lane raises the flag
+        {
+            const int64_t obase = ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu;
+            const unsigned long long v =
+                (unsigned long long)((unsigned)bf16_bits(hn[0]) | ((unsigned)bf16_bits(hn[1]) << 16)) |
+                ((unsigned long long)((unsigned)bf16_bits(hn[2]) | ((unsigned)bf16_bits(hn[3]) << 16)) << 32);
+            __hip_atomic_store((gu64*)(hx + obase), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        pstamp(dbg, s, 5);
         __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pstamp(dbg, s, 6);
+        if (tid == 0) __hip_atomic_store(gflags + member, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pstamp(dbg, s, 4);
 
-        // 6. the rest (layer output + saved tensors) drains behind the next step
-        //    pieces: out 128, hprev 128, cprev 256, acts 512 (16 B each) = 4 per thread
+        // 7. the layer output and the tensors saved for the backward pass
+        //    (time order; they drain behind the next step)
+        const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+        if (valid) st4(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu, hn);
+        st4(hprev_t + tb * H + u0 + eu, hp);
+        st4(cprev_t + tb * H + u0 + eu, cp);
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int id = tid + 256 * v;
-            if (id < 128) {                                           // out [t][b][2H]
-                const int lr = id / 4, q = id % 4;
-                const int64_t o = ((int64_t)s_t[lr] * B + b0 + lr) * 2 * H + dir * H + u0 + 8 * q;
-                if (s_valid[lr]) *reinterpret_cast<u32x4*>(out + o) = *reinterpret_cast<const u32x4*>(&so_out[lr * PHU + 8 * q]);
-            } else if (id < 256) {                                    // hprev [t][b][2][H]
-                const int lr = (id - 128) / 4, q = (id - 128) % 4;
-                const int64_t o = (((int64_t)s_t[lr] * B + b0 + lr) * 2 + dir) * H + u0 + 8 * q;
-                *reinterpret_cast<u32x4*>(hprev_t + o) = *reinterpret_cast<const u32x4*>(&so_hp[lr * PHU + 8 * q]);
-            } else if (id < 512) {                                    // cprev [t][b][2][H] f32
-                const int lr = (id - 256) / 8, q = (id - 256) % 8;
-                const int64_t o = (((int64_t)s_t[lr] * B + b0 + lr) * 2 + dir) * H + u0 + 4 * q;
-                *reinterpret_cast<f32x4*>(cprev_t + o) = *reinterpret_cast<const f32x4*>(&so_cp[lr * PHU + 4 * q]);
-            } else {                                                  // acts [t][b][2][4H]
-                const int k = id - 512, lr = k / 16, gq = k % 16, gate = gq / 4, q = gq % 4;
-                const int64_t o = (((int64_t)s_t[lr] * B + b0 + lr) * 2 + dir) * G4 + gate * H + u0 + 8 * q;
-                *reinterpret_cast<u32x4*>(acts_t + o) = *reinterpret_cast<const u32x4*>(&so_a[(lr * 4 + gate) * PHU + 8 * q]);
+        for (int k = 0; k < 4; ++k) st4(acts_t + tb * G4 + k * H + u0 + eu, a4[k]);
+        pstamp(dbg, s, 5);
+    }
+}
+
+// ---------------------------------------------------------------- backward
+// BPTT of the same layer as ONE persistent launch (groups, members and the
+// hand-off form of the forward). Member (group, unit slice) owns units
+// u0..u0+31 of one direction for 32 batch rows. Reverse step i (s = T-1-i):
+//   dh_rec[rows, own units] = dz_{i-1}[rows, 4H] . W_h[own units, 4H]^T
+// with K = 4H split over the 4 waves by gate (wave w: the H columns of gate
+// w; its W_h slice [32 units x H] stays in VGPRs as B fragments), the A
+// operand being the group's published dz rows, which each wave stages for its
+// own k-range in LDS with full-row sc1 loads (each byte once per workgroup). The 4 partial products meet
+// in LDS; the cell's gradient (dc kept in registers across steps) gives dz
+// for (row, 4 units, 4 gates) per thread, published (sc1) for step i+1 and
+// stored in time order for the weight-gradient GEMMs.
+template <int KS>
+__global__ void __launch_bounds__(256, 1)
+lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len,
+                           int T, int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
+                           const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
+                           unsigned* __restrict__ err, long long* __restrict__ dbg) {
+    constexpr int H = KS * 32;
+    constexpr int G4 = 4 * H;
+    constexpr int NU = H / PHU;
+    constexpr int LDP = PHU + 4;                        // padded partial row (floats)
+    constexpr int LDA = H + 8;                          // padded staged dz row (bf16)
+    static_assert(NU <= 64 && (H == 256 || H == 512), "one poll lane per member; whole-row wave loads");
+    __shared__ __attribute__((aligned(16))) float sP[4 * PBR * LDP];   // [wave][row][unit]
+    __shared__ __attribute__((aligned(16))) unsigned short sA[4 * PBR * LDA];   // [wave][row][k of gate w]
+
+    int group, member;
+    persistent_role(2 * (B / PBR), NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * PHU, b0 = bs * PBR;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    gu32* gflags = (gu32*)(flags) + group * NU;
+
+    // resident B fragments: N-tile j = units u0 + 16 j + c; k = w H + 32 ks + 8 g
+    bf16x8 bw[2][KS];
+    const bf16* wdir = wh + (size_t)dir * H * G4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bf16* row = wdir + (size_t)(u0 + 16 * j + c) * G4 + w * H + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
+    }
+
+    const int er = tid >> 3, eu = 4 * (tid & 7);
+    const int elen = seq_len[b0 + er];
+    float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+    const int64_t zx_elems = (int64_t)2 * 2 * B * G4;
+    auto zx_rsrc = __builtin_amdgcn_make_buffer_rsrc(dzx, 0, (int)(zx_elems * 2), 0x00020000);
+
+    for (int i = 0; i < T; ++i) {
+        const int s = T - 1 - i;
+        pstamp(dbg, i, 0);
+        const bool valid = s < elen;
+        const int t = step_time(dir, s, elen);
+        const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+        // 0. epilogue operands (independent of the recurrence) in flight first
+        float pa[4][4], pcp[4], pdo[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ld4(pa[k], acts_t + tb * G4 + k * H + u0 + eu);
+        ld4(pcp, cprev_t + tb * H + u0 + eu);
+        ld4(pdo, dout + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu);
+
+        floatx4 acc[2][2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (i > 0) {
+            // 1. wait until every member of the group published dz_{i-1} (flag >= i)
+            if (w == 0) {
+                unsigned spins = 0;
+                while (true) {
+                    unsigned f = (unsigned)i;
+                    if (lane < NU) f = __hip_atomic_load(gflags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(f >= (unsigned)i)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > SPIN_LIMIT) {
+                        if (lane == 0) __hip_atomic_store((gu32*)err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            pstamp(dbg, i, 1);
+            // 2. wave w stages the 32 dz rows of gate w's k-range (32 x H bf16) in
+            //    its own LDS region: full rows per wave instruction (16 B per lane,
+            //    sc1), 8 rows per batch, two batches in flight; M-tile mt's MFMAs
+            //    start once its 16 rows are in (wave-local: no workgroup barrier)
+            const int64_t rbase = ((int64_t)(((i - 1) & 1) * 2 + dir) * B + b0) * G4 + w * H;
+            unsigned short* sa = sA + w * PBR * LDA;
+            constexpr int LPR = H / 8, RPI = 64 / LPR, NI = 8 / RPI;     // lanes per row, rows per instruction
+            const int lrow = lane / LPR, lcol = 8 * (lane % LPR);
+            auto load_rows = [&](u32x4 (&v)[NI], int r0) {
+#pragma unroll
+                for (int q = 0; q < NI; ++q) {
+                    const int off = (int)((rbase + (int64_t)(r0 + q * RPI + lrow) * G4 + lcol) * 2);
+                    v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(zx_rsrc, off, 0, 16));
+                }
+            };
+            auto store_rows = [&](const u32x4 (&v)[NI], int r0) {
+#pragma unroll
+                for (int q = 0; q < NI; ++q)
+                    *reinterpret_cast<u32x4*>(&sa[(r0 + q * RPI + lrow) * LDA + lcol]) = v[q];
+            };
+            auto mma_tile = [&](int mt) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const bf16x8 af = *reinterpret_cast<const bf16x8*>(&sa[(16 * mt + c) * LDA + ks * 32 + 8 * g]);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][ks], acc[mt][j], 0, 0, 0);
+                }
+            };
+            u32x4 v0[NI], v1[NI];
+            load_rows(v0, 0);
+            load_rows(v1, 8);
+            store_rows(v0, 0);
+            load_rows(v0, 16);
+            store_rows(v1, 8);
+            load_rows(v1, 24);
+            mma_tile(0);
+            store_rows(v0, 16);
+            store_rows(v1, 24);
+            mma_tile(1);
+        }
+        // 3. the four partial products (one per gate's k-range) meet in LDS
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sP[(w * PBR + 16 * mt + 4 * g + r) * LDP + 16 * j + c] = acc[mt][j][r];
+        __syncthreads();
+        pstamp(dbg, i, 2);
+
+        // 4. the cell's gradient for (row er, units eu..eu+3)
+        float dz[4][4];
+        {
+            f32x4 p[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p[q] = *reinterpret_cast<const f32x4*>(&sP[(q * PBR + er) * LDP + eu]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float dh = ((p[0][e] + p[1][e]) + (p[2][e] + p[3][e])) + pdo[e];
+                const float ai = pa[0][e], aj = pa[1][e], af = pa[2][e], ao = pa[3][e];
+                const float cp = pcp[e];
+                const float cc = af * cp + ai * aj;
+                const float tc = tanh_fast(cc);
+                const float dc = dcs[e] + dh * ao * (1.f - tc * tc);
+                dz[3][e] = valid ? dh * tc * ao * (1.f - ao) : 0.f;
+                dz[0][e] = valid ? dc * aj * ai * (1.f - ai) : 0.f;
+                dz[1][e] = valid ? dc * ai * (1.f - aj * aj) : 0.f;
+                dz[2][e] = valid ? dc * cp * af * (1.f - af) : 0.f;
+                dcs[e] = valid ? dc * af : 0.f;
             }
         }
+        // 5. publish dz (8-B sc1 stores, one per gate), drain, barrier, one lane raises the flag
+        {
+            const int64_t zbase = ((int64_t)((i & 1) * 2 + dir) * B + b0 + er) * G4 + u0 + eu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned long long v =
+                    (unsigned long long)((unsigned)bf16_bits(dz[k][0]) | ((unsigned)bf16_bits(dz[k][1]) << 16)) |
+                    ((unsigned long long)((unsigned)bf16_bits(dz[k][2]) | ((unsigned)bf16_bits(dz[k][3]) << 16)) << 32);
+                __hip_atomic_store((gu64*)(dzx + zbase + k * H), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(gflags + member, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pstamp(dbg, i, 3);
+        // 6. time-order copy for the weight-gradient GEMMs (drains behind the next step)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st4(dG_t + tb * G4 + k * H + u0 + eu, dz[k]);
+        pstamp(dbg, i, 4);
     }
 }
 
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H) {
-    // group counters (16-B aligned block) + error word, then the h exchange buffer
-    size_t counters = ((size_t)2 * (B / PBR) * sizeof(unsigned) + 16 + 15) / 16 * 16;
+    // one flag word per workgroup (128-B aligned block), then the h exchange buffer
+    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     return counters + (size_t)2 * 2 * B * H * sizeof(bf16);
 }
 
@@ -277,11 +479,11 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     OCRK_REQUIRE(ocrk_lstm_fwd_persistent_supported(B, H), "ocrk_lstm_fwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_fwd_persistent_workspace_size(B, H), "ocrk_lstm_fwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
-    size_t counters = ((size_t)2 * (B / PBR) * sizeof(unsigned) + 16 + 15) / 16 * 16;
+    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     unsigned* cnt = (unsigned*)ws;
     bf16* hx = (bf16*)((char*)ws + counters);
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
-    dim3 grid(H / PHU, B / PBR, 2);
+    const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512)
         lstm_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                              (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
@@ -289,4 +491,44 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
         lstm_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                             (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
     return ocrk::launch_status("ocrk_lstm_fwd_persistent");
+}
+
+// ---------------------------------------------------------- backward C ABI
+extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
+    // one flag word per workgroup (128-B aligned block), then the dz exchange buffer
+    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    return counters + (size_t)2 * 2 * B * 4 * H * sizeof(bf16);
+}
+
+extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
+    if (B % PBR || H % PHU || !(H == 256 || H == 512)) return 0;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    hipError_t e = H == 512
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<16>, 256, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<8>, 256, 0);
+    if (e != hipSuccess) return 0;
+    const long grid = 2L * (B / PBR) * (H / PHU);
+    return grid <= (long)cus * per_cu ? 1 : 0;
+}
+
+extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
+                                        const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
+                                        void* ws, size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(ocrk_lstm_bwd_persistent_supported(B, H), "ocrk_lstm_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
+    OCRK_REQUIRE(ws_bytes >= ocrk_lstm_bwd_persistent_workspace_size(B, H), "ocrk_lstm_bwd_persistent: workspace too small");
+    hipStream_t st = ocrk::as_stream(stream);
+    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    unsigned* cnt = (unsigned*)ws;
+    bf16* zx = (bf16*)((char*)ws + counters);
+    if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");
+    const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
+    if (H == 512)
+        lstm_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
+                                                             (const bf16*)acts_t, (bf16*)dG_t, cnt, err, g_lstm_dbg);
+    else
+        lstm_bwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
+                                                            (const bf16*)acts_t, (bf16*)dG_t, cnt, err, g_lstm_dbg);
+    return ocrk::launch_status("ocrk_lstm_bwd_persistent");
 }

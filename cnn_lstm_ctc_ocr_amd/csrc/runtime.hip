@@ -32,6 +32,59 @@ int ocrk_version(void) { return OCRK_ABI_VERSION; }
 
 const char* ocrk_last_error(void) { return ocrk::g_err; }
 
+// Event timers for launch probes. Recorded on a capturing stream they become
+// event-record nodes of the hipGraph (appended at the capture frontier), so a
+// replayed graph still timestamps the launches it brackets.
+int ocrk_timer_create(void** ev) {
+    OCRK_REQUIRE(ev != nullptr, "ocrk_timer_create: null handle slot");
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return ocrk::launch_status("ocrk_timer_create");
+    *ev = e;
+    return OCRK_OK;
+}
+
+int ocrk_timer_record(void* ev, void* stream) {
+    OCRK_REQUIRE(ev != nullptr, "ocrk_timer_record: null event");
+    hipStream_t st = ocrk::as_stream(stream);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return ocrk::launch_status("ocrk_timer_record");
+    hipError_t e = hipSuccess;
+    if (cs == hipStreamCaptureStatusActive) {
+        // append an event-record node after the capture's current frontier and
+        // make it the new frontier (the stream-ordered equivalent of a record)
+        unsigned long long id = 0;
+        hipGraph_t g = nullptr;
+        const hipGraphNode_t* deps = nullptr;
+        size_t nd = 0;
+        hipGraphNode_t node = nullptr;
+        e = hipStreamGetCaptureInfo_v2(st, &cs, &id, &g, &deps, &nd);
+        if (e == hipSuccess) e = hipGraphAddEventRecordNode(&node, g, deps, nd, (hipEvent_t)ev);
+        if (e == hipSuccess) e = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
+    } else {
+        e = hipEventRecord((hipEvent_t)ev, st);
+    }
+    if (e != hipSuccess) {
+        ocrk::set_error("ocrk_timer_record: %s", hipGetErrorString(e));
+        return OCRK_ERR_HIP;
+    }
+    return OCRK_OK;
+}
+
+int ocrk_timer_elapsed(void* ev0, void* ev1, float* ms) {
+    OCRK_REQUIRE(ev0 && ev1 && ms, "ocrk_timer_elapsed: null argument");
+    hipError_t e = hipEventElapsedTime(ms, (hipEvent_t)ev0, (hipEvent_t)ev1);
+    if (e != hipSuccess) {
+        ocrk::set_error("ocrk_timer_elapsed: %s", hipGetErrorString(e));
+        return OCRK_ERR_HIP;
+    }
+    return OCRK_OK;
+}
+
+int ocrk_timer_destroy(void* ev) {
+    if (ev) (void)hipEventDestroy((hipEvent_t)ev);
+    return OCRK_OK;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------ host CRC32C

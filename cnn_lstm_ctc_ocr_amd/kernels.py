@@ -208,15 +208,17 @@ _PERSISTENT = {}
 
 
 def lstm_persistent_ok(B, H, dtype):
-    """bf16 persistent time loop enabled (OCRK_LSTM_PERSISTENT=1) and usable (grid co-resident)?
-    Off by default: measured 14.1-14.5 us/step vs 11.4 us for the per-step kernels at B=256
-    (DESIGN.md section 5)."""
+    """Run the bf16 time loops as persistent launches (csrc/lstm_persistent.hip)?
+    On by default where the grid fits co-resident (B % 32 == 0, H in {256,
+    512}); OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
     import os
-    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "0") != "1":
+    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
         return False
     key = (B, H)
     if key not in _PERSISTENT:
-        _PERSISTENT[key] = bool(_lib.lib().ocrk_lstm_fwd_persistent_supported(B, H))
+        lib = _lib.lib()
+        _PERSISTENT[key] = bool(lib.ocrk_lstm_fwd_persistent_supported(B, H)) and \
+            bool(lib.ocrk_lstm_bwd_persistent_supported(B, H))
     return _PERSISTENT[key]
 
 
@@ -260,9 +262,15 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
     _chk(wh, seq_len, dout, cprev, acts)
     dtype = dout.dtype
     dev = dout.device
+    dG = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
+    if lstm_persistent_ok(B, H, dtype):
+        nb = _lib.lib().ocrk_lstm_bwd_persistent_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        call("ocrk_lstm_bwd_persistent", ptr(wh), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev), ptr(acts), ptr(dG),
+             ptr(lstm_error_word(dev)), ptr(ws), nb, _stream(dout))
+        return dG
     dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
     dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
-    dG = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
     call("ocrk_lstm_bwd", ptr(wh), ptr(dg_state), ptr(dc_state), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev),
          ptr(acts), ptr(dG), dtype_code(dtype), _stream(dout))
     return dG

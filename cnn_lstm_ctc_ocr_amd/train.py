@@ -19,7 +19,7 @@ import torch.distributed as dist
 
 from . import kernels as K
 from .config import TRAIN
-from .model import convnet_layers, ctc_loss_layer, rnn_layers
+from .model import convnet_layers, ctc_loss_layer, dense_labels, rnn_layers
 
 
 def allreduce_mean_scale(flat_grad, group=None):
@@ -94,3 +94,84 @@ class Trainer:
         loss = self.loss_and_grads(image, width, label)
         self.apply_gradients()
         return loss
+
+    def graphed(self, image, width, label, max_label_len=None):
+        """A GraphedStep for batches shaped like (image, width, label)."""
+        return GraphedStep(self, image, width, label, max_label_len)
+
+
+class GraphedStep:
+    """The train step with its forward + backward captured ONCE into a HIP
+    graph (torch.cuda.CUDAGraph over the libocrk launches, side-stream weight
+    gradients included as graph branches) and replayed for every batch.
+
+    The reference executes a prebuilt dataflow graph per step as well
+    (`sess.run([train_op, global_step])`, train.py:196-199); here the graph is
+    the ~600 kernel launches of one step, so a step costs one graph launch on
+    the host instead of a Python walk over every op. Replays run exactly the
+    captured kernels on the static input buffers: `step(image, width, label)`
+    copies a new batch (same shape; labels up to `max_label_len`) into them
+    first. The gradient all-reduce (world_size > 1) and the Adam launch stay
+    eager after the replay, so the learning-rate schedule and RCCL see the live
+    host step count.
+
+    Capture needs every per-stream lazy resource (hipBLASLt workspace, kernel
+    attributes) to exist, so one eager forward + backward runs first on the
+    capture stream; the BatchNorm moving statistics it would have updated are
+    restored, and gradients are rewritten by every step anyway. The derived
+    weight images are invalidated before capture so that their rebuild from
+    the live fp32 master values is part of every replay.
+    """
+
+    def __init__(self, trainer, image, width, label, max_label_len=None):
+        store = trainer.store
+        dev = store.device
+        self.trainer = trainer
+        self.B = int(image.shape[0])
+        self.image = image.detach().to(dev).clone()
+        self.width = torch.as_tensor(width).to(device=dev, dtype=torch.int32).clone()
+        lab, ln = dense_labels(label, self.B, dev)
+        lmax = int(max_label_len or lab.shape[1])
+        if lab.shape[1] > lmax:
+            raise ValueError(f"labels of {lab.shape[1]} > max_label_len={lmax}")
+        self.labels = torch.zeros(self.B, lmax, dtype=torch.int32, device=dev)
+        self.labels[:, :lab.shape[1]].copy_(lab)
+        self.label_len = ln.clone()
+        self.stream = torch.cuda.Stream(dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        moving = store.flat_stats.clone()
+        with torch.cuda.stream(self.stream):
+            trainer.loss_and_grads(self.image, self.width, (self.labels, self.label_len))
+            store.flat_stats.copy_(moving)
+            store.join()
+        self.stream.synchronize()
+        store.bump()                 # the weight-image rebuilds must be captured, not cache hits
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.loss = trainer.loss_and_grads(self.image, self.width, (self.labels, self.label_len))
+        torch.cuda.current_stream(dev).wait_stream(self.stream)
+
+    def load(self, image=None, width=None, label=None):
+        """Copy a batch into the graph's static input buffers."""
+        if image is not None:
+            if tuple(image.shape) != tuple(self.image.shape) or image.dtype != self.image.dtype:
+                raise ValueError(f"image {tuple(image.shape)} {image.dtype} does not match the captured "
+                                 f"{tuple(self.image.shape)} {self.image.dtype}")
+            self.image.copy_(image)
+        if width is not None:
+            self.width.copy_(torch.as_tensor(width).to(device=self.width.device, dtype=torch.int32))
+        if label is not None:
+            lab, ln = dense_labels(label, self.B, self.labels.device)
+            if lab.shape[1] > self.labels.shape[1]:
+                raise ValueError(f"labels of {lab.shape[1]} > captured max_label_len={self.labels.shape[1]}")
+            self.labels.zero_()
+            self.labels[:, :lab.shape[1]].copy_(lab)
+            self.label_len.copy_(ln)
+
+    def step(self, image=None, width=None, label=None):
+        """One training iteration on the given batch (or the loaded one);
+        returns the graph's device loss tensor (overwritten by the next step)."""
+        self.load(image, width, label)
+        self.graph.replay()
+        self.trainer.apply_gradients()
+        return self.loss

@@ -167,14 +167,24 @@ int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* d
                        const void* acts_t, void* dG_t, int dtype, void* stream);
 /* Persistent forward time loop (bf16, H in {256, 512}, B % 32 == 0): ONE launch
  * runs all T steps of both directions; W_h stays in registers, h is exchanged
- * between co-resident workgroups through write-through stores and per-group
- * counters. Same outputs as ocrk_lstm_fwd (h_state/c_state not needed).
+ * between co-resident workgroups through write-through stores and per-member
+ * flags (model_bu.py:167-199). Same outputs as ocrk_lstm_fwd (h_state/c_state not needed).
  * _supported() says whether the grid fits co-resident on this device; err
  * (u32, device) is set non-zero if a hand-off wait timed out. */
 int ocrk_lstm_fwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                              void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err, void* ws,
+                             size_t ws_bytes, void* stream);
+/* Persistent backward time loop (BPTT of the same layer, bf16): ONE launch runs
+ * all T reverse steps of both directions with W_h slices in registers, the
+ * gate gradients dz exchanged between the co-resident workgroups of a
+ * (direction, 32-row batch slice) group, dc kept in registers. Same dG_t as
+ * ocrk_lstm_bwd (dg_state/dc_state not needed); err set on a hand-off timeout. */
+int ocrk_lstm_bwd_persistent_supported(int B, int H);
+size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
+int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
+                             const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err, void* ws,
                              size_t ws_bytes, void* stream);
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
  * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
@@ -240,6 +250,16 @@ int ocrk_mul_scalar(float* x, int64_t n, const float* s, void* stream);
 int ocrk_mean(const float* x, int n, float* out, void* stream);
 /* model.py:152-163: seq_len = floor((width - 2) / 2) - 2 */
 int ocrk_seq_len(const int* widths, int n, int* out, void* stream);
+
+/* Launch-probe timers (bench.py's roofline leg; no reference counterpart).
+ * A hipEvent_t behind an opaque handle; ocrk_timer_record on a stream that is
+ * being captured into a hipGraph adds an event-record node at the capture
+ * frontier, so graph replays keep timing the bracketed work.
+ * ocrk_timer_elapsed = milliseconds between two completed records. */
+int ocrk_timer_create(void** ev);
+int ocrk_timer_record(void* ev, void* stream);
+int ocrk_timer_elapsed(void* ev0, void* ev1, float* ms);
+int ocrk_timer_destroy(void* ev);
 
 /* Host-side CRC32C (Castagnoli) of n bytes continuing from `crc` (0 to start):
  * TFRecord framing and TensorBundle checksums for the input pipeline and the

@@ -4,6 +4,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cnn_lstm_ctc_ocr_amd import kernels as K, _lib
 
 def run(B, H=512, n_in=1024, T=125, reps=3, dt=torch.bfloat16):
+    os.environ["OCRK_LSTM_PERSISTENT"] = "0"
+    K._PERSISTENT.clear()
     dev = torch.device("cuda")
     gx = torch.randn(T * B, 8 * H, device=dev).to(dt)
     whT = (torch.randn(2, 4 * H, H, device=dev) * 0.02).to(dt)
@@ -83,6 +85,30 @@ if "--persistent" in sys.argv:
         e[1].record()
         torch.cuda.synchronize()
         print(f"B={B}: persistent fwd {e[0].elapsed_time(e[1]) / 5 / T * 1e3:.2f} us/step, err={K.lstm_error_word(dev).item()}")
+        wh = (torch.randn(2, H, 4 * H, device=dev) * 0.05).bfloat16()
+        dout = torch.randn(T, B, 2 * H, device=dev).bfloat16()
+        _, _, cprev, acts = got
+        os.environ["OCRK_LSTM_PERSISTENT"] = "0"
+        K._PERSISTENT.clear()
+        dref = K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+        e[0].record()
+        for _ in range(5):
+            K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+        e[1].record()
+        torch.cuda.synchronize()
+        print(f"B={B}: step-kernel bwd {e[0].elapsed_time(e[1]) / 5 / T * 1e3:.2f} us/step")
+        os.environ["OCRK_LSTM_PERSISTENT"] = "1"
+        K._PERSISTENT.clear()
+        dgot = K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+        torch.cuda.synchronize()
+        d = (dref.float() - dgot.float()).abs().max().item()
+        print(f"  dG: max |step-kernel - persistent| = {d:.3e} (max |dG| {dref.float().abs().max().item():.3e})")
+        e[0].record()
+        for _ in range(5):
+            K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+        e[1].record()
+        torch.cuda.synchronize()
+        print(f"B={B}: persistent bwd {e[0].elapsed_time(e[1]) / 5 / T * 1e3:.2f} us/step, err={K.lstm_error_word(dev).item()}")
 
 if "--pstamps" in sys.argv:
     import numpy as np
@@ -101,10 +127,38 @@ if "--pstamps" in sys.argv:
     torch.cuda.synchronize()
     _lib.call("ocrk_lstm_debug_stamps", None)
     st = dbg.view(-1, 8)[:, :7].cpu().numpy().astype(np.float64) * 10.0
-    names = ["top", "poll done", "h staged", "mfma done", "epilogue done", "drained", "signalled"]
+    names = ["top", "poll done", "h+gx staged", "mfma+spill done", "cell+flag done", "outputs issued", "next top"]
     t0 = st[:, 0].min()
     for i, n in enumerate(names):
         print(f"  {n:16s} median {np.median(st[:, i] - t0):8.0f}  max {np.max(st[:, i] - t0):8.0f} ns")
     d = np.diff(st, axis=1)
     for i in range(6):
+        print(f"  {names[i]:>14s} -> {names[i+1]:14s}: median {np.median(d[:, i]):7.0f} ns  max {np.max(d[:, i]):7.0f}")
+
+if "--bstamps" in sys.argv:
+    import numpy as np
+    os.environ["OCRK_LSTM_PERSISTENT"] = "1"
+    K._PERSISTENT.clear()
+    B, H, T = 256, 512, 125
+    dev = torch.device("cuda")
+    gx = torch.randn(T * B, 8 * H, device=dev).bfloat16()
+    whT = (torch.randn(2, 4 * H, H, device=dev) * 0.05).bfloat16()
+    wh = (torch.randn(2, H, 4 * H, device=dev) * 0.05).bfloat16()
+    seq = torch.full((B,), T, dtype=torch.int32, device=dev)
+    _, _, cprev, acts = K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
+    dout = torch.randn(T, B, 2 * H, device=dev).bfloat16()
+    K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    dbg = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", _lib.ptr(dbg))
+    K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    torch.cuda.synchronize()
+    _lib.call("ocrk_lstm_debug_stamps", None)
+    st = dbg.view(-1, 8)[:, [0, 1, 2, 3, 4, 6]].cpu().numpy().astype(np.float64) * 10.0
+    names = ["top", "poll done", "mfma+spill done", "cell+flag done", "dG issued", "next top"]
+    t0 = st[:, 0].min()
+    for i, n in enumerate(names):
+        print(f"  {n:16s} median {np.median(st[:, i] - t0):8.0f}  max {np.max(st[:, i] - t0):8.0f} ns")
+    d = np.diff(st, axis=1)
+    for i in range(5):
         print(f"  {names[i]:>14s} -> {names[i+1]:14s}: median {np.median(d[:, i]):7.0f} ns  max {np.max(d[:, i]):7.0f}")
