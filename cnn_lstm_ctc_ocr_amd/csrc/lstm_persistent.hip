@@ -69,6 +69,60 @@ __device__ __forceinline__ void persistent_role(int ngroups, int nu, int& group,
     }
 }
 
+// Are all members of this workgroup's group on ONE XCD? Each workgroup posts
+// its HW_REG_XCC_ID (+1) once per launch (sc1), wave 0 waits for the group's
+// posts and compares. Placement is the dispatcher's choice: it is measured
+// here, never assumed. On one XCD the group's hand-offs stay in that XCD's L2
+// (plain stores keep the lines in L2; nt loads bypass only the reader's L1);
+// otherwise they use the placement-independent sc1 form.
+__device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member, unsigned* err, int* s_flag) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid == 0) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        __hip_atomic_store(xtab + member, (x & 15u) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < 64) {
+        unsigned v = 1u, spins = 0;
+        while (true) {
+            if (lane < nu) v = __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(v != 0u)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > SPIN_LIMIT) {
+                if (lane == 0) __hip_atomic_store(err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        const unsigned first = __shfl(v, 0, 64);
+        const bool same = __all(lane >= nu || v == first);
+        if (lane == 0) *s_flag = same ? 1 : 0;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// The two hand-off forms (see group_on_one_xcd): flag poll, flag raise,
+// 8-B payload store, 16-B payload load.
+__device__ __forceinline__ unsigned poll_word(gu32* p, bool local) {
+    if (local) {
+        asm volatile("" ::: "memory");
+        return __builtin_nontemporal_load(p);
+    }
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void raise_flag(gu32* p, unsigned v, bool local) {
+    if (local) *p = v;
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put8(gu64* p, unsigned long long v, bool local) {
+    if (local) *p = v;
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u32x4 get16(__amdgpu_buffer_rsrc_t r, int off, bool local) {
+    return local ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2))     // nt
+                 : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));   // sc1
+}
+
 }  // namespace
 
 extern long long* g_lstm_dbg;
@@ -100,6 +154,9 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     const int lu = 8 * w + (c & 7);                     // the unit (within the slice) this lane finishes
     const int my_unit = u0 + lu;
     gu32* gflags = (gu32*)(flags) + group * NU;
+    __shared__ int s_local;
+    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, &s_local);
+    if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // ---- resident B fragments: N-tile j holds gates 2j + (c >> 3) of unit my_unit
     bf16x8 bw[2][KS];
@@ -156,7 +213,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                 unsigned spins = 0;
                 while (true) {
                     unsigned f = (unsigned)s;
-                    if (lane < NU) f = __hip_atomic_load(gflags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(f >= (unsigned)s)) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > SPIN_LIMIT) {
@@ -175,7 +232,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                 const int idx = tid + 256 * v;
                 const int row = idx / (H / 8), kq = idx % (H / 8);
                 const int off = (int)((base + (int64_t)row * H + 8 * kq) * 2);
-                hv[v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(hx_rsrc, off, 0, 16));
+                hv[v] = get16(hx_rsrc, off, local);
             }
 #pragma unroll
             for (int v = 0; v < PBR * H / 8 / 256; ++v) {
@@ -250,11 +307,11 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             const unsigned long long v =
                 (unsigned long long)((unsigned)bf16_bits(hn[0]) | ((unsigned)bf16_bits(hn[1]) << 16)) |
                 ((unsigned long long)((unsigned)bf16_bits(hn[2]) | ((unsigned)bf16_bits(hn[3]) << 16)) << 32);
-            __hip_atomic_store((gu64*)(hx + obase), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            put8((gu64*)(hx + obase), v, local);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(gflags + member, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) raise_flag(gflags + member, (unsigned)(s + 1), local);
         pstamp(dbg, s, 4);
 
         // 7. the layer output and the tensors saved for the backward pass
@@ -303,6 +360,9 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
+    __shared__ int s_local;
+    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, &s_local);
+    if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // resident B fragments: N-tile j = units u0 + 16 j + c; k = w H + 32 ks + 8 g
     bf16x8 bw[2][KS];
@@ -344,7 +404,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                 unsigned spins = 0;
                 while (true) {
                     unsigned f = (unsigned)i;
-                    if (lane < NU) f = __hip_atomic_load(gflags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(f >= (unsigned)i)) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > SPIN_LIMIT) {
@@ -367,7 +427,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 #pragma unroll
                 for (int q = 0; q < NI; ++q) {
                     const int off = (int)((rbase + (int64_t)(r0 + q * RPI + lrow) * G4 + lcol) * 2);
-                    v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(zx_rsrc, off, 0, 16));
+                    v[q] = get16(zx_rsrc, off, local);
                 }
             };
             auto store_rows = [&](const u32x4 (&v)[NI], int r0) {
@@ -438,12 +498,12 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                 const unsigned long long v =
                     (unsigned long long)((unsigned)bf16_bits(dz[k][0]) | ((unsigned)bf16_bits(dz[k][1]) << 16)) |
                     ((unsigned long long)((unsigned)bf16_bits(dz[k][2]) | ((unsigned)bf16_bits(dz[k][3]) << 16)) << 32);
-                __hip_atomic_store((gu64*)(dzx + zbase + k * H), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                put8((gu64*)(dzx + zbase + k * H), v, local);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(gflags + member, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) raise_flag(gflags + member, (unsigned)(i + 1), local);
         pstamp(dbg, i, 3);
         // 6. time-order copy for the weight-gradient GEMMs (drains behind the next step)
 #pragma unroll
@@ -454,8 +514,8 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H) {
-    // one flag word per workgroup (128-B aligned block), then the h exchange buffer
-    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    // flag word + XCC word per workgroup (128-B aligned block), then the h exchange buffer
+    size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     return counters + (size_t)2 * 2 * B * H * sizeof(bf16);
 }
 
@@ -479,7 +539,7 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     OCRK_REQUIRE(ocrk_lstm_fwd_persistent_supported(B, H), "ocrk_lstm_fwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_fwd_persistent_workspace_size(B, H), "ocrk_lstm_fwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
-    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     unsigned* cnt = (unsigned*)ws;
     bf16* hx = (bf16*)((char*)ws + counters);
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
@@ -495,8 +555,8 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
 
 // ---------------------------------------------------------- backward C ABI
 extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
-    // one flag word per workgroup (128-B aligned block), then the dz exchange buffer
-    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    // flag word + XCC word per workgroup (128-B aligned block), then the dz exchange buffer
+    size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     return counters + (size_t)2 * 2 * B * 4 * H * sizeof(bf16);
 }
 
@@ -519,7 +579,7 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     OCRK_REQUIRE(ocrk_lstm_bwd_persistent_supported(B, H), "ocrk_lstm_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_bwd_persistent_workspace_size(B, H), "ocrk_lstm_bwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
-    size_t counters = ((size_t)2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
     unsigned* cnt = (unsigned*)ws;
     bf16* zx = (bf16*)((char*)ws + counters);
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");

@@ -155,6 +155,7 @@ if "--bstamps" in sys.argv:
     torch.cuda.synchronize()
     _lib.call("ocrk_lstm_debug_stamps", None)
     st = dbg.view(-1, 8)[:, [0, 1, 2, 3, 4, 6]].cpu().numpy().astype(np.float64) * 10.0
+    print("  workgroups with an XCD-local group:", int(dbg.view(-1, 8)[:, 7].sum().item()), "of 256")
     names = ["top", "poll done", "mfma+spill done", "cell+flag done", "dG issued", "next top"]
     t0 = st[:, 0].min()
     for i, n in enumerate(names):
