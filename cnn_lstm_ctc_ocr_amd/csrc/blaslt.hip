@@ -8,6 +8,16 @@
 // epilogue or an implicit-GEMM operand stays on the hand-written engines.
 // OCRK_BLASLT=0 disables the route.
 //
+// Also the weight gradients (TN): C[M,N] f32 (+= when accumulating) =
+// A[K,M]^T . B[K,N] with both operands stored k-major (dW = x^T dG,
+// h_prev^T dG, logits x^T dpre): hipBLASLt sees A' = B as N x K (ld = ldb,
+// op N) and B' = A as M x K (ld = lda, op T); beta = 1 accumulates into the
+// f32 gradient, and one call covers all of K (no split-K partials).
+// Opt-in (OCRK_BLASLT_TN=1): on the step's shapes (M = 256..1024, N = 2048,
+// K = 32000) the library's heuristic pick measured 200-394 TFLOP/s
+// (tools/bench_gemm.py), and the train step 8.25 ms against 8.03 ms with the
+// split-K gemm_tn engine, so gemm_tn stays the default.
+//
 // Row-major C[M][N] is column-major C^T (N x M, ld = ldc) = B . A^T: hipBLASLt
 // sees A' = B as a K x N column-major matrix (ld = ldb) with op T, B' = A as
 // K x M (ld = lda) with op N, m = N, n = M; the bias (one value per n of our
@@ -30,7 +40,7 @@ struct LtPlan {
     bool ok = false;
 };
 
-typedef std::tuple<int, int, int, int64_t, int64_t, int64_t, bool> PlanKey;
+typedef std::tuple<int, int, int, int64_t, int64_t, int64_t, bool, bool> PlanKey;   // ..., bias, tn
 
 constexpr size_t LT_WS_BYTES = 32u << 20;
 
@@ -66,16 +76,16 @@ void* lt_ws(LtState& s, hipStream_t st) {
     return p;
 }
 
-LtPlan* lt_plan(LtState& s, const GemmParams& p, bool bias) {
-    PlanKey key{p.M, p.N, p.K, p.lda, p.ldb, p.ldc, bias};
+LtPlan* lt_plan(LtState& s, const GemmParams& p, bool bias, bool tn) {
+    PlanKey key{p.M, p.N, p.K, p.lda, p.ldb, p.ldc, bias, tn};
     auto it = s.plans.find(key);
     if (it != s.plans.end()) return it->second.ok ? &it->second : nullptr;
     LtPlan& pl = s.plans[key];
     bool good = hipblasLtMatmulDescCreate(&pl.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS;
-    const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
-    good = good && hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT)) ==
+    const hipblasOperation_t opA = tn ? HIPBLAS_OP_N : HIPBLAS_OP_T, opB = tn ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+    good = good && hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)) ==
                        HIPBLAS_STATUS_SUCCESS;
-    good = good && hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN)) ==
+    good = good && hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)) ==
                        HIPBLAS_STATUS_SUCCESS;
     if (bias) {
         const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
@@ -85,9 +95,15 @@ LtPlan* lt_plan(LtState& s, const GemmParams& p, bool bias) {
         good = good && hipblasLtMatmulDescSetAttribute(pl.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt,
                                                        sizeof(bt)) == HIPBLAS_STATUS_SUCCESS;
     }
-    good = good && hipblasLtMatrixLayoutCreate(&pl.la, HIP_R_16BF, p.K, p.N, p.ldb) == HIPBLAS_STATUS_SUCCESS;
-    good = good && hipblasLtMatrixLayoutCreate(&pl.lb, HIP_R_16BF, p.K, p.M, p.lda) == HIPBLAS_STATUS_SUCCESS;
-    good = good && hipblasLtMatrixLayoutCreate(&pl.lc, HIP_R_16BF, p.N, p.M, p.ldc) == HIPBLAS_STATUS_SUCCESS;
+    if (tn) {
+        good = good && hipblasLtMatrixLayoutCreate(&pl.la, HIP_R_16BF, p.N, p.K, p.ldb) == HIPBLAS_STATUS_SUCCESS;
+        good = good && hipblasLtMatrixLayoutCreate(&pl.lb, HIP_R_16BF, p.M, p.K, p.lda) == HIPBLAS_STATUS_SUCCESS;
+        good = good && hipblasLtMatrixLayoutCreate(&pl.lc, HIP_R_32F, p.N, p.M, p.ldc) == HIPBLAS_STATUS_SUCCESS;
+    } else {
+        good = good && hipblasLtMatrixLayoutCreate(&pl.la, HIP_R_16BF, p.K, p.N, p.ldb) == HIPBLAS_STATUS_SUCCESS;
+        good = good && hipblasLtMatrixLayoutCreate(&pl.lb, HIP_R_16BF, p.K, p.M, p.lda) == HIPBLAS_STATUS_SUCCESS;
+        good = good && hipblasLtMatrixLayoutCreate(&pl.lc, HIP_R_16BF, p.N, p.M, p.ldc) == HIPBLAS_STATUS_SUCCESS;
+    }
     if (good) {
         hipblasLtMatmulPreference_t pref;
         good = hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS;
@@ -110,12 +126,26 @@ LtPlan* lt_plan(LtState& s, const GemmParams& p, bool bias) {
 
 }  // namespace
 
+bool blaslt_tn_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("OCRK_BLASLT_TN");      // OCRK_BLASLT_TN=1: weight gradients on hipBLASLt
+        on = (e && e[0] == '1') ? 1 : 0;
+    }
+    return on == 1;
+}
+
 int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {
-    if (amode != A_ROWK || bmode != B_NK || dtype != OCRK_BF16 || !p.c_bf16) return -1;
-    if (p.batch != 1 || p.splits != 1 || p.stats || p.mask || p.accumulate || p.relu || p.alpha != 1.f) return -1;
+    const bool nt = amode == A_ROWK && bmode == B_NK && p.c_bf16 && !p.accumulate;
+    const bool tn = amode == A_COLK && bmode == B_KN && !p.c_bf16 && !p.bias && blaslt_tn_enabled();
+    if (!(nt || tn) || dtype != OCRK_BF16) return -1;
+    if (p.batch != 1 || p.stats || p.mask || p.relu || p.alpha != 1.f) return -1;
+    if (nt && p.splits != 1) return -1;
+    if (tn && (((uintptr_t)p.A | (uintptr_t)p.B | (uintptr_t)p.C) % 16 != 0 || p.lda % 8 || p.ldb % 8 || p.ldc % 4))
+        return -1;
     LtState& s = lt();
     if (!s.ok) return -1;
-    LtPlan* pl = lt_plan(s, p, p.bias != nullptr);
+    LtPlan* pl = lt_plan(s, p, p.bias != nullptr, tn);
     if (!pl) return -1;
     void* ws = pl->ws ? lt_ws(s, stream) : nullptr;
     if (pl->ws && !ws) return -1;
@@ -125,7 +155,7 @@ int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_
             HIPBLAS_STATUS_SUCCESS)
             return -1;
     }
-    const float alpha = 1.f, beta = 0.f;
+    const float alpha = 1.f, beta = p.accumulate ? 1.f : 0.f;
     hipblasStatus_t st = hipblasLtMatmul(s.h, pl->desc, &alpha, p.B, pl->la, p.A, pl->lb, &beta, p.C, pl->lc, p.C,
                                          pl->lc, &pl->algo, ws, pl->ws, stream);
     if (st != HIPBLAS_STATUS_SUCCESS) {

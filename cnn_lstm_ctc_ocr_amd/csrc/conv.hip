@@ -1,8 +1,8 @@
 // a1+a2: the conv tower's convolutions (src/weinman/model.py:84-109, :126-146).
 //
 //   conv1   3x3 'valid', Cin = 1: a direct stencil fused with the uint8 ->
-//           float preprocess (validate.py:56-68) and bias + ReLU. One thread
-//           per output pixel computes all Cout channels from 9 cached pixels;
+//           float preprocess (validate.py:56-68) and bias + ReLU. Cout/8 lanes
+//           per output pixel, 8 channels each, from 9 cached pixels;
 //           HBM-bound on the Cout-wide output write.
 //   conv2-8 3x3 'same', Cin >= 32: implicit GEMM on MFMA (gemm.hip) --
 //           M = B*H*W pixels, N = Cout, K = 9*Cin ordered (kh, kw, cin) so one
@@ -17,10 +17,16 @@
 #include "reduce.h"
 
 // ----------------------------------------------------------------- conv1 fwd
+// G = COUT/8 lanes per output pixel, 8 channels each: a wave's 16-B stores
+// cover 64/G consecutive pixels' whole channel rows (contiguous NHWC bytes)
+// instead of one 16-B piece of 64 different pixels; the G lanes of a pixel
+// read the same 9 input bytes (one cache line). Same fma order per channel.
 template <typename TIn, typename TOut, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __restrict__ w,
                  const float* __restrict__ bias, TOut* __restrict__ y) {
+    constexpr int G = COUT / 8, PPB = 256 / G;
+    static_assert(COUT % 8 == 0 && 256 % G == 0, "channel groups");
     __shared__ float sw[9 * COUT];
     __shared__ float sb[COUT];
     for (int i = threadIdx.x; i < 9 * COUT; i += 256) sw[i] = w[i];
@@ -28,7 +34,8 @@ conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __
     __syncthreads();
     const int Ho = H - 2, Wo = W - 2;
     const int64_t npix = (int64_t)B * Ho * Wo;
-    for (int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x; pix < npix; pix += (int64_t)gridDim.x * 256) {
+    const int c0 = 8 * (threadIdx.x % G);
+    for (int64_t pix = (int64_t)blockIdx.x * PPB + threadIdx.x / G; pix < npix; pix += (int64_t)gridDim.x * PPB) {
         int wo = (int)(pix % Wo);
         int64_t t = pix / Wo;
         int ho = (int)(t % Ho);
@@ -46,27 +53,15 @@ conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __
                     px[kh * 3 + kw] = to_f32(v);
                 }
             }
-        TOut* out = y + pix * COUT;
+        F8 o;
 #pragma unroll
-        for (int c0 = 0; c0 < COUT; c0 += 8) {
-            float o[8];
+        for (int c = 0; c < 8; ++c) {
+            float acc = sb[c0 + c];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                float acc = sb[c0 + c];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) acc = fmaf(px[k], sw[k * COUT + c0 + c], acc);
-                o[c] = fmaxf(acc, 0.f);
-            }
-            if constexpr (sizeof(TOut) == 2) {
-                union { uint4 q; bf16 e[8]; } u;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) u.e[c] = (bf16)o[c];
-                *reinterpret_cast<uint4*>(out + c0) = u.q;
-            } else {
-                reinterpret_cast<float4*>(out + c0)[0] = make_float4(o[0], o[1], o[2], o[3]);
-                reinterpret_cast<float4*>(out + c0)[1] = make_float4(o[4], o[5], o[6], o[7]);
-            }
+            for (int k = 0; k < 9; ++k) acc = fmaf(px[k], sw[k * COUT + c0 + c], acc);
+            o.v[c] = fmaxf(acc, 0.f);
         }
+        store8(y + pix * COUT + c0, o);
     }
 }
 
@@ -161,7 +156,7 @@ extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, c
     OCRK_REQUIRE(cout == 32, "ocrk_conv1_fwd: Cout=%d (this build carries the model.py:47 Cout=32)", cout);
     if (B == 0) return OCRK_OK;
     int64_t npix = (int64_t)B * (H - 2) * (W - 2);
-    dim3 grid((unsigned)std::min<int64_t>(ocrk::cdiv(npix, 256), 65535));
+    dim3 grid((unsigned)std::min<int64_t>(ocrk::cdiv(npix, 256 / (32 / 8)), 65535));   // 64 pixels per block pass
     hipStream_t s = ocrk::as_stream(stream);
     if (x_is_u8) {
         if (dtype == OCRK_BF16) conv1_fwd_kernel<uint8_t, bf16, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (bf16*)y);

@@ -8,10 +8,12 @@
 // Layout / work split: one 256-thread workgroup per sequence b. The extended
 // label l' = [blank, l1, blank, l2, ..., blank] (S = 2L+1 states) lives in
 // registers of a single wave: lane j holds states j, j+64, ... (R registers).
-// Wave 0 runs the alpha recursion while wave 1 runs the beta recursion at the
-// same time (wave-synchronous, shuffles only, no barriers inside the time
-// loop); both stream their [T, S] log-lattices to a global workspace, then all
-// four waves form the gradient, one time step per wave.
+// The frame log-sum-exps and the emission log-probs of the extended label are
+// gathered first with many loads in flight; then wave 0 runs the alpha
+// recursion while wave 1 runs the beta recursion (wave-synchronous, shuffles
+// only, no barriers inside the time loop) on emissions and lattices held in
+// LDS (a global workspace when [T, S] is too large); finally every thread forms
+// gradient elements, rows of C contiguous.
 #include "common.h"
 
 #define CTC_THREADS 256
@@ -52,21 +54,28 @@ __device__ __forceinline__ float shift_dn2(const float* a, int r, int R, int lan
     return lane >= 62 ? (r + 1 < R ? w : -INFINITY) : v;
 }
 
-template <int R>
-__device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, const int* lab,
-                          int S, int L, int B, int C, int b, int blank, float* __restrict__ alpha_ws) {
+// Emission log-probabilities of the extended label, em[t*S + s] =
+// logit(t, l'_s) - lse(t): with LAT they are precomputed into LDS (every
+// gather issued up front, in parallel), so the serial recursions below read
+// LDS instead of waiting on a global load per step; without LAT (lattices too
+// large for LDS) they are read from the logits in the loop, as before. The
+// values are the same fp32 expressions either way.
+template <int R, bool LAT>
+__device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, const float* em, const int* lab,
+                          int S, int L, int B, int C, int b, int blank, float* alpha) {
     const int lane = threadIdx.x & 63;
-    int cls[R];
+    int cls[R], es[R];
     bool skip[R];
     float a[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int s = lane + 64 * r;
         cls[r] = (s < S) ? ((s & 1) ? lab[s >> 1] : blank) : blank;
+        es[r] = s < S ? s : S - 1;
         skip[r] = (s < S) && (s & 1) && s >= 3 && lab[s >> 1] != lab[(s >> 1) - 1];
-        float lp = logits[(size_t)b * C + cls[r]] - lse[0];
+        float lp = LAT ? em[es[r]] : logits[(size_t)b * C + cls[r]] - lse[0];
         a[r] = (s < 2 && s < S) ? lp : -INFINITY;
-        if (s < S) alpha_ws[s] = a[r];
+        if (s < S) alpha[s] = a[r];
     }
     for (int t = 1; t < L; ++t) {
         const float* row = logits + ((size_t)t * B + b) * C;
@@ -77,32 +86,34 @@ __device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, co
             float a1 = shift_up1(a, r, lane);
             float a2 = shift_up2(a, r, lane);
             a2 = skip[r] ? a2 : -INFINITY;
-            nxt[r] = lse3(a[r], a1, a2) + (row[cls[r]] - lse[t]);
+            const float e = LAT ? em[(size_t)t * S + es[r]] : row[cls[r]] - lse[t];
+            nxt[r] = lse3(a[r], a1, a2) + e;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             int s = lane + 64 * r;
             a[r] = s < S ? nxt[r] : -INFINITY;
-            if (s < S) alpha_ws[(size_t)t * S + s] = a[r];
+            if (s < S) alpha[(size_t)t * S + s] = a[r];
         }
     }
 }
 
-template <int R>
-__device__ void ctc_beta(const float* __restrict__ logits, const float* lse, const int* lab,
-                         int S, int L, int B, int C, int b, int blank, float* __restrict__ beta_ws) {
+template <int R, bool LAT>
+__device__ void ctc_beta(const float* __restrict__ logits, const float* lse, const float* em, const int* lab,
+                         int S, int L, int B, int C, int b, int blank, float* beta) {
     const int lane = threadIdx.x & 63;
-    int cls[R];
+    int cls[R], es[R];
     bool skipn[R];   // transition s -> s+2 allowed
     float bt[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int s = lane + 64 * r;
         cls[r] = (s < S) ? ((s & 1) ? lab[s >> 1] : blank) : blank;
+        es[r] = s < S ? s : S - 1;
         int s2 = s + 2;
         skipn[r] = (s2 < S) && (s2 & 1) && s2 >= 3 && lab[s2 >> 1] != lab[(s2 >> 1) - 1];
         bt[r] = (s < S && s >= S - 2) ? 0.f : -INFINITY;
-        if (s < S) beta_ws[(size_t)(L - 1) * S + s] = bt[r];
+        if (s < S) beta[(size_t)(L - 1) * S + s] = bt[r];
     }
     for (int t = L - 2; t >= 0; --t) {
         const float* row = logits + ((size_t)(t + 1) * B + b) * C;
@@ -110,7 +121,8 @@ __device__ void ctc_beta(const float* __restrict__ logits, const float* lse, con
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             int s = lane + 64 * r;
-            nb[r] = s < S ? bt[r] + (row[cls[r]] - lse[t + 1]) : -INFINITY;
+            const float e = LAT ? em[(size_t)(t + 1) * S + es[r]] : row[cls[r]] - lse[t + 1];
+            nb[r] = s < S ? bt[r] + e : -INFINITY;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -122,20 +134,24 @@ __device__ void ctc_beta(const float* __restrict__ logits, const float* lse, con
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             int s = lane + 64 * r;
-            if (s < S) beta_ws[(size_t)t * S + s] = bt[r];
+            if (s < S) beta[(size_t)t * S + s] = bt[r];
             else bt[r] = -INFINITY;
         }
     }
 }
 
-template <int R>
+// LAT: the emissions and both lattices live in dynamic LDS ([T][Smax] each,
+// CTC_LAT_MAX bytes at most); otherwise the lattices go to the global workspace.
+#define CTC_LAT_MAX (112 * 1024)
+
+template <int R, bool LAT>
 __global__ void __launch_bounds__(CTC_THREADS)
 ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
                 const int* __restrict__ label_len, const int* __restrict__ seq_len, int T, int B,
                 int C, int max_label, float grad_scale, float* __restrict__ loss,
                 float* __restrict__ grad, int* __restrict__ status, float* __restrict__ ws) {
+    extern __shared__ float s_lat[];
     __shared__ float s_lse[CTC_MAX_T];
-    __shared__ float s_occ[CTC_THREADS / 64][CTC_MAX_C];
     __shared__ float s_logp;
     __shared__ int s_req;
     __shared__ int s_lab[CTC_MAX_R * 32];
@@ -147,8 +163,10 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     const int Lab = label_len[b];
     const int S = 2 * Lab + 1;
     const int Smax = 2 * max_label + 1;
-    float* alpha_ws = ws + (size_t)b * 2 * T * Smax;
-    float* beta_ws = alpha_ws + (size_t)T * Smax;
+    const size_t TS = (size_t)T * Smax;
+    float* em = s_lat;
+    float* alpha = LAT ? s_lat + TS : ws + (size_t)b * 2 * TS;
+    float* beta = alpha + TS;
 
     for (int i = threadIdx.x; i < Lab; i += CTC_THREADS) s_lab[i] = labels[(size_t)b * max_label + i];
 
@@ -174,26 +192,70 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     }
     if (status && threadIdx.x == 0) status[b] = 0;
 
-    // log-sum-exp of every valid frame, one frame per wave at a time
-    for (int t = wave; t < L; t += CTC_THREADS / 64) {
-        const float* row = logits + ((size_t)t * B + b) * C;
-        float m = -INFINITY;
-        for (int k = lane; k < C; k += 64) m = fmaxf(m, row[k]);
-        m = wave_max(m);
-        float s = 0.f;
-        for (int k = lane; k < C; k += 64) s += expf(row[k] - m);
-        s = wave_sum(s);
-        if (lane == 0) s_lse[t] = m + logf(s);
+    // log-sum-exp of every valid frame: a wave takes U frames at a time with all
+    // of their loads in flight, then reduces them one by one
+    constexpr int NW = CTC_THREADS / 64, NQ = CTC_MAX_C / 64, U = 4;
+    for (int t0 = wave; t0 < L; t0 += U * NW) {
+        float v[U][NQ];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u * NW;
+            const float* row = logits + ((size_t)t * B + b) * C;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int k = lane + 64 * q;
+                v[u][q] = (t < L && k < C) ? row[k] : -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u * NW;                   // wave-uniform
+            if (t >= L) break;
+            float m = -INFINITY;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) m = fmaxf(m, v[u][q]);
+            m = wave_max(m);
+            float sum = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                if (lane + 64 * q < C) sum += expf(v[u][q] - m);
+            sum = wave_sum(sum);
+            if (lane == 0) s_lse[t] = m + logf(sum);
+        }
     }
     __syncthreads();
 
+    if constexpr (LAT) {
+        // emissions of the extended label, 4 gathers per thread in flight
+        const int n = L * S;
+        for (int i0 = threadIdx.x; i0 < n; i0 += 4 * CTC_THREADS) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * CTC_THREADS;
+                v[u] = 0.f;
+                if (i < n) {
+                    const int t = i / S, s = i - t * S;
+                    const int k = (s & 1) ? s_lab[s >> 1] : blank;
+                    v[u] = logits[((size_t)t * B + b) * C + k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * CTC_THREADS;
+                if (i < n) em[i] = v[u] - s_lse[i / S];
+            }
+        }
+        __syncthreads();
+    }
+
     if (wave == 0)
-        ctc_alpha<R>(logits, s_lse, s_lab, S, L, B, C, b, blank, alpha_ws);
+        ctc_alpha<R, LAT>(logits, s_lse, em, s_lab, S, L, B, C, b, blank, alpha);
     else if (wave == 1)
-        ctc_beta<R>(logits, s_lse, s_lab, S, L, B, C, b, blank, beta_ws);
+        ctc_beta<R, LAT>(logits, s_lse, em, s_lab, S, L, B, C, b, blank, beta);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float* last = alpha_ws + (size_t)(L - 1) * S;
+        const float* last = alpha + (size_t)(L - 1) * S;
         s_logp = S >= 2 ? lse2(last[S - 1], last[S - 2]) : last[0];
     }
     __syncthreads();
@@ -201,26 +263,38 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     if (threadIdx.x == 0) loss[b] = -logp;
     if (!grad) return;
 
-    // grad[t,k] = softmax - sum_{s: l'_s = k} exp(alpha + beta - logp)
-    float* occ = s_occ[wave];
-    for (int t = wave; t < T; t += CTC_THREADS / 64) {
-        float* grow = grad + ((size_t)t * B + b) * C;
-        if (t >= L) {
-            for (int k = lane; k < C; k += 64) grow[k] = 0.f;
-            continue;
+    // grad[t,k] = softmax - sum_{s: l'_s = k} exp(alpha + beta - logp): one
+    // element per thread (rows of C contiguous), 4 logit loads per thread in
+    // flight; the occupation sum runs over the states of class k in state order
+    const int n = T * C;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 4 * CTC_THREADS) {
+        float lg[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * CTC_THREADS;
+            const int t = i / C;
+            lg[u] = (i < n && t < L) ? logits[((size_t)t * B + b) * C + (i - t * C)] : 0.f;
         }
-        for (int k = lane; k < C; k += 64) occ[k] = 0.f;
-        __builtin_amdgcn_wave_barrier();
-        for (int s = lane; s < S; s += 64) {
-            float v = expf(alpha_ws[(size_t)t * S + s] + beta_ws[(size_t)t * S + s] - logp);
-            int k = (s & 1) ? s_lab[s >> 1] : blank;
-            atomicAdd(&occ[k], v);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * CTC_THREADS;
+            if (i >= n) break;
+            const int t = i / C, k = i - t * C;
+            float gv = 0.f;
+            if (t < L) {
+                const float* at = alpha + (size_t)t * S;
+                const float* bt = beta + (size_t)t * S;
+                float occ = 0.f;
+                if (k == blank) {
+                    for (int s = 0; s < S; s += 2) occ += expf(at[s] + bt[s] - logp);
+                } else {
+                    for (int j = 0; j < Lab; ++j)
+                        if (s_lab[j] == k) occ += expf(at[2 * j + 1] + bt[2 * j + 1] - logp);
+                }
+                gv = grad_scale * (expf(lg[u] - s_lse[t]) - occ);
+            }
+            grad[((size_t)t * B + b) * C + k] = gv;
         }
-        __builtin_amdgcn_wave_barrier();
-        const float* row = logits + ((size_t)t * B + b) * C;
-        for (int k = lane; k < C; k += 64)
-            grow[k] = grad_scale * (expf(row[k] - s_lse[t]) - occ[k]);
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -296,15 +370,29 @@ extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* 
     OCRK_REQUIRE(logits && labels && label_len && seq_len && loss && ws, "ocrk_ctc_loss: null pointer");
     int R = (2 * max_label_len + 1 + 63) / 64;
     hipStream_t s = ocrk::as_stream(stream);
-#define CTC_LAUNCH(RR)                                                                          \
-    ctc_loss_kernel<RR><<<B, CTC_THREADS, 0, s>>>(logits, labels, label_len, seq_len, T, B, C,  \
-                                                  max_label_len, grad_scale, loss, grad, status, \
-                                                  (float*)ws)
+    const size_t lat = 3 * (size_t)T * (2 * (size_t)max_label_len + 1) * sizeof(float);
+    const bool in_lds = lat <= CTC_LAT_MAX;
+#define CTC_ARGS logits, labels, label_len, seq_len, T, B, C, max_label_len, grad_scale, loss, grad, status, (float*)ws
+#define CTC_LAUNCH(RR)                                                                                      \
+    do {                                                                                                    \
+        if (in_lds) {                                                                                       \
+            static bool attr = false;                                                                       \
+            if (!attr) {                                                                                    \
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ctc_loss_kernel<RR, true>),        \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, CTC_LAT_MAX);         \
+                attr = true;                                                                                \
+            }                                                                                               \
+            ctc_loss_kernel<RR, true><<<B, CTC_THREADS, lat, s>>>(CTC_ARGS);                                \
+        } else {                                                                                            \
+            ctc_loss_kernel<RR, false><<<B, CTC_THREADS, 0, s>>>(CTC_ARGS);                                 \
+        }                                                                                                   \
+    } while (0)
     if (R <= 1) CTC_LAUNCH(1);
     else if (R <= 2) CTC_LAUNCH(2);
     else if (R <= 4) CTC_LAUNCH(4);
     else CTC_LAUNCH(8);
 #undef CTC_LAUNCH
+#undef CTC_ARGS
     return ocrk::launch_status("ocrk_ctc_loss");
 }
 

@@ -106,7 +106,8 @@ class _ConvBlock(torch.autograd.Function):
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
                                 dbias=G[pe + "/bias"])                  # conv bias grad fused
         B, H, W, C = dz.shape
-        K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
+        with _conv_side(store, y_odd, dz):                 # overlaps the data-gradient GEMM below
+            K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None)
@@ -115,7 +116,8 @@ class _ConvBlock(torch.autograd.Function):
             K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
             store.join()                                   # side-stream weight gradients are in
         else:
-            K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
+            with _conv_side(store, x, dy_odd):
+                K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
             if ctx.needs_input_grad[0]:
                 _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
@@ -202,6 +204,14 @@ class side_work:
             t.record_stream(self.side)
         self.store.pending.append(done)
         return False
+
+
+def _conv_side(store, *tensors):
+    """Conv weight gradients on the side stream, overlapping the main stream's
+    data-gradient GEMMs and BN backward (OCRK_CONV_SIDE=0: issue them inline)."""
+    if os.environ.get("OCRK_CONV_SIDE", "1") == "0":
+        return contextlib.nullcontext()
+    return side_work(store, *tensors)
 
 
 class _BiLSTM(torch.autograd.Function):

@@ -228,3 +228,22 @@ def test_adam_matches_oracle(cuda):
     np.testing.assert_allclose(pd.cpu().numpy(), p, rtol=1e-6, atol=1e-7)
     # the device forms (1 - beta2) in float32 like TF's ApplyAdam (0.00099998713 vs 0.001)
     np.testing.assert_allclose(vd.cpu().numpy(), v, rtol=3e-5, atol=1e-9)
+
+
+def test_gemm_weight_grad_form_bf16(cuda):
+    """dW += x^T . dG as the recurrent backward issues it (bf16 operands, f32
+    accumulate into an existing gradient, dG a strided column view, split-K
+    requested): the split-K gemm_tn engine (default) or, with OCRK_BLASLT_TN=1,
+    one hipBLASLt call over all of K must give the float64 product."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(5)
+    R, n_in, G4 = 1000, 96, 256
+    x = torch.from_numpy(rng.standard_normal((R, n_in)).astype(np.float32)).bfloat16()
+    dG = torch.from_numpy(rng.standard_normal((R, 2 * G4)).astype(np.float32)).bfloat16()
+    C0 = rng.standard_normal((n_in, G4)).astype(np.float32)
+    out = _t(C0, cuda)
+    xd, dGd = x.to(cuda), dG.to(cuda)
+    Kn.gemm(xd, dGd[:, G4:], trans_a=True, out=out, accumulate=True, M=n_in, N=G4, K=R, lda=n_in, ldb=2 * G4,
+            ldc=G4, splits=4)
+    ref = C0 + x.float().numpy().astype(np.float64).T @ dG.float().numpy()[:, G4:].astype(np.float64)
+    assert _rel(out.cpu().numpy(), ref) < 1e-5
