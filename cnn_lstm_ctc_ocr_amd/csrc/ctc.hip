@@ -155,6 +155,9 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     __shared__ float s_logp;
     __shared__ int s_req;
     __shared__ int s_lab[CTC_MAX_R * 32];
+    __shared__ int s_next[CTC_MAX_R * 32];          // next label index with the same class, or -1
+    __shared__ int s_first[CTC_MAX_C];              // first label index of each class, or -1
+    __shared__ float s_bocc[CTC_MAX_T];             // blank occupation per frame
 
     const int b = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -210,7 +213,7 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int t = t0 + u * NW;                   // wave-uniform
-            if (t >= L) break;
+            if (t >= L) continue;
             float m = -INFINITY;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) m = fmaxf(m, v[u][q]);
@@ -263,9 +266,33 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     if (threadIdx.x == 0) loss[b] = -logp;
     if (!grad) return;
 
-    // grad[t,k] = softmax - sum_{s: l'_s = k} exp(alpha + beta - logp): one
-    // element per thread (rows of C contiguous), 4 logit loads per thread in
-    // flight; the occupation sum runs over the states of class k in state order
+    // grad[t,k] = softmax - sum_{s: l'_s = k} exp(alpha + beta - logp).
+    // (1) occupations E = exp(alpha + beta - logp) of every (t, s), in place of
+    // alpha; the class -> label-index chains (first / next) for (3)
+    const int ns = L * S;
+    for (int i = threadIdx.x; i < ns; i += CTC_THREADS) alpha[i] = expf(alpha[i] + beta[i] - logp);
+    for (int k = threadIdx.x; k < C; k += CTC_THREADS) {
+        int f = -1;
+        for (int j = Lab - 1; j >= 0; --j) f = s_lab[j] == k ? j : f;
+        s_first[k] = f;
+    }
+    for (int j = threadIdx.x; j < Lab; j += CTC_THREADS) {
+        int nx = -1;
+        for (int q = Lab - 1; q > j; --q) nx = s_lab[q] == s_lab[j] ? q : nx;
+        s_next[j] = nx;
+    }
+    __syncthreads();
+    // (2) blank occupation of each frame: a wave per frame, lanes over the even states
+    for (int t = wave; t < L; t += CTC_THREADS / 64) {
+        const float* et = alpha + (size_t)t * S;
+        float o = 0.f;
+        for (int s2 = 2 * lane; s2 < S; s2 += 128) o += et[s2];
+        o = wave_sum(o);
+        if (lane == 0) s_bocc[t] = o;
+    }
+    __syncthreads();
+    // (3) one gradient element per thread (rows of C contiguous), 4 logit loads
+    // per thread in flight; a label class walks its (usually 0 or 1) states
     const int n = T * C;
     for (int i0 = threadIdx.x; i0 < n; i0 += 4 * CTC_THREADS) {
         float lg[4];
@@ -278,22 +305,22 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = i0 + u * CTC_THREADS;
-            if (i >= n) break;
-            const int t = i / C, k = i - t * C;
-            float gv = 0.f;
-            if (t < L) {
-                const float* at = alpha + (size_t)t * S;
-                const float* bt = beta + (size_t)t * S;
-                float occ = 0.f;
-                if (k == blank) {
-                    for (int s = 0; s < S; s += 2) occ += expf(at[s] + bt[s] - logp);
-                } else {
-                    for (int j = 0; j < Lab; ++j)
-                        if (s_lab[j] == k) occ += expf(at[2 * j + 1] + bt[2 * j + 1] - logp);
+            if (i < n) {
+                const int t = i / C, k = i - t * C;
+                float gv = 0.f;
+                if (t < L) {
+                    float occ;
+                    if (k == blank) {
+                        occ = s_bocc[t];
+                    } else {
+                        occ = 0.f;
+                        const float* et = alpha + (size_t)t * S;
+                        for (int j = s_first[k]; j >= 0; j = s_next[j]) occ += et[2 * j + 1];
+                    }
+                    gv = grad_scale * (expf(lg[u] - s_lse[t]) - occ);
                 }
-                gv = grad_scale * (expf(lg[u] - s_lse[t]) - occ);
+                grad[((size_t)t * B + b) * C + k] = gv;
             }
-            grad[((size_t)t * B + b) * C + k] = gv;
         }
     }
 }
@@ -371,7 +398,8 @@ extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* 
     int R = (2 * max_label_len + 1 + 63) / 64;
     hipStream_t s = ocrk::as_stream(stream);
     const size_t lat = 3 * (size_t)T * (2 * (size_t)max_label_len + 1) * sizeof(float);
-    const bool in_lds = lat <= CTC_LAT_MAX;
+    const char* lds_env = getenv("OCRK_CTC_LDS");         // OCRK_CTC_LDS=0: lattices in the global workspace
+    const bool in_lds = lat <= CTC_LAT_MAX && !(lds_env && lds_env[0] == '0');
 #define CTC_ARGS logits, labels, label_len, seq_len, T, B, C, max_label_len, grad_scale, loss, grad, status, (float*)ws
 #define CTC_LAUNCH(RR)                                                                                      \
     do {                                                                                                    \
