@@ -68,17 +68,25 @@ conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __
 // ------------------------------------------------------- conv1 weight grad
 // dw[k][c] = sum_pix x(pix + tap k) * dz[pix][c]; db[c] = sum_pix dz[pix][c].
 // Each block reduces a pixel range into a [10][COUT] partial (slab); a second
-// kernel sums the slabs in a fixed order (deterministic).
+// kernel sums the slabs in a fixed order (deterministic). A thread (8
+// channels) keeps U pixels' loads in flight per pass; the lanes of a wave
+// that share a channel group are combined with a fixed xor-shuffle tree, so
+// the block needs only a [waves][groups][80] scratch and several blocks fit
+// on a CU (the former [256][81] scratch allowed one: one wave per SIMD,
+// latency-bound).
 template <typename TIn, typename TG, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B, int H, int W,
                     int64_t pix_per_block, float* __restrict__ slab) {
     constexpr int G = COUT / 8;              // channel groups of 8
     constexpr int P = 256 / G;               // pixels processed in parallel
-    __shared__ float red[256][10 * 8 + 1];
+    constexpr int U = 4;                     // pixels per thread per pass
+    static_assert(64 % G == 0, "groups within a wave");
+    __shared__ float red[4][G][10 * 8 + 1];
     const int Ho = H - 2, Wo = W - 2;
     const int64_t npix = (int64_t)B * Ho * Wo;
     const int cg = threadIdx.x % G, pl = threadIdx.x / G;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float acc[10][8];
 #pragma unroll
     for (int k = 0; k < 10; ++k)
@@ -86,45 +94,62 @@ conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B,
         for (int c = 0; c < 8; ++c) acc[k][c] = 0.f;
     const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
     const int64_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
-    for (int64_t pix = p0 + pl; pix < p1; pix += P) {
-        int wo = (int)(pix % Wo);
-        int64_t t = pix / Wo;
-        int ho = (int)(t % Ho);
-        int b = (int)(t / Ho);
-        float g[8];
-        const TG* gp = dz + pix * COUT + cg * 8;
+    for (int64_t q0 = p0 + pl; q0 < p1; q0 += (int64_t)P * U) {
+        F8 g[U];
+        float xv[U][9];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) g[c] = to_f32(gp[c]);
+        for (int u = 0; u < U; ++u) {
+            const int64_t pix = q0 + (int64_t)u * P;
+            if (pix < p1) {
+                const int wo = (int)(pix % Wo);
+                const int64_t t = pix / Wo;
+                const int ho = (int)(t % Ho);
+                const int b = (int)(t / Ho);
+                g[u] = load8(dz + pix * COUT + cg * 8);
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+                for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                TIn v = x[((int64_t)b * H + ho + kh) * W + wo + kw];
-                float xv;
-                if constexpr (sizeof(TIn) == 1) {
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const TIn v = x[((int64_t)b * H + ho + kh) * W + wo + kw];
+                        if constexpr (sizeof(TIn) == 1) {
 #pragma clang fp contract(off)
-                    xv = (float)v * (1.0f / 255.0f) - 0.5f;
-                } else {
-                    xv = to_f32(v);
-                }
+                            xv[u][kh * 3 + kw] = (float)v * (1.0f / 255.0f) - 0.5f;
+                        } else {
+                            xv[u][kh * 3 + kw] = to_f32(v);
+                        }
+                    }
+            } else {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[kh * 3 + kw][c] = fmaf(xv, g[c], acc[kh * 3 + kw][c]);
+                for (int c = 0; c < 8; ++c) g[u].v[c] = 0.f;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) xv[u][k] = 0.f;
             }
+        }
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[9][c] += g[c];
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) acc[k][c] = fmaf(xv[u][k], g[u].v[c], acc[k][c]);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc[9][c] += g[u].v[c];
+        }
     }
+    // lanes l, l ^ G, l ^ 2G, ... of a wave hold the same channel group
 #pragma unroll
     for (int k = 0; k < 10; ++k)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) red[threadIdx.x][k * 8 + c] = acc[k][c];
+        for (int c = 0; c < 8; ++c) {
+            float v = acc[k][c];
+#pragma unroll
+            for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+            if (lane < G) red[wave][lane][k * 8 + c] = v;
+        }
     __syncthreads();
-    // thread (k, channel) sums the P partials of its channel group in order
     for (int o = threadIdx.x; o < 10 * COUT; o += 256) {
-        int k = o / COUT, c = o % COUT;
-        int g = c / 8, ci = c % 8;
-        float s = 0.f;
-        for (int q = 0; q < P; ++q) s += red[q * G + g][k * 8 + ci];
-        slab[(int64_t)blockIdx.x * 10 * COUT + o] = s;
+        const int k = o / COUT, c = o % COUT, gg = c / 8, ci = c % 8;
+        slab[(int64_t)blockIdx.x * 10 * COUT + o] =
+            ((red[0][gg][k * 8 + ci] + red[1][gg][k * 8 + ci]) + red[2][gg][k * 8 + ci]) + red[3][gg][k * 8 + ci];
     }
 }
 
