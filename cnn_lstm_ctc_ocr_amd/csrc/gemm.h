@@ -39,6 +39,7 @@ struct GemmParams {
     int splits;
     int k_chunk;                   // k-range per split (multiple of 32)
     int convH, convW, convC;       // im2col source geometry (NHWC) for the A_IM2COL* modes
+    int epi_staged;                // gemm_nt (set by it): bf16 C (and the mask) move through an LDS tile
 };
 
 // XCD-aware tile order for a 1-D grid of 8 * ceil(tm * tn / 8) workgroups.

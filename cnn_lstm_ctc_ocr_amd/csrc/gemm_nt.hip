@@ -208,6 +208,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     const bf16* mask = reinterpret_cast<const bf16*>(p.mask);
     float* Cf = reinterpret_cast<float*>(p.C) + zb * p.strideC;
     bf16* Cb = reinterpret_cast<bf16*>(p.C) + zb * p.strideC;
+    // Staged epilogue (bf16 C): the tile goes through LDS (pitch TP bytes, after
+    // the statistics scratch) and leaves as 16-B row chunks, so a wave's store
+    // covers whole output rows instead of 16 two-byte columns x 4 rows; the
+    // ReLU mask comes in the same way. Values are bit-identical to the direct path.
+    constexpr int TP = BN * 2 + 16, T_OFF = 4096, CPT = BN / 8;
+    constexpr bool TILE_FITS = T_OFF + BM * TP <= S * STAGE;
+    const bool staged = TILE_FITS && p.epi_staged;
+    char* tile = smem + T_OFF;
+    if (staged && mask) {
+        for (int q = tid; q < BM * CPT; q += NW * 64) {
+            const int r = q / CPT, cc = q - r * CPT;
+            const int row = m0 + r, col = n0 + 8 * cc;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (row < p.M && col < p.N) v = *reinterpret_cast<const uint4*>(mask + (int64_t)row * p.ldmask + col);
+            *reinterpret_cast<uint4*>(tile + r * TP + cc * 16) = v;
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int col = col_base + j * 16;
@@ -219,18 +237,35 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
                 const int row = row_base + i * 16 + r;
                 float v = p.alpha * acc[i][j][r] + bcol;
                 if (row < p.M && col < p.N) {
-                    if (mask && !((float)mask[(int64_t)row * p.ldmask + col] > 0.f)) v = 0.f;
-                    if (p.relu) v = fmaxf(v, 0.f);
-                    const int64_t off = (int64_t)row * p.ldc + col;
-                    if (p.c_bf16) {
-                        Cb[off] = (bf16)v;
+                    if (staged) {
+                        bf16* e = reinterpret_cast<bf16*>(tile + (row - m0) * TP + (col - n0) * 2);
+                        if (mask && !((float)*e > 0.f)) v = 0.f;
+                        if (p.relu) v = fmaxf(v, 0.f);
+                        *e = (bf16)v;
                     } else {
-                        if (p.accumulate) v += Cf[off];
-                        Cf[off] = v;
+                        if (mask && !((float)mask[(int64_t)row * p.ldmask + col] > 0.f)) v = 0.f;
+                        if (p.relu) v = fmaxf(v, 0.f);
+                        const int64_t off = (int64_t)row * p.ldc + col;
+                        if (p.c_bf16) {
+                            Cb[off] = (bf16)v;
+                        } else {
+                            if (p.accumulate) v += Cf[off];
+                            Cf[off] = v;
+                        }
                     }
                 }
                 acc[i][j][r] = v;
             }
+    }
+    if (staged) {
+        __syncthreads();
+        for (int q = tid; q < BM * CPT; q += NW * 64) {
+            const int r = q / CPT, cc = q - r * CPT;
+            const int row = m0 + r, col = n0 + 8 * cc;
+            if (row < p.M && col < p.N)
+                *reinterpret_cast<uint4*>(Cb + (int64_t)row * p.ldc + col) =
+                    *reinterpret_cast<const uint4*>(tile + r * TP + cc * 16);
+        }
     }
     if constexpr (!ST) return;
     if (!p.stats) return;
@@ -367,9 +402,23 @@ bool gemm_nt_enabled() {
     return on == 1;
 }
 
+bool nt_staged_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("OCRK_GEMM_NT_STAGED");      // OCRK_GEMM_NT_STAGED=0: direct 2-B stores
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+
 // Runs the NT engine when it covers (mode, dtype); returns -1 when it does not.
-int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {
+int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t stream) {
     if (!gemm_nt_enabled() || dtype != OCRK_BF16 || bmode != B_NK) return -1;
+    GemmParams p = p0;
+    // 16-B row chunks of C (and of the mask) must be aligned and never straddle N
+    p.epi_staged = nt_staged_enabled() && p.c_bf16 && p.splits == 1 && p.N % 8 == 0 && p.ldc % 8 == 0 &&
+                   p.strideC % 8 == 0 && (uintptr_t)p.C % 16 == 0 &&
+                   (!p.mask || (p.ldmask % 8 == 0 && (uintptr_t)p.mask % 16 == 0));
     // wide N with short K (a few k-steps: store-bound) runs better on the
     // generic engine's three resident workgroups per CU (measured)
     if (p.K % 8 != 0 || (p.k_chunk < 512 && p.N > 64)) return -1;
