@@ -149,7 +149,11 @@ def main():
         # captured with the probe timers inside it as external event nodes
         trainer.step(img, widths, labels)
         arm_probes()
-        graphed = trainer.graphed(img, widths, labels)
+        def drop_warmup_records():          # only the captured launches are timed
+            probe.clear()
+            for r in table.values():
+                r.clear()
+        graphed = trainer.graphed(img, widths, labels, before_capture=drop_warmup_records)
         _lib.PROBES.clear()
         run_step = graphed.step
     else:

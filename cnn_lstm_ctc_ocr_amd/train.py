@@ -95,9 +95,9 @@ class Trainer:
         self.apply_gradients()
         return loss
 
-    def graphed(self, image, width, label, max_label_len=None):
+    def graphed(self, image, width, label, max_label_len=None, before_capture=None):
         """A GraphedStep for batches shaped like (image, width, label)."""
-        return GraphedStep(self, image, width, label, max_label_len)
+        return GraphedStep(self, image, width, label, max_label_len, before_capture)
 
 
 class GraphedStep:
@@ -123,7 +123,7 @@ class GraphedStep:
     the live fp32 master values is part of every replay.
     """
 
-    def __init__(self, trainer, image, width, label, max_label_len=None):
+    def __init__(self, trainer, image, width, label, max_label_len=None, before_capture=None):
         store = trainer.store
         dev = store.device
         self.trainer = trainer
@@ -146,6 +146,8 @@ class GraphedStep:
             store.join()
         self.stream.synchronize()
         store.bump()                 # the weight-image rebuilds must be captured, not cache hits
+        if before_capture is not None:
+            before_capture()         # e.g. drop timers recorded by the eager warm-up
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=self.stream):
             self.loss = trainer.loss_and_grads(self.image, self.width, (self.labels, self.label_len))
