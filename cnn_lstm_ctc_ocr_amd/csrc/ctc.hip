@@ -60,6 +60,19 @@ __device__ __forceinline__ float shift_dn2(const float* a, int r, int R, int lan
 // LDS instead of waiting on a global load per step; without LAT (lattices too
 // large for LDS) they are read from the logits in the loop, as before. The
 // values are the same fp32 expressions either way.
+// Whole-wave DPP shifts (GFX9 wave_shr:1 / wave_shl:1): lane i takes lane i-1
+// (resp. i+1); the lane shifted in gets -inf. Used when the lattice fits one
+// register (S <= 64) instead of ds_bpermute shuffles on the recursion's
+// critical path.
+__device__ __forceinline__ float wave_shr1(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY),
+                                                                 __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_shl1(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY),
+                                                                 __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
 template <int R, bool LAT>
 __device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, const float* em, const int* lab,
                           int S, int L, int B, int C, int b, int blank, float* alpha) {
@@ -83,8 +96,14 @@ __device__ void ctc_alpha(const float* __restrict__ logits, const float* lse, co
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             // shuffles run in every lane (convergent); select afterwards
-            float a1 = shift_up1(a, r, lane);
-            float a2 = shift_up2(a, r, lane);
+            float a1, a2;
+            if constexpr (R == 1) {
+                a1 = wave_shr1(a[0]);
+                a2 = wave_shr1(a1);
+            } else {
+                a1 = shift_up1(a, r, lane);
+                a2 = shift_up2(a, r, lane);
+            }
             a2 = skip[r] ? a2 : -INFINITY;
             const float e = LAT ? em[(size_t)t * S + es[r]] : row[cls[r]] - lse[t];
             nxt[r] = lse3(a[r], a1, a2) + e;
@@ -126,8 +145,14 @@ __device__ void ctc_beta(const float* __restrict__ logits, const float* lse, con
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            float b1 = shift_dn1(nb, r, R, lane);
-            float b2 = shift_dn2(nb, r, R, lane);
+            float b1, b2;
+            if constexpr (R == 1) {
+                b1 = wave_shl1(nb[0]);
+                b2 = wave_shl1(b1);
+            } else {
+                b1 = shift_dn1(nb, r, R, lane);
+                b2 = shift_dn2(nb, r, R, lane);
+            }
             b2 = skipn[r] ? b2 : -INFINITY;
             bt[r] = lse3(nb[r], b1, b2);
         }
