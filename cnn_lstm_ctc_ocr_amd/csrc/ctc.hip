@@ -222,7 +222,7 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
 
     // log-sum-exp of every valid frame: a wave takes U frames at a time with all
     // of their loads in flight, then reduces them one by one
-    constexpr int NW = CTC_THREADS / 64, NQ = CTC_MAX_C / 64, U = 4;
+    constexpr int NW = CTC_THREADS / 64, NQ = CTC_MAX_C / 64, U = 8;
     for (int t0 = wave; t0 < L; t0 += U * NW) {
         float v[U][NQ];
 #pragma unroll
@@ -248,34 +248,26 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
             for (int q = 0; q < NQ; ++q)
                 if (lane + 64 * q < C) sum += expf(v[u][q] - m);
             sum = wave_sum(sum);
-            if (lane == 0) s_lse[t] = m + logf(sum);
+            const float lse_t = m + logf(sum);           // the same value in every lane
+            if (lane == 0) s_lse[t] = lse_t;
+            if constexpr (LAT) {
+                // the frame's emissions from the registers already loaded (lane k % 64, slot k / 64)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int s = lane + 64 * r;
+                    const int k = s < S ? ((s & 1) ? s_lab[s >> 1] : blank) : blank;
+                    float val = 0.f;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const float w = __shfl(v[u][q], k & 63, 64);
+                        if ((k >> 6) == q) val = w;
+                    }
+                    if (s < S) em[(size_t)t * S + s] = val - lse_t;
+                }
+            }
         }
     }
     __syncthreads();
-
-    if constexpr (LAT) {
-        // emissions of the extended label, 4 gathers per thread in flight
-        const int n = L * S;
-        for (int i0 = threadIdx.x; i0 < n; i0 += 4 * CTC_THREADS) {
-            float v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + u * CTC_THREADS;
-                v[u] = 0.f;
-                if (i < n) {
-                    const int t = i / S, s = i - t * S;
-                    const int k = (s & 1) ? s_lab[s >> 1] : blank;
-                    v[u] = logits[((size_t)t * B + b) * C + k];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + u * CTC_THREADS;
-                if (i < n) em[i] = v[u] - s_lse[i / S];
-            }
-        }
-        __syncthreads();
-    }
 
     if (wave == 0)
         ctc_alpha<R, LAT>(logits, s_lse, em, s_lab, S, L, B, C, b, blank, alpha);
