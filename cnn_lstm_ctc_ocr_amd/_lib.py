@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (see module docstring: runtime must be torch's)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libocrk.so")
+LIB_PATH = os.environ.get("OCRK_LIB") or os.path.join(_HERE, "libocrk.so")   # OCRK_LIB: experiment builds
 
 OCRK_OK = 0
 OCRK_ERR_INVALID_ARG = 1

@@ -55,8 +55,8 @@ LtState& lt() {
     static LtState s;
     if (!s.tried) {
         s.tried = true;
-        const char* e = getenv("OCRK_BLASLT");
-        if (e && e[0] == '0') return s;
+        const char* e = getenv("OCRK_BLASLT");   // opt-in A/B reference only (OCRK_BLASLT=1)
+        if (!(e && e[0] == '1')) return s;
         s.ok = hipblasLtCreate(&s.h) == HIPBLAS_STATUS_SUCCESS;
     }
     return s;

@@ -74,6 +74,11 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
 // uses the generic engine), else a status. OCRK_GEMM_NT=0 disables it.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
+// 8-wave ping-pong engine (gemm_pp.hip): 256 x {256,128} x 64 tiles for the
+// large bf16 A_ROWK / A_IM2COL / A_IM2COL_FLIP x B_NK GEMMs (N >= 96). Returns
+// -1 when it does not cover the call. OCRK_GEMM_PP=0 disables it.
+int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+
 // Plain A_ROWK x B_NK bf16 GEMMs with a bf16 C and at most a bias epilogue
 // on hipBLASLt (blaslt.hip). Returns -1 when not covered. OCRK_BLASLT=0 disables it.
 int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);

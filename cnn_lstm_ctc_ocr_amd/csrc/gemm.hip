@@ -430,9 +430,11 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     OCRK_REQUIRE(amode < A_IM2COL || p.convC % 8 == 0, "gemm: conv channels must be a multiple of 8");
     OCRK_REQUIRE(!(p.stats && (p.splits > 1 || p.batch > 1)), "gemm: stats need splits=1, batch=1");
     OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
+    int nt = gemm_pp(p, amode, bmode, dtype, stream);
+    if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     const int lt = gemm_blaslt(p, amode, bmode, dtype, stream);     // whole K in one library call
     if (lt >= 0) return lt;
-    int nt = gemm_nt(p, amode, bmode, dtype, stream);
+    nt = gemm_nt(p, amode, bmode, dtype, stream);
     if (nt < 0) nt = gemm_tn(p, amode, bmode, dtype, stream);
     if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     if (dtype == OCRK_BF16) return dispatch_modes<bf16>(p, amode, bmode, stream);

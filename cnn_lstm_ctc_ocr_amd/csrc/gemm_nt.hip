@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     static_assert(TM >= 1 && TN >= 1, "wave tile");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const TileIdx tix = xcd_tile((p.M + BM - 1) / BM, (p.N + BN - 1) / BN);
     if (!tix.valid) return;
@@ -73,8 +73,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     int64_t a_elems, b_elems = (int64_t)p.N * p.ldb;
     if constexpr (AM == A_ROWK) a_elems = (int64_t)p.M * p.lda;
     else a_elems = (int64_t)p.M * p.convC;               // NHWC source with M = B*H*W pixels
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min<int64_t>(a_elems * 2, 0x7fffffff), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min<int64_t>(b_elems * 2, 0x7fffffff), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, a_elems * 2);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, b_elems * 2);
 
     // this lane's row within its instruction and the chunk it fetches (global side of the swizzle);
     // instruction rows start at multiples of RPI, so row & (RPI-1) == lrow

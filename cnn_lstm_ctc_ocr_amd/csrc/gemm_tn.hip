@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_tn_kernel(const GemmParams p) {
     static_assert(CPRA >= 4 && CPRB >= 4 && TM >= 1 && TN >= 1, "tile");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int zb = blockIdx.z / p.splits, zs = blockIdx.z - zb * p.splits;
@@ -55,8 +55,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_tn_kernel(const GemmParams p) {
     if constexpr (AM == A_COLK) a_elems = (int64_t)p.K * p.lda;
     else a_elems = (int64_t)p.K * p.convC;                        // NHWC source, K = B*H*W pixels
     const int64_t b_elems = (int64_t)p.K * p.ldb;
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min<int64_t>(a_elems * 2, 0x7fffffff), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min<int64_t>(b_elems * 2, 0x7fffffff), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, a_elems * 2);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, b_elems * 2);
 
     // ---- per-lane geometry of each A instruction (stage-invariant parts)
     const int qa = lane / CPRA, sa_slot = lane % CPRA;

@@ -66,4 +66,17 @@ __device__ __forceinline__ bf16x8 frag_perm(const unsigned short* row, int g) {
     return __builtin_bit_cast(bf16x8, v);
 }
 
+// Buffer resource from provably wave-uniform words (readfirstlane; the byte
+// count clamped with integer ops -- HIP's min<int64_t> lowers to v_min_f64, a
+// VALU value). A descriptor the compiler cannot prove uniform is kept in VGPRs
+// and every buffer op on it is wrapped in a waterfall loop
+// (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(bytes > 0x7fffffff ? 0x7fffffff : (int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+
 }  // namespace ocrk
