@@ -36,7 +36,7 @@ SIGNATURES = {
     "ocrk_last_error": [],
     "ocrk_preprocess": [_p, _i64, _p, _i32, _p],
     "ocrk_ctc_workspace_size": [_i32, _i32, _i32],
-    "ocrk_ctc_loss": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _f32, _p, _p, _p, _p, _sz, _p],
+    "ocrk_ctc_loss": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _f32, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_ctc_greedy_decode": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],
     "ocrk_ctc_beam_workspace_size": [_i32, _i32, _i32],
     "ocrk_gru_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
@@ -106,6 +106,43 @@ class OcrkError(RuntimeError):
 
 class InvalidArgumentError(OcrkError):
     """Mirrors tf.errors.InvalidArgumentError (e.g. infeasible CTC labels)."""
+
+
+class DeviceError(OcrkError):
+    """A device-side wait gave up (persistent recurrent kernels): its outputs are invalid."""
+
+
+# device status word bits (include/ocrk.h, enum ocrk_device_status)
+STATUS_CTC_INFEASIBLE = 1 << 1
+STATUS_CTC_BAD_LENGTH = 1 << 2
+STATUS_CTC_BAD_LABEL = 1 << 3
+STATUS_LSTM_FWD_TIMEOUT = 1 << 4
+STATUS_LSTM_BWD_TIMEOUT = 1 << 5
+STATUS_LSTM_CENSUS = 1 << 6
+STATUS_CTC = STATUS_CTC_INFEASIBLE | STATUS_CTC_BAD_LENGTH | STATUS_CTC_BAD_LABEL
+STATUS_LSTM = STATUS_LSTM_FWD_TIMEOUT | STATUS_LSTM_BWD_TIMEOUT | STATUS_LSTM_CENSUS
+
+_STATUS_TEXT = {
+    STATUS_CTC_INFEASIBLE: "ctc_loss: not enough time for the target transition sequence "
+                           "(label + repeats > sequence_length)",
+    STATUS_CTC_BAD_LENGTH: "ctc_loss: a label length is negative or exceeds the labels' width",
+    STATUS_CTC_BAD_LABEL: "ctc_loss: a label value is outside [0, num_classes - 1)",
+    STATUS_LSTM_FWD_TIMEOUT: "persistent recurrent forward: a hand-off wait gave up (co-residency lost)",
+    STATUS_LSTM_BWD_TIMEOUT: "persistent recurrent backward: a hand-off wait gave up (co-residency lost)",
+    STATUS_LSTM_CENSUS: "persistent recurrent launch: the placement census gave up",
+}
+
+
+def raise_for_status(word):
+    """Raise the error a non-zero device status word stands for (CTC bits as
+    InvalidArgumentError, like tf.nn.ctc_loss; recurrent timeouts as DeviceError)."""
+    word = int(word)
+    if not word:
+        return
+    text = "; ".join(t for b, t in _STATUS_TEXT.items() if word & b)
+    if word & STATUS_LSTM:
+        raise DeviceError(OCRK_ERR_HIP, f"device status 0x{word:x}: {text}")
+    raise InvalidArgumentError(OCRK_ERR_INFEASIBLE, f"device status 0x{word:x}: {text}")
 
 
 _lib = None

@@ -296,6 +296,16 @@ def restore(store, path, trainer=None, strict=True):
     return prefix
 
 
+def adam_power(beta, updates):
+    """TF1 AdamOptimizer's beta_power slot after `updates` updates: created as
+    beta (_create_slots) and multiplied by beta in float32 by every _finish."""
+    b = np.float32(beta)
+    p = np.float32(beta)
+    for _ in range(int(updates)):
+        p = np.float32(p * b)
+    return np.array(p, np.float32)
+
+
 def save(store, model_dir, global_step=0, trainer=None, name="model.ckpt"):
     """Saver.save(sess, model_dir/name, global_step): variables, BN moving
     statistics, Adam slots when a Trainer is given; updates `checkpoint`."""
@@ -308,8 +318,11 @@ def save(store, model_dir, global_step=0, trainer=None, name="model.ckpt"):
             _, off, shape = store.offsets[n]
             tensors[f"{n}/Adam"] = m[off:off + p.numel()].reshape(shape).copy()
             tensors[f"{n}/Adam_1"] = v[off:off + p.numel()].reshape(shape).copy()
-        tensors["beta1_power"] = np.array(trainer.beta1 ** global_step, np.float32)
-        tensors["beta2_power"] = np.array(trainer.beta2 ** global_step, np.float32)
+        # TF1 AdamOptimizer creates beta*_power = beta* and multiplies it by
+        # beta* in _finish after every update: after t updates it holds beta^(t+1)
+        # (float32 products, one per update, as the assign_mul ops form them)
+        tensors["beta1_power"] = adam_power(trainer.beta1, trainer.global_step)
+        tensors["beta2_power"] = adam_power(trainer.beta2, trainer.global_step)
     prefix = os.path.join(model_dir, f"{name}-{global_step}")
     write_bundle(prefix, tensors)
     write_checkpoint_state(model_dir, prefix)

@@ -174,7 +174,8 @@ __global__ void __launch_bounds__(CTC_THREADS)
 ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
                 const int* __restrict__ label_len, const int* __restrict__ seq_len, int T, int B,
                 int C, int max_label, float grad_scale, float* __restrict__ loss,
-                float* __restrict__ grad, int* __restrict__ status, float* __restrict__ ws) {
+                float* __restrict__ grad, int* __restrict__ status, unsigned* __restrict__ status_word,
+                float* __restrict__ ws) {
     extern __shared__ float s_lat[];
     __shared__ float s_lse[CTC_MAX_T];
     __shared__ float s_logp;
@@ -196,20 +197,36 @@ ctc_loss_kernel(const float* __restrict__ logits, const int* __restrict__ labels
     float* alpha = LAT ? s_lat + TS : ws + (size_t)b * 2 * TS;
     float* beta = alpha + TS;
 
-    for (int i = threadIdx.x; i < Lab; i += CTC_THREADS) s_lab[i] = labels[(size_t)b * max_label + i];
-
-    // feasibility: L + #repeats <= seq_len  ([TF1] ctc_loss_calculator)
+    // validation (TF1 raises InvalidArgumentError for every case flagged here):
+    // a label_len outside [0, max_label] never indexes the label row or the
+    // lattice; label values must lie in [0, C-1) (C-1 is the blank)
+    __shared__ int s_code;
+    if (threadIdx.x == 0) s_code = (Lab < 0 || Lab > max_label) ? 2 : 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (s_code == 0) {
+        bool bad = false;
+        for (int i = threadIdx.x; i < Lab; i += CTC_THREADS) {
+            const int v = labels[(size_t)b * max_label + i];
+            bad |= v < 0 || v >= blank;
+            s_lab[i] = v;
+        }
+        if (__syncthreads_or(bad) && threadIdx.x == 0) s_code = 3;
+    }
+    __syncthreads();
+    // feasibility: L + #repeats <= seq_len  ([TF1] ctc_loss_calculator)
+    if (threadIdx.x == 0 && s_code == 0) {
         int reps = 0;
         for (int i = 1; i < Lab; ++i) reps += s_lab[i] == s_lab[i - 1];
         s_req = Lab + reps;
+        if (s_req > L || L == 0) s_code = 1;
     }
     __syncthreads();
-    if (s_req > L || L == 0) {
+    if (s_code != 0) {
         if (threadIdx.x == 0) {
             loss[b] = INFINITY;
-            if (status) status[b] = 1;
+            if (status) status[b] = s_code;
+            if (status_word)
+                __hip_atomic_fetch_or(status_word, 1u << s_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (grad)
             for (int i = threadIdx.x; i < T * C; i += CTC_THREADS) {
@@ -402,8 +419,8 @@ extern "C" size_t ocrk_ctc_workspace_size(int T, int B, int max_label_len) {
 
 extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* label_len,
                              const int* seq_len, int T, int B, int C, int max_label_len,
-                             float grad_scale, float* loss, float* grad, int* status, void* ws,
-                             size_t ws_bytes, void* stream) {
+                             float grad_scale, float* loss, float* grad, int* status,
+                             unsigned* status_word, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(T > 0 && T <= CTC_MAX_T, "ocrk_ctc_loss: T=%d out of range (1..%d)", T, CTC_MAX_T);
     OCRK_REQUIRE(B >= 0 && C >= 2 && C <= CTC_MAX_C, "ocrk_ctc_loss: bad B=%d / C=%d", B, C);
     OCRK_REQUIRE(max_label_len >= 0 && 2 * max_label_len + 1 <= 64 * CTC_MAX_R,
@@ -417,7 +434,7 @@ extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* 
     const size_t lat = 3 * (size_t)T * (2 * (size_t)max_label_len + 1) * sizeof(float);
     const char* lds_env = getenv("OCRK_CTC_LDS");         // OCRK_CTC_LDS=0: lattices in the global workspace
     const bool in_lds = lat <= CTC_LAT_MAX && !(lds_env && lds_env[0] == '0');
-#define CTC_ARGS logits, labels, label_len, seq_len, T, B, C, max_label_len, grad_scale, loss, grad, status, (float*)ws
+#define CTC_ARGS logits, labels, label_len, seq_len, T, B, C, max_label_len, grad_scale, loss, grad, status, status_word, (float*)ws
 #define CTC_LAUNCH(RR)                                                                                      \
     do {                                                                                                    \
         if (in_lds) {                                                                                       \

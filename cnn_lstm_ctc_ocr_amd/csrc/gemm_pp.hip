@@ -69,7 +69,6 @@ namespace ocrk {
 namespace {
 
 constexpr unsigned PP_OOB = 0x80000000u;
-constexpr unsigned PP_BAD = 0xFFFFFFFFu;
 
 __device__ __forceinline__ void pp_dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);

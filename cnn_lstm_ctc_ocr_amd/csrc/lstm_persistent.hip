@@ -39,7 +39,8 @@ namespace {
 constexpr int PBR = 32, PHU = 32;          // batch rows, hidden units per workgroup
 typedef __attribute__((address_space(1))) unsigned gu32;            // hand-off words: global, never flat
 typedef __attribute__((address_space(1))) unsigned long long gu64;
-constexpr unsigned SPIN_LIMIT = 1u << 22;  // polls (with s_sleep) before giving up
+// polls (with s_sleep) before a hand-off wait gives up: OCRK_LSTM_SPIN_LIMIT
+// (tests force tiny limits), default 1 << 22; the launch passes it in.
 
 __device__ __forceinline__ unsigned short bf16_bits(float x) {
     bf16 b = (bf16)x;
@@ -75,7 +76,8 @@ __device__ __forceinline__ void persistent_role(int ngroups, int nu, int& group,
 // here, never assumed. On one XCD the group's hand-offs stay in that XCD's L2
 // (plain stores keep the lines in L2; nt loads bypass only the reader's L1);
 // otherwise they use the placement-independent sc1 form.
-__device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member, unsigned* err, int* s_flag) {
+__device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member, unsigned* err, unsigned spin_limit,
+                                                 int* s_flag) {
     const int tid = threadIdx.x, lane = tid & 63;
     if (tid == 0) {
         unsigned x;
@@ -88,8 +90,8 @@ __device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member,
             if (lane < nu) v = __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__all(v != 0u)) break;
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > SPIN_LIMIT) {
-                if (lane == 0) __hip_atomic_store(err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (++spins > spin_limit) {
+                if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_CENSUS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }
@@ -127,13 +129,20 @@ __device__ __forceinline__ u32x4 get16(__amdgpu_buffer_rsrc_t r, int off, bool l
 
 extern long long* g_lstm_dbg;
 
+static unsigned lstm_spin_limit() {
+    const char* e = getenv("OCRK_LSTM_SPIN_LIMIT");      // read per launch: tests force tiny limits
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (unsigned)v : (1u << 22);
+}
+
 // KS = H / 32 k-steps
 template <int KS>
 __global__ void __launch_bounds__(256, 1)
 lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
                            const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out,
                            bf16* __restrict__ hprev_t, float* __restrict__ cprev_t, bf16* __restrict__ acts_t,
-                           unsigned* __restrict__ flags, unsigned* __restrict__ err, long long* __restrict__ dbg) {
+                           unsigned* __restrict__ flags, unsigned* __restrict__ err, unsigned spin_limit,
+                           long long* __restrict__ dbg) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;                         // members per group
@@ -155,7 +164,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     const int my_unit = u0 + lu;
     gu32* gflags = (gu32*)(flags) + group * NU;
     __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, &s_local);
+    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
     if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // ---- resident B fragments: N-tile j holds gates 2j + (c >> 3) of unit my_unit
@@ -216,8 +225,8 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(f >= (unsigned)s)) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > SPIN_LIMIT) {
-                        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_FWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
                     }
                 }
@@ -343,7 +352,7 @@ __global__ void __launch_bounds__(256, 1)
 lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len,
                            int T, int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
                            const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
-                           unsigned* __restrict__ err, long long* __restrict__ dbg) {
+                           unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;
@@ -361,7 +370,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
     __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, &s_local);
+    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
     if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // resident B fragments: N-tile j = units u0 + 16 j + c; k = w H + 32 ks + 8 g
@@ -407,8 +416,8 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(f >= (unsigned)i)) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > SPIN_LIMIT) {
-                        if (lane == 0) __hip_atomic_store((gu32*)err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
                     }
                 }
@@ -546,10 +555,10 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512)
         lstm_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
-                                                             (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
+                                                             (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     else
         lstm_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
-                                                            (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, g_lstm_dbg);
+                                                            (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     return ocrk::launch_status("ocrk_lstm_fwd_persistent");
 }
 
@@ -586,9 +595,9 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512)
         lstm_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
-                                                             (const bf16*)acts_t, (bf16*)dG_t, cnt, err, g_lstm_dbg);
+                                                             (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     else
         lstm_bwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
-                                                            (const bf16*)acts_t, (bf16*)dG_t, cnt, err, g_lstm_dbg);
+                                                            (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     return ocrk::launch_status("ocrk_lstm_bwd_persistent");
 }

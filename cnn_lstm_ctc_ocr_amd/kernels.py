@@ -222,14 +222,34 @@ def lstm_persistent_ok(B, H, dtype):
     return _PERSISTENT[key]
 
 
-_ERR = {}
+_STATUS = {}
 
 
-def lstm_error_word(device):
-    """u32 device word the persistent kernels set when a hand-off wait times out."""
-    if device not in _ERR:
-        _ERR[device] = torch.zeros(1, dtype=torch.int32, device=device)
-    return _ERR[device]
+def status_word(device):
+    """The device status word (include/ocrk.h, ocrk_device_status): one u32 per
+    device that the CTC kernel and the persistent recurrent kernels OR their
+    failure bits into. Read it at a sync point with check_status / read_status."""
+    device = torch.device(device)
+    if device not in _STATUS:
+        _STATUS[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _STATUS[device]
+
+
+lstm_error_word = status_word          # the persistent kernels' bits live in the same word
+
+
+def read_status(device, reset=True):
+    """Synchronising read of the device status word (optionally cleared)."""
+    w = status_word(device)
+    v = int(w.item())
+    if v and reset:
+        w.zero_()
+    return v
+
+
+def check_status(device, reset=True):
+    """Raise (InvalidArgumentError / DeviceError) if the device status word is set."""
+    _lib.raise_for_status(read_status(device, reset))
 
 
 def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
@@ -392,7 +412,8 @@ def ctc_loss(logits, labels, label_len, seq_len, grad_scale=1.0, need_grad=True,
     if status is None:
         status = torch.empty(B, dtype=torch.int32, device=logits.device)
     call("ocrk_ctc_loss", ptr(logits), ptr(labels), ptr(label_len), ptr(seq_len), T, B, C, Lmax,
-         float(grad_scale), ptr(loss), ptr(grad), ptr(status), ptr(ws), nb, _stream(logits))
+         float(grad_scale), ptr(loss), ptr(grad), ptr(status), ptr(status_word(logits.device)), ptr(ws), nb,
+         _stream(logits))
     return loss, grad, status
 
 

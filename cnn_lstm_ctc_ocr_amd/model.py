@@ -447,15 +447,54 @@ def check_feasible(sequence_labels_dense, label_len, seq_len):
                                           f"(required: {need}, available: {sl[b]}), batch {b}")
 
 
-def ctc_loss_layer(rnn_logits, sequence_labels, sequence_length, check=False):
+def host_labels(sequence_labels):
+    """True when the labels are host data (a list of sequences or a
+    SparseTensor-like triple), i.e. checkable without touching the device."""
+    return not (isinstance(sequence_labels, (tuple, list)) and len(sequence_labels) == 2 and
+                isinstance(sequence_labels[0], torch.Tensor))
+
+
+def check_feasible_host(sequence_labels, widths):
+    """[TF1] the InvalidArgumentError of tf.nn.ctc_loss (model.py:226,
+    ignore_longer_outputs_than_inputs=False) decided on the host, before any
+    launch: label + repeats must fit seq_len = floor((w-2)/2) - 2 (model.py:152-163),
+    labels must lie in [0, num_classes)."""
+    from ._lib import InvalidArgumentError
+    from .mjsynth import num_classes
+    w = np.asarray(widths.cpu() if isinstance(widths, torch.Tensor) else widths, np.int64).reshape(-1)
+    seq = np.floor((w - 2) / 2).astype(np.int64) - 2
+    lab, ln = dense_labels(sequence_labels, len(w), "cpu")
+    lab, ln = lab.numpy(), ln.numpy()
+    for b in range(len(w)):
+        row = lab[b, :ln[b]]
+        if row.size and (row.min() < 0 or row.max() >= num_classes()):
+            raise InvalidArgumentError(3, f"Label values must be in [0, {num_classes()}), batch {b}")
+        need = len(row) + int(np.sum(row[1:] == row[:-1]))
+        if need > seq[b] or seq[b] <= 0:
+            raise InvalidArgumentError(3, f"Not enough time for target transition sequence "
+                                          f"(required: {need}, available: {max(int(seq[b]), 0)}), batch {b}")
+
+
+def ctc_loss_layer(rnn_logits, sequence_labels, sequence_length, check="deferred"):
     """ctc_loss_layer (src/weinman/model.py:224-229): mean over the batch of
-    tf.nn.ctc_loss(labels, logits, seq_len, time_major=True)."""
+    tf.nn.ctc_loss(labels, logits, seq_len, time_major=True).
+
+    A sequence that cannot be scored (label + repeats > seq_len, a bad label
+    length or value) gets loss +inf and zero gradient, and the kernel sets a
+    bit in the device status word (kernels.status_word). check="deferred"
+    (default): the error is raised at the caller's next status check
+    (Trainer.step polls the word one step later without a sync, and
+    Trainer.check_status / kernels.check_status sync and raise) -- TF raises
+    InvalidArgumentError at sess.run; check=True: synchronise now and raise;
+    check=False: leave the word to the caller."""
     T, B, _ = rnn_logits.shape
     lab, ln = dense_labels(sequence_labels, B, rnn_logits.device)
-    if check:
-        check_feasible(lab, ln, sequence_length)
-    return _CTCLoss.apply(rnn_logits, lab, ln, sequence_length.to(torch.int32).contiguous())
+    loss = _CTCLoss.apply(rnn_logits, lab, ln, sequence_length.to(torch.int32).contiguous())
+    if check is True:
+        K.check_status(rnn_logits.device)
+    return loss
 
 
 __all__ = ["convnet_layers", "rnn_layers", "ctc_loss_layer", "layer_params", "rnn_size", "TRAIN", "INFER",
-           "ParamStore", "ModelConfig", "use_store", "default_store", "dense_labels", "check_feasible"]
+           "ParamStore", "ModelConfig", "use_store", "default_store", "dense_labels", "check_feasible",
+           "check_feasible_host", "host_labels"]

@@ -17,9 +17,10 @@ import math
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from . import kernels as K
 from .config import TRAIN
-from .model import convnet_layers, ctc_loss_layer, dense_labels, rnn_layers
+from .model import check_feasible_host, convnet_layers, ctc_loss_layer, dense_labels, host_labels, rnn_layers
 
 
 def allreduce_mean_scale(flat_grad, group=None):
@@ -34,6 +35,15 @@ def allreduce_mean_scale(flat_grad, group=None):
 
 
 class Trainer:
+    """Device failures surface as exceptions (TF raises at sess.run):
+    * labels given as host data (lists / SparseTensor triples) with host widths
+      are checked before any launch -- an infeasible batch raises
+      InvalidArgumentError and nothing is updated, exactly as in TF;
+    * otherwise the CTC kernel and the persistent recurrent kernels set bits in
+      the device status word; every step queues a non-blocking copy of it and
+      the next step raises if the copy shows a bit (no sync is added), and
+      check_status() synchronises and raises."""
+
     def __init__(self, store, learning_rate=1e-4, momentum=0.9, decay_rate=0.9, decay_steps=2 ** 16,
                  decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0):
         self.store = store
@@ -48,6 +58,8 @@ class Trainer:
         self.global_step = global_step
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
+        self._status_host = None
+        self._status_ev = None
 
     def learning_rate(self, step=None):
         """train.py:120-126 tf.train.exponential_decay."""
@@ -65,6 +77,8 @@ class Trainer:
     def loss_and_grads(self, image, width, label):
         """Forward + backward only; gradients land in store.flat_grad."""
         store = self.store
+        if host_labels(label) and not (isinstance(width, torch.Tensor) and width.is_cuda):
+            check_feasible_host(label, width)
         store.zero_grad()
         features, seq_len = convnet_layers(image, width, TRAIN, store)
         logits = rnn_layers(features, seq_len, store.cfg.num_classes, store)
@@ -91,9 +105,40 @@ class Trainer:
 
     def step(self, image, width, label):
         """One training iteration; returns the (device) mean CTC loss."""
+        self.poll_status()
         loss = self.loss_and_grads(image, width, label)
         self.apply_gradients()
+        self.post_status()
         return loss
+
+    # ---- device status word (include/ocrk.h, ocrk_device_status)
+    def post_status(self):
+        """Queue a non-blocking copy of the device status word (after the step's work)."""
+        dev = self.store.device
+        if dev.type != "cuda" or self._status_ev is not None:
+            return
+        if self._status_host is None:
+            self._status_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._status_host.copy_(K.status_word(dev), non_blocking=True)
+        self._status_ev = torch.cuda.Event()
+        self._status_ev.record(torch.cuda.current_stream(dev))
+
+    def poll_status(self):
+        """Raise if an earlier step's queued status copy has landed and shows a bit
+        (never waits)."""
+        if self._status_ev is None or not self._status_ev.query():
+            return
+        v = int(self._status_host[0])
+        self._status_ev = None
+        if v:
+            K.status_word(self.store.device).zero_()
+            _lib.raise_for_status(v)
+
+    def check_status(self):
+        """Synchronise and raise if any step so far set a device status bit."""
+        self._status_ev = None
+        if self.store.device.type == "cuda":
+            K.check_status(self.store.device)
 
     def graphed(self, image, width, label, max_label_len=None, before_capture=None):
         """A GraphedStep for batches shaped like (image, width, label)."""
@@ -163,6 +208,8 @@ class GraphedStep:
         if width is not None:
             self.width.copy_(torch.as_tensor(width).to(device=self.width.device, dtype=torch.int32))
         if label is not None:
+            if host_labels(label) and width is not None and not (isinstance(width, torch.Tensor) and width.is_cuda):
+                check_feasible_host(label, width)
             lab, ln = dense_labels(label, self.B, self.labels.device)
             if lab.shape[1] > self.labels.shape[1]:
                 raise ValueError(f"labels of {lab.shape[1]} > captured max_label_len={self.labels.shape[1]}")
@@ -173,7 +220,9 @@ class GraphedStep:
     def step(self, image=None, width=None, label=None):
         """One training iteration on the given batch (or the loaded one);
         returns the graph's device loss tensor (overwritten by the next step)."""
+        self.trainer.poll_status()
         self.load(image, width, label)
         self.graph.replay()
         self.trainer.apply_gradients()
+        self.trainer.post_status()
         return self.loss

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 1
+#define OCRK_ABI_VERSION 2
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -41,6 +41,22 @@ enum ocrk_status {
 };
 
 enum ocrk_dtype { OCRK_F32 = 0, OCRK_BF16 = 1 };
+
+/* Device status word: a caller-owned, zero-initialised u32 in device memory.
+ * Kernels OR these bits into it (agent-scope atomics) when a sequence cannot
+ * be processed or a bounded device wait gives up, and still run to completion
+ * (no hang, no trap). The library never synchronises: the caller reads the word
+ * at a sync point it already has and raises (the Python layer does this;
+ * model.py:224-229's tf.nn.ctc_loss raises InvalidArgumentError for the CTC
+ * cases with ignore_longer_outputs_than_inputs=False). */
+enum ocrk_device_status {
+    OCRK_STATUS_CTC_INFEASIBLE = 1 << 1,   /* label + repeats > seq_len, or seq_len == 0 */
+    OCRK_STATUS_CTC_BAD_LENGTH = 1 << 2,   /* label_len < 0 or > max_label_len */
+    OCRK_STATUS_CTC_BAD_LABEL = 1 << 3,    /* a label value outside [0, C-1) (C-1 is the blank) */
+    OCRK_STATUS_LSTM_FWD_TIMEOUT = 1 << 4, /* persistent recurrent forward: a hand-off wait gave up */
+    OCRK_STATUS_LSTM_BWD_TIMEOUT = 1 << 5, /* persistent BPTT: a hand-off wait gave up */
+    OCRK_STATUS_LSTM_CENSUS = 1 << 6       /* persistent launch: a group's placement census gave up */
+};
 
 int ocrk_version(void);
 const char* ocrk_last_error(void);
@@ -54,13 +70,16 @@ int ocrk_preprocess(const uint8_t* in, int64_t n, void* out, int dtype, void* st
  * ctc_merge_repeated=True, blank = C-1, softmax taken inside.
  *   logits  f32 [T, B, C]           labels   i32 [B, max_label_len] (dense, padded)
  *   label_len i32 [B]               seq_len  i32 [B] (frames used per sequence)
- *   loss    f32 [B]  (-log p; +inf and status[b]=1 when infeasible)
- *   grad    f32 [T, B, C] or NULL: grad_scale * d loss_b / d logits (0 for t >= seq_len)
- *   status  i32 [B] or NULL        ws: >= ocrk_ctc_workspace_size(T, B, max_label_len) bytes */
+ *   loss    f32 [B]  (-log p; +inf for a sequence that cannot be scored)
+ *   grad    f32 [T, B, C] or NULL: grad_scale * d loss_b / d logits (0 for t >= seq_len,
+ *           all 0 for a sequence that cannot be scored)
+ *   status  i32 [B] or NULL: 0 scored, 1 infeasible, 2 bad label_len, 3 bad label value
+ *   status_word u32* or NULL: the device status word (OCRK_STATUS_CTC_* bits)
+ *   ws: >= ocrk_ctc_workspace_size(T, B, max_label_len) bytes */
 size_t ocrk_ctc_workspace_size(int T, int B, int max_label_len);
 int ocrk_ctc_loss(const float* logits, const int* labels, const int* label_len, const int* seq_len,
                   int T, int B, int C, int max_label_len, float grad_scale, float* loss, float* grad,
-                  int* status, void* ws, size_t ws_bytes, void* stream);
+                  int* status, unsigned* status_word, void* ws, size_t ws_bytes, void* stream);
 
 /* a10 -- validate._get_output (src/weinman/validate.py:81-92) =
  * tf.nn.ctc_greedy_decoder(logits, seq_len, merge_repeated) + sparse_to_dense(-1):
@@ -169,8 +188,9 @@ int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* d
  * runs all T steps of both directions; W_h stays in registers, h is exchanged
  * between co-resident workgroups through write-through stores and per-member
  * flags (model_bu.py:167-199). Same outputs as ocrk_lstm_fwd (h_state/c_state not needed).
- * _supported() says whether the grid fits co-resident on this device; err
- * (u32, device) is set non-zero if a hand-off wait timed out. */
+ * _supported() says whether the grid fits co-resident on this device; err is
+ * the device status word (OCRK_STATUS_LSTM_FWD_TIMEOUT / _CENSUS bits OR-ed in
+ * when a bounded hand-off wait gives up; OCRK_LSTM_SPIN_LIMIT sets the bound). */
 int ocrk_lstm_fwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
@@ -180,7 +200,8 @@ int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len
  * all T reverse steps of both directions with W_h slices in registers, the
  * gate gradients dz exchanged between the co-resident workgroups of a
  * (direction, 32-row batch slice) group, dc kept in registers. Same dG_t as
- * ocrk_lstm_bwd (dg_state/dc_state not needed); err set on a hand-off timeout. */
+ * ocrk_lstm_bwd (dg_state/dc_state not needed); err: the device status word
+ * (OCRK_STATUS_LSTM_BWD_TIMEOUT / _CENSUS). */
 int ocrk_lstm_bwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,

@@ -534,10 +534,11 @@ def _lse(a, b):
 def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True, blank=None):
     """One sequence of [TF1] CTCBeamSearchDecoder with the default scorer
     (test.py:84-88 beam 128; client.py:227-231 merge_repeated=False).
-    logits [T, C] (already cut to seq_len). Step() subtracts the row max only
-    (no log-softmax); leaves are a bounded top-N by newp.total with strict '>'
-    against the bottom; ties keep the earlier insertion. Returns (paths,
-    log_probs)."""
+    logits [T, C] (already cut to seq_len). Each frame is normalised to
+    log-softmax (row max subtracted, then the log-sum-exp), as SURVEY a11
+    states for the TF1 decoder's input; leaves are a bounded top-N by
+    newp.total with strict '>' against the bottom; ties keep the earlier
+    insertion. Returns (paths, log_probs)."""
     T, C = logits.shape
     blank = C - 1 if blank is None else blank
     root = _BeamEntry(None, -1)

@@ -41,12 +41,12 @@ def test_library_exports_every_symbol():
     lib = _lib.lib()
     for name in _declarations():
         assert hasattr(lib, name), name
-    assert lib.ocrk_version() == 1
+    assert lib.ocrk_version() == 2
 
 
 def test_no_compute_without_device_pointers():
     """A bad argument is reported through the status + message, not a crash."""
     from cnn_lstm_ctc_ocr_amd import _lib
     with pytest.raises(_lib.InvalidArgumentError, match="T=0"):
-        _lib.call("ocrk_ctc_loss", None, None, None, None, 0, 1, 96, 1, 1.0, None, None, None, None, 0, None)
+        _lib.call("ocrk_ctc_loss", None, None, None, None, 0, 1, 96, 1, 1.0, None, None, None, None, None, 0, None)
     assert _lib.lib().ocrk_ctc_workspace_size(125, 256, 19) == 256 * 2 * 125 * 39 * 4

@@ -120,3 +120,26 @@ def test_store_save_restore_with_adam_slots(tmp_path, cell, sizes):
     names = C.read_bundle(prefix)
     assert "rnn/bdrnn1/fw/" + ("lstm_cell/kernel" if cell == "lstm" else "gru_cell/gates/kernel") in names
     assert "convnet/conv1/kernel/Adam_1" in names and names["global_step"] == 42
+
+
+def test_saved_adam_powers_follow_tf1_finish():
+    """TF1 AdamOptimizer holds beta^(t+1) after t updates (created as
+    beta, multiplied by beta in every _finish). A checkpoint written at t = 0
+    must not hold 1.0 (TF would compute lr_t = lr * 0 / 0)."""
+    import tempfile
+
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    assert C.adam_power(0.9, 0) == np.float32(0.9)
+    p = np.float32(0.999)
+    for _ in range(3):
+        p = np.float32(p * np.float32(0.999))
+    assert C.adam_power(0.999, 3) == p
+    cfg = ModelConfig(cell="lstm", rnn_sizes=(32, 32), dtype=torch.float32)
+    store = ParamStore(cfg, device="cpu", seed=1)
+    tr = Trainer(store)
+    tr.global_step = 5
+    with tempfile.TemporaryDirectory() as d:
+        t = C.read_bundle(C.save(store, d, global_step=5, trainer=tr))
+    np.testing.assert_allclose(t["beta1_power"], 0.9 ** 6, rtol=1e-6)
+    np.testing.assert_allclose(t["beta2_power"], 0.999 ** 6, rtol=1e-6)

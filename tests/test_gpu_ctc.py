@@ -67,13 +67,44 @@ def test_ctc_long_labels_multi_register(cuda):
 
 
 def test_ctc_infeasible_flags(cuda):
+    from cnn_lstm_ctc_ocr_amd import _lib
     from cnn_lstm_ctc_ocr_amd import kernels as K
+    K.status_word(cuda).zero_()
     logits = torch.zeros(3, 2, 96, device=cuda)
     lab = torch.tensor([[1, 1, 2], [1, 2, 3]], dtype=torch.int32, device=cuda)
     loss, grad, status = K.ctc_loss(logits, lab, torch.tensor([3, 3], dtype=torch.int32, device=cuda),
                                     torch.tensor([3, 3], dtype=torch.int32, device=cuda))
     assert status.cpu().tolist() == [1, 0]
     assert np.isinf(loss[0].item()) and np.isfinite(loss[1].item())
+    assert K.read_status(cuda) == _lib.STATUS_CTC_INFEASIBLE
+    assert K.read_status(cuda) == 0                        # read_status cleared it
+
+
+def test_ctc_bad_lengths_and_labels_are_flagged_not_read(cuda):
+    """label_len outside [0, max_label_len] or label values outside
+    [0, C-1) must never index past the label row / the lattice: the row is
+    flagged (status 2 / 3, loss +inf, zero gradient), the others are scored."""
+    from cnn_lstm_ctc_ocr_amd import _lib
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    K.status_word(cuda).zero_()
+    rng = np.random.default_rng(5)
+    T, B, C = 20, 5, 96
+    logits = torch.from_numpy(rng.standard_normal((T, B, C)).astype(np.float32)).to(cuda)
+    lab = torch.tensor([[1, 2, 3], [1, 2, 3], [1, 95, 3], [4, -1, 3], [7, 8, 9]], dtype=torch.int32, device=cuda)
+    ln = torch.tensor([3, 400, 3, 3, -2], dtype=torch.int32, device=cuda)
+    seq = torch.full((B,), T, dtype=torch.int32, device=cuda)
+    loss, grad, status = K.ctc_loss(logits, lab, ln, seq)
+    assert status.cpu().tolist() == [0, 2, 3, 3, 2]
+    lv = loss.cpu().numpy()
+    assert np.isfinite(lv[0]) and np.all(np.isinf(lv[1:]))
+    g = grad.cpu().numpy()
+    assert np.all(g[:, 1:] == 0) and np.abs(g[:, 0]).sum() > 0
+    ref_loss, _ = G.ctc_loss(logits.cpu().numpy()[:, :1], [[1, 2, 3]], np.array([T], np.int32))
+    np.testing.assert_allclose(lv[0], ref_loss[0], rtol=1e-3)
+    w = K.read_status(cuda)
+    assert w == _lib.STATUS_CTC_BAD_LENGTH | _lib.STATUS_CTC_BAD_LABEL
+    with pytest.raises(_lib.InvalidArgumentError):
+        _lib.raise_for_status(w)
 
 
 @pytest.mark.parametrize("merge", [True, False])

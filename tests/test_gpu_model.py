@@ -174,3 +174,33 @@ def test_ragged_batch_bf16_rows_independent_of_padding(cuda):
     full, alone = outs
     assert alone.shape[1] == 5
     np.testing.assert_allclose(alone, full[:, :5], rtol=0, atol=1e-6)
+
+
+def test_trainer_raises_on_infeasible_labels(cuda):
+    """tf.nn.ctc_loss (model.py:226, ignore_longer_outputs_than_inputs=False)
+    raises InvalidArgumentError at sess.run. Host labels + host widths: raised
+    before any launch, nothing updated. Device labels: the kernel's status bit
+    surfaces at the next Trainer.step / check_status, never silently."""
+    from cnn_lstm_ctc_ocr_amd import _lib
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    store, vals, img, widths, labels, T = _setup(cuda, torch.float32)
+    K.status_word(cuda).zero_()
+    tr = Trainer(store)
+    bad = [list(l) for l in labels]
+    bad[3] = [7] * (T + 5)                                  # needs 2T+4 frames
+    before = store.flat.clone()
+    with pytest.raises(_lib.InvalidArgumentError):
+        tr.step(torch.from_numpy(img).to(cuda), widths, bad)
+    assert torch.equal(store.flat, before) and tr.global_step == 0
+    # device labels: deferred to the next check
+    from cnn_lstm_ctc_ocr_amd.model import dense_labels
+    lab, ln = dense_labels(bad, len(bad), cuda)
+    tr.step(torch.from_numpy(img).to(cuda), torch.from_numpy(widths).to(cuda), (lab, ln))
+    with pytest.raises(_lib.InvalidArgumentError):
+        tr.check_status()
+    assert K.read_status(cuda) == 0
+    # a good batch after the error trains normally
+    loss = tr.step(torch.from_numpy(img).to(cuda), widths, labels)
+    tr.check_status()
+    assert np.isfinite(loss.item())
