@@ -93,6 +93,45 @@ def cpu_baseline(sample, steps=3, threads=16):
                       f"{threads} BLAS threads, {dt:.1f} s"}
 
 
+def cer_vs_ref(device):
+    """The "CER vs ref" half of BASELINE.json's metric, measured outside the
+    timed region: the HIP path's greedy (validate.py:81-92) and beam-16
+    (test.py:84-88 with BASELINE configs[4]'s width) decodes of the committed
+    golden batch (tests/golden/mjsynth_test_bucket.npz: 8 real crops of the
+    reference's data/test shard, serving uint8 layout and training float
+    layout) against the float64 oracle's decodes stored in that fixture, with
+    the reference initialisers (seed 0, LSTM 512/512; no trained checkpoint
+    exists). CER = sum(edit distance) / sum(len(oracle decode)) (test.py:90-99,
+    tf.edit_distance normalize=False), on device; fp32 and bf16 compute."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
+    g = np.load(os.path.join(ROOT, "tests", "golden", "mjsynth_test_bucket.npz"))
+    widths = torch.from_numpy(g["widths"])
+    res = {"data": "tests/golden/mjsynth_test_bucket.npz (8 crops, data/test shard), oracle decodes at seed-0 weights"}
+    for dname, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=dt), device=device, seed=0)
+        edits = {"greedy": [0, 0, 0], "beam16": [0, 0, 0]}         # sum edit, sum ref length, rows differing
+        for inp in ("u8", "f32"):
+            x = torch.from_numpy(g["x_u8"] if inp == "u8" else g["x_f32"]).to(device)
+            if inp == "f32":
+                x = x.to(dt)
+            with torch.no_grad():
+                feats, seq = model.convnet_layers(x, widths, model.INFER, store)
+                logits = model.rnn_layers(feats, seq, 95, store).float()
+                hyps = {"greedy": decode.ctc_greedy_decoder(logits, seq)[0][0],
+                        "beam16": decode.ctc_beam_search_decoder(logits, seq, beam_width=16)[0][0]}
+            for kind, hyp in hyps.items():
+                ref = torch.from_numpy(g[f"{inp}_{kind}"]).to(device)
+                ref_len = (ref >= 0).sum(1).to(torch.int32)
+                hyp_len = (hyp >= 0).sum(1).to(torch.int32)
+                d = decode.edit_distance(hyp, hyp_len, ref.to(torch.int32), ref_len).cpu().numpy()
+                edits[kind][0] += float(d.sum())
+                edits[kind][1] += int(ref_len.sum().item())
+                edits[kind][2] += int((d > 0).sum())
+        for kind, (e, n, rows) in edits.items():
+            res[f"{dname}_{kind}"] = {"cer": round(e / max(n, 1), 5), "rows_differing": rows, "rows": 16}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +147,7 @@ def main():
     ap.add_argument("--breakdown", action="store_true", help="per-entry-point event timing table on stderr")
     ap.add_argument("--cpu-sample", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
                     help="PMC summary (tools/pmc_traffic.py) for roofline.traffic of the conv roofline kernel")
     args = ap.parse_args()
@@ -247,6 +287,8 @@ def main():
         result["roofline"]["traffic"] = pmc["bytes_per_launch"]
         result["roofline"]["traffic_unit"] = "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
         result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
+    if rank == 0 and not args.no_cer:
+        result["cer_vs_ref"] = cer_vs_ref(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample)
     if rank == 0:

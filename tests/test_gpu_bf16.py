@@ -1,0 +1,201 @@
+"""bf16 parity of the BENCHED routes against the float64 oracle.
+
+The headline bench runs bf16 (BASELINE.json configs[2]); these tests pin the
+bf16 engines it uses at the layer shapes it uses, against the oracle on the
+SAME bf16-rounded operands (so the only differences are the kernels' fp32
+accumulation order and the bf16 rounding of their outputs):
+  * the NT im2col conv engine (forward with the BN-statistics epilogue and the
+    ReLU epilogue, backward-data with the producer's ReLU mask and the fused
+    bias gradient) and the TN weight-gradient engine, at conv2 (32->32,
+    30x254) and conv8 (256->256, 3x125) -- model.py:84-109,126-146;
+  * the ping-pong GEMM engine (gemm_pp) with a bias epilogue and bf16 C on the
+    recurrent input-projection and data-gradient shapes -- model_bu.py:186-192;
+  * the whole bf16 train step (persistent LSTM, every default route) at the
+    bench's width and LSTM sizes, B=64 (T*B=8000 rows: the same kernels and
+    tile configurations as B=256; two float64 oracle runs of a 256-crop step
+    take minutes of host time), loss / logits / every variable's gradient,
+    with the bf16 bounds stated in the test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_graph as G
+from oracle import ref_model as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).bfloat16().float().numpy()
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# bf16 output rounding alone is 2^-9 relative per element (~1.6e-3 RMS on
+# random data); accumulation-order differences are below 1e-5
+BF16_OUT = 4e-3
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout", [(4, 30, 254, 32, 32), (16, 3, 125, 256, 256)])
+def test_bf16_conv_engines_at_layer_shapes(cuda, B, H, W, cin, cout):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(cin * 7 + W)
+    x = _bf(rng.standard_normal((B, H, W, cin)))
+    w = _bf(rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin))
+    b = rng.standard_normal(cout).astype(np.float32)
+    x64, w64 = x.astype(np.float64), w.astype(np.float64)
+    z = G.conv2d(x64, w64, b.astype(np.float64), "same")
+    xd = torch.from_numpy(x).to(cuda).bfloat16()
+    wd = torch.from_numpy(w).to(cuda)
+    w_nk = Kn.permute3(wd, 9 * cin, cout, 1, torch.bfloat16).view(cout, 9 * cin)
+    w_bwd = Kn.permute3(wd, 9, cin, cout, torch.bfloat16).view(cin, 9 * cout)
+    M_ = B * H * W
+    # forward with the BN statistics epilogue (conv2/4/6/8) and with ReLU (conv3/5/7)
+    stats = torch.empty(Kn.conv_stats_tiles(M_), 2, cout, device=cuda)
+    y = Kn.conv3x3_fwd(xd, w_nk, torch.from_numpy(b).to(cuda), False, stats=stats)
+    assert _rel(y.float().cpu().numpy(), z) < BF16_OUT
+    mean, invstd = Kn.bn_finalize(stats, M_, cout, 1e-3, 0.99)
+    zf = z.reshape(-1, cout)
+    np.testing.assert_allclose(mean.cpu().numpy(), zf.mean(0), rtol=1e-4, atol=1e-4 * np.abs(zf).max())
+    np.testing.assert_allclose(invstd.cpu().numpy(), 1 / np.sqrt(zf.var(0) + 1e-3), rtol=1e-3)
+    yr = Kn.conv3x3_fwd(xd, w_nk, torch.from_numpy(b).to(cuda), True)
+    assert _rel(yr.float().cpu().numpy(), np.maximum(z, 0)) < BF16_OUT
+    # backward-data with the producer's ReLU mask and the fused bias gradient
+    dy = _bf(rng.standard_normal(z.shape))
+    dx_ref, dw_ref, _ = G.conv2d_bwd(x64, w64, dy.astype(np.float64), "same")
+    mask = _bf(rng.standard_normal(x.shape))
+    dmask = dx_ref * (mask > 0)
+    dbias = torch.zeros(cin, device=cuda)
+    dx = Kn.conv3x3_bwd_data(torch.from_numpy(dy).to(cuda).bfloat16(), w_bwd,
+                             relu_mask=torch.from_numpy(mask).to(cuda).bfloat16(), dbias=dbias)
+    assert _rel(dx.float().cpu().numpy(), dmask) < BF16_OUT
+    # the bias gradient sums the fp32 values before their bf16 rounding
+    assert _rel(dbias.cpu().numpy(), dmask.reshape(-1, cin).sum(0)) < 1e-4
+    # TN weight gradient, f32 accumulation over B*H*W pixels
+    dw = torch.zeros(3, 3, cin, cout, device=cuda)
+    Kn.conv3x3_bwd_weight(xd, torch.from_numpy(dy).to(cuda).bfloat16(), dw, accumulate=False)
+    assert _rel(dw.cpu().numpy(), dw_ref) < 1e-4
+
+
+@pytest.mark.parametrize("M_,N,K,tag", [(8000, 4096, 256, "proj L1"), (8000, 4096, 1024, "proj L2"),
+                                         (8000, 1024, 4096, "dx L2"), (8000, 256, 4096, "dx L1"),
+                                         (8000, 1024, 96, "logits dx")])
+def test_bf16_plain_gemms_bias_bf16_out(cuda, M_, N, K, tag):
+    """The recurrent projection / data-gradient GEMMs with a bf16 C (the
+    hand-written ping-pong engine for N >= 512, the NT engine below)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(N + K)
+    a = _bf(rng.standard_normal((M_, K)))
+    w = _bf(rng.standard_normal((N, K)) / np.sqrt(K))
+    bias = rng.standard_normal(N).astype(np.float32)
+    ref = a.astype(np.float64) @ w.astype(np.float64).T + bias
+    out = Kn.gemm(torch.from_numpy(a).to(cuda).bfloat16(), torch.from_numpy(w).to(cuda).bfloat16(), trans_b=True,
+                  bias=torch.from_numpy(bias).to(cuda), out_dtype=torch.bfloat16)
+    assert _rel(out.float().cpu().numpy(), ref) < BF16_OUT, tag
+    # every element within its own bf16 rounding (+ accumulation noise)
+    err = np.abs(out.float().cpu().numpy() - ref)
+    assert np.all(err <= 2 ** -8 * np.abs(ref) + 1e-3 * np.abs(ref).max()), tag
+
+
+def test_bf16_tn_weight_gradient_recurrent_shape(cuda):
+    """dW_x = x^T . dG over T*B rows (split-K TN engine, f32 accumulate)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(3)
+    R, n_in, G4 = 8000, 1024, 2048
+    x = _bf(rng.standard_normal((R, n_in)))
+    dG = _bf(rng.standard_normal((R, 2 * G4)))
+    ref = x.astype(np.float64).T @ dG[:, :G4].astype(np.float64)
+    gk = torch.zeros(n_in, G4, device=cuda)
+    xd, dGd = torch.from_numpy(x).to(cuda).bfloat16(), torch.from_numpy(dG).to(cuda).bfloat16()
+    Kn.gemm(xd, dGd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in, ldb=2 * G4, ldc=G4,
+            splits=4)
+    assert _rel(gk.cpu().numpy(), ref) < 1e-5
+
+
+def _bf16_storage_oracle_grads(monkeypatch, vals, x, widths, labels, sizes):
+    """The float64 oracle with every conv-tower op's output rounded to bf16
+    (conv, BN, ReLU, max-pool and their backward ops): what bf16 STORAGE of
+    the activations and gradients alone does to the exact result."""
+    def wrap(f):
+        def g(*a, **k):
+            r = f(*a, **k)
+            if isinstance(r, tuple):
+                return tuple(_bf(v).astype(np.float64) if isinstance(v, np.ndarray) and v.ndim >= 3 else v
+                             for v in r)
+            return _bf(r).astype(np.float64) if isinstance(r, np.ndarray) else r
+        return g
+    for n in ("conv2d", "conv2d_bwd", "bn_train", "bn_bwd", "relu", "relu_bwd", "maxpool", "maxpool_bwd"):
+        monkeypatch.setattr(G, n, wrap(getattr(G, n)))
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", sizes)
+    out = ref.loss_and_grads(x, widths, labels)
+    monkeypatch.undo()
+    return out[1]
+
+
+def test_bf16_train_step_bench_routes_vs_float64_oracle(cuda, monkeypatch):
+    """One bf16 training forward + backward with every route of the bench
+    (W=256, LSTM 512/512, persistent time loops, ping-pong projections),
+    against the float64 oracle run on the bf16-rounded weights and inputs.
+    Bounds: logits rel-L2 < 2e-2, mean CTC loss rel < 1e-3 (north_star), per-
+    sequence loss rel < 1e-2, recurrent + logits gradients rel-L2 < 1e-2.
+    The conv-tower gradients carry the error of bf16 activation storage
+    itself, which grows down the tower through the BatchNorm backward
+    (measured with the float64 oracle rounding its conv-tower op outputs to
+    bf16: ~4e-2 at conv8 .. ~0.25 at conv1 at this random init); each conv
+    variable's error must stay within 1.5x of that storage-only error (+1e-2)."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, model
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    B, W, sizes = 64, 256, (512, 512)
+    rng = np.random.default_rng(2026)
+    vals = M.init_params(seed=11, rnn_sizes=sizes)
+    vals = {k: (_bf(v) if v.ndim >= 1 and "moving" not in k else v) for k, v in vals.items()}
+    img = rng.integers(0, 256, (B, 32, W, 1)).astype(np.uint8)
+    widths = np.full(B, W, np.int32)
+    widths[1:8] = [250, 240, 230, 220, 210, 200, 190]
+    labels = []
+    for b in range(B):
+        tl = G.seq_len_from_width([widths[b]])[0]
+        while True:
+            lab = list(rng.integers(0, 95, rng.integers(2, 20)))
+            if G.ctc_required_time(lab) <= tl:
+                break
+        labels.append(lab)
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=sizes, dtype=torch.bfloat16), device=cuda, values=vals)
+    store.zero_grad()
+    feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN, store)
+    logits = model.rnn_layers(feats, seq, 95, store)
+    lab, ln = model.dense_labels(labels, B, cuda)
+    loss_b, _, status = Kn.ctc_loss(logits.float().contiguous(), lab, ln, seq.to(torch.int32), need_grad=False)
+    loss = model.ctc_loss_layer(logits, labels, seq)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+
+    x = G.preprocess(img).astype(np.float64)
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", sizes)
+    loss_ref, grads_ref, losses_ref, logits_ref, seq_ref = ref.loss_and_grads(x, widths, labels)
+    grads_emu = _bf16_storage_oracle_grads(monkeypatch, vals, x, widths, labels, sizes)
+    assert seq.cpu().numpy().tolist() == seq_ref.tolist()
+    lg = logits.detach().float().cpu().numpy()
+    errs = {"logits": _rel(lg, logits_ref), "loss": abs(loss.item() - loss_ref) / abs(loss_ref),
+            "loss_b": float(np.max(np.abs(loss_b.cpu().numpy() - losses_ref) / np.abs(losses_ref)))}
+    bound = {}
+    for name, g in grads_ref.items():
+        got = store.grads[name].cpu().numpy()
+        scale = np.linalg.norm(g)
+        if name.endswith("/bias") and name.split("/")[1] in ("conv2", "conv4", "conv6", "conv8"):
+            # a bias in front of BatchNorm: exactly zero gradient, both sides are rounding noise
+            scale = max(scale, 1e-2 * np.linalg.norm(grads_ref[name.replace("/bias", "/kernel")]))
+        errs[name] = float(np.linalg.norm(got - g) / max(scale, 1e-12))
+        emu = float(np.linalg.norm(grads_emu[name] - g) / max(scale, 1e-12))
+        bound[name] = 1e-2 if name.startswith("rnn/") else 1.5 * emu + 1e-2
+    print("bf16 bench-route errors vs float64 oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
+    print("bounds (bf16-storage oracle):", {k: f"{v:.2e}" for k, v in bound.items()})
+    assert errs["logits"] < 2e-2, errs
+    assert errs["loss"] < 1e-3, errs
+    assert errs["loss_b"] < 1e-2, errs
+    bad = {k: (errs[k], bound[k]) for k in bound if errs[k] > bound[k]}
+    assert not bad, bad
