@@ -68,29 +68,110 @@ ROOFLINE_OPS = {
 }
 
 
-def cpu_baseline(sample, steps=3, threads=16):
-    """The oracle (NumPy restatement of the reference graph) train step timed on
-    the host cores: a bounded sample of `sample` 32x256 crops."""
-    from threadpoolctl import threadpool_limits
+def host_cpu():
+    """(host threads for the CPU legs, CPU model name). The GPU box is a slice
+    of a 256-CPU host whose CPU share is OMP_NUM_THREADS (16): more threads
+    than that measured slower (16 / 32 / 64 threads: 35 / 23 / 8 crops/s on a
+    16-crop train step), so the share is used when it is set."""
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        threads = min(threads, int(share))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, model
 
-    from oracle import ref_graph as G
+
+def _cpu_batch(rng, B, W):
+    T = (W - 2) // 2 - 2
+    img, _, (lab, ln) = synthetic_batch(rng, B, W, T, torch.device("cpu"))
+    return img, lab.long(), ln.long()
+
+
+def cpu_baseline(sample, warmup=3, steps=10):
+    """BASELINE.md CPU-baseline plan: the reference graph's train step (conv ->
+    BiLSTM 512/512 -> CTC -> TF1 Adam) as the PyTorch-CPU restatement
+    (oracle/torch_ref.py, checked against the NumPy oracle in
+    tests/test_oracle.py; TensorFlow 1.x is unavailable), with every host
+    thread this process may use, 3 warm-up + 10 timed steps on `sample`
+    synthetic 32x256 crops (bounded so the default run stays within minutes)."""
     from oracle import ref_model as M
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    rng = np.random.default_rng(20260)
-    vals = M.init_params(seed=0)
-    img = rng.integers(0, 256, (sample, 32, 256, 1)).astype(np.uint8)
-    x = G.preprocess(img)
-    widths = np.full(sample, 256, np.int32)
-    labels = [list(rng.integers(0, 95, 8)) for _ in range(sample)]
-    with threadpool_limits(limits=threads):
-        M.train_step(vals, {}, 0, x, widths, labels)                 # warm-up
+    from oracle.torch_ref import TorchRef
+    threads, model = host_cpu()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        ref = TorchRef(M.init_params(seed=0), (512, 512))
+        img, lab, ln = _cpu_batch(np.random.default_rng(20260), sample, 256)
+        for _ in range(warmup):
+            ref.train_step(img, lab, ln)
+        print(f"# cpu baseline: {warmup} warm-up steps done", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         for i in range(steps):
-            M.train_step(vals, {}, i, x, widths, labels)
+            ref.train_step(img, lab, ln)
+            print(f"# cpu baseline: step {i + 1}/{steps}", file=sys.stderr, flush=True)
         dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
     return {"value": round(sample * steps / dt, 3), "unit": "line-crops/sec", "cores": threads, "kind": "port",
-            "sample": f"{steps} oracle train steps (NumPy fp32, LSTM 512/512) on {sample} synthetic 32x256 crops, "
-                      f"{threads} BLAS threads, {dt:.1f} s"}
+            "cpu": model,
+            "sample": f"reference graph on CPU (PyTorch restatement oracle/torch_ref.py; TF1 unavailable): "
+                      f"{warmup} warm-up + {steps} timed train steps (fp32, LSTM 512/512, Adam) on {sample} "
+                      f"synthetic 32x256 crops, {threads} threads, {dt:.1f} s"}
+
+
+def c1_latency(device, reps=20):
+    """BASELINE configs[0] (C1): one 32x128 crop, INFER forward + greedy decode
+    (validate.py:131-177 with common.py's bucket_size=1): the CPU reference
+    path (PyTorch restatement, all host threads) and this path on one GPU
+    (fp32, the reference's precision), median latency."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, model, validate
+    from oracle import ref_model as M
+    from oracle.torch_ref import TorchRef
+    rng = np.random.default_rng(20260)
+    img = rng.integers(0, 256, (1, 32, 128, 1), dtype=np.uint8)
+    threads, cpu = host_cpu()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        ref = TorchRef(M.init_params(seed=0), (512, 512))
+        x = torch.from_numpy(img)
+        cpu_ms = []
+        for i in range(3 + reps):
+            t0 = time.perf_counter()
+            cpu_dec = ref.greedy(x)
+            if i >= 3:
+                cpu_ms.append(1e3 * (time.perf_counter() - t0))
+    finally:
+        torch.set_num_threads(prev)
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
+    xd = torch.from_numpy(img).to(device)
+    wd = torch.tensor([128], dtype=torch.int32)
+    gpu_ms = []
+    for i in range(3 + reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            feats, seq = model.convnet_layers(xd, wd, model.INFER, store)
+            dense = validate._get_output(model.rnn_layers(feats, seq, 95, store), seq)[0].cpu()
+        if i >= 3:
+            gpu_ms.append(1e3 * (time.perf_counter() - t0))
+    same = [int(v) for v in dense[0].tolist() if v >= 0] == cpu_dec[0]
+    return {"workload": "C1: 1 crop 32x128, INFER forward + greedy decode, reference initialisers",
+            "cpu_ms": round(float(np.median(cpu_ms)), 3), "cpu_threads": threads, "cpu": cpu,
+            "gpu_ms": round(float(np.median(gpu_ms)), 3), "gpu_dtype": "f32",
+            "gpu_note": "host wall time incl. launches and the decode's device->host copy",
+            "decode_equal": bool(same)}
 
 
 def cer_vs_ref(device):
@@ -132,6 +213,98 @@ def cer_vs_ref(device):
     return res
 
 
+def run_c2(args, world, rank, device):
+    """BASELINE configs[1] (C2): B=64 synthetic 32x256 crops, INFER forward +
+    CTC loss + greedy decode, fp32 (test.py:75-104's evaluation graph with the
+    greedy decoder of validate.py:81-92). One line, value = crops/s."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, model, validate
+    B, W = 64, 256
+    T = (W - 2) // 2 - 2
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
+    img, widths, labels = synthetic_batch(np.random.default_rng(1234 + rank), B, W, T, device)
+
+    def step():
+        with torch.no_grad():
+            feats, seq = model.convnet_layers(img, widths, model.INFER, store)
+            logits = model.rnn_layers(feats, seq, 95, store)
+            loss = model.ctc_loss_layer(logits, labels, seq, check=False)
+            dense = validate._get_output(logits, seq)[0]
+        return loss, dense
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, _ = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return {"metric": "line-crops/sec (fwd + CTC loss + greedy decode) at 32x256 bs=64",
+            "value": round(world * B * args.steps / elapsed, 2), "unit": "line-crops/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (uint8 crops, labels len U{2..19}; reference initialisers)",
+            "config": {"workload": "C2: INFER fwd + CTC loss + greedy, LSTM 512/512", "per_gpu_batch": B,
+                       "image": f"32x{W}", "parallelism": f"dp{world}"},
+            "loss": round(float(loss.item()), 4)}, elapsed, world * B * args.steps
+
+
+def run_c5(args, world, rank, device, n_crops=2048, beam=16):
+    """BASELINE configs[4] (C5): variable-width crops batched by the serving
+    path's 32-px width buckets (server.py:28-42,64-65: bucket (w, w+32], crops
+    right-padded with uint8 0 to its upper width), INFER forward + beam-16
+    decode per bucket, fp32. Whole buckets are sharded over the ranks (largest
+    first, round robin) -- replicas, no exchange. value = crops/s of
+    the whole job."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
+    rng = np.random.default_rng(20265)
+    true_w = rng.integers(65, 513, n_crops)
+    upper = ((true_w - 1) // 32 + 1) * 32                       # bucket (w, w + 32] -> its upper width
+    buckets = sorted({int(u) for u in upper}, key=lambda u: -int((upper == u).sum()))
+    mine = [u for i, u in enumerate(buckets) if i % world == rank]
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
+    batches = []
+    for u in mine:
+        idx = np.nonzero(upper == u)[0]
+        img = np.zeros((len(idx), 32, u, 1), np.uint8)
+        for j, i in enumerate(idx):
+            img[j, :, :true_w[i]] = rng.integers(0, 256, (32, true_w[i], 1))
+        batches.append((torch.from_numpy(img).to(device), torch.from_numpy(true_w[idx].astype(np.int32))))
+
+    def run():
+        out = []
+        for img, w in batches:
+            with torch.no_grad():
+                feats, seq = model.convnet_layers(img, w, model.INFER, store)
+                logits = model.rnn_layers(feats, seq, 95, store)
+                out.append(decode.ctc_beam_search_decoder_raw(logits, seq, beam_width=beam))
+        return out
+    for _ in range(max(1, args.warmup // 2)):
+        run()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = max(1, args.steps // 4)
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = (time.perf_counter() - t0) / reps
+    return {"metric": "line-crops/sec (bucketed 32x{64..512}, INFER + beam-16 decode)",
+            "value": round(n_crops / elapsed, 2), "unit": "line-crops/sec", "n_gpus": world, "steps": reps,
+            "warmup": max(1, args.warmup // 2), "ms_per_step": round(1e3 * elapsed, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic: {n_crops} uint8 crops, true widths U{{65..512}}, server-style 32-px buckets",
+            "config": {"workload": "C5: bucketed INFER + CTC beam search (beam 16), LSTM 512/512",
+                       "buckets": len(buckets), "crops": n_crops, "beam_width": beam,
+                       "parallelism": f"replicas x{world} (whole buckets per rank)"}}, elapsed, n_crops
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,7 +318,10 @@ def main():
                     help="graph: forward+backward captured once as a HIP graph and replayed per step "
                          "(all-reduce + Adam eager); eager: every launch issued from Python each step")
     ap.add_argument("--breakdown", action="store_true", help="per-entry-point event timing table on stderr")
-    ap.add_argument("--cpu-sample", type=int, default=8)
+    ap.add_argument("--cpu-sample", type=int, default=32, help="crops per CPU-baseline train step")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
+                    help="c3: the headline train step (default); c2: B=64 fp32 fwd+CTC+greedy; "
+                         "c5: bucketed 32x{64..512} crops, beam-16 decode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
@@ -159,6 +335,18 @@ def main():
     device = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+    if args.config in ("c2", "c5"):
+        res, elapsed, work = (run_c2 if args.config == "c2" else run_c5)(args, world, rank, device)
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        res["value"] = round(work / elapsed, 2)             # whole job over the slowest rank
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, _lib
     from cnn_lstm_ctc_ocr_amd.train import Trainer
@@ -291,6 +479,7 @@ def main():
         result["cer_vs_ref"] = cer_vs_ref(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+        result["c1_latency"] = c1_latency(device)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

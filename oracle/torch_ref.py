@@ -1,0 +1,125 @@
+"""PyTorch-CPU restatement of the reference graph -- the CPU BASELINE leg of
+bench.py only (BASELINE.md "CPU-baseline plan": TensorFlow 1.x cannot run
+here or on the GPU box, so the reference's CPU path is timed as this
+restatement of the same graph on the box's host cores).
+
+Test infrastructure: imported by bench.py's cpu_baseline / C1 legs and by
+tests/test_oracle.py, which checks it against the NumPy oracle (ref_model,
+pinned as described in DESIGN.md section 4) at a small shape -- so the timed
+graph is the oracle's graph. Never part of the product path.
+
+Graph (src/weinman/model_bu.py, the LSTM variant the bench times):
+  preprocess x*(1/255)-0.5 (validate.py:56-68) -> 8 x conv3x3 (model.py:84-109,
+  layer_params :47-54) with training-mode BatchNorm eps 1e-3 on conv2/4/6/8
+  (:118-123) + ReLU + max-pools (:111-116, :145) -> time-major features ->
+  2 x bidirectional TF1 LSTMCell (i,j,f,o gates, forget bias 1, :167-199) ->
+  dense + ReLU logits (:216-220) -> tf.nn.ctc_loss mean (:224-229, blank 95)
+  -> autograd backward -> TF1 Adam (train.py:101-141).
+Sequence-length masking is not restated: the baseline batches are full-width
+(every crop 32 x W, seq_len = T), where dynamic_rnn runs every step.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+LAYERS = [("conv1", 1, 32, "valid", False), ("conv2", 32, 32, "same", True), ("conv3", 32, 64, "same", False),
+          ("conv4", 64, 64, "same", True), ("conv5", 64, 128, "same", False), ("conv6", 128, 128, "same", True),
+          ("conv7", 128, 256, "same", False), ("conv8", 256, 256, "same", True)]
+POOLS = {"conv2": ((2, 2), (2, 2)), "conv4": ((2, 2), (2, 1)), "conv6": ((2, 2), (2, 1)), "conv8": ((3, 1), (3, 1))}
+
+
+class TorchRef:
+    """Parameters as torch CPU tensors under the TF variable names (the
+    oracle's init_params / the ParamStore layout: kernels HWIO / [in+H, 4H])."""
+
+    def __init__(self, params, rnn_sizes=(512, 512), dtype=torch.float32):
+        self.rnn_sizes = tuple(rnn_sizes)
+        self.dtype = dtype
+        self.p = {k: torch.tensor(v, dtype=dtype) for k, v in params.items()}
+        self.train_names = [k for k in self.p if not k.endswith(("moving_mean", "moving_variance"))]
+        for k in self.train_names:
+            self.p[k].requires_grad_(True)
+        self.m = {k: torch.zeros_like(self.p[k]) for k in self.train_names}
+        self.v = {k: torch.zeros_like(self.p[k]) for k in self.train_names}
+        self.step_count = 0
+
+    def forward(self, img_u8, training=True):
+        """img_u8 uint8 [B, 32, W, 1] -> logits [T, B, 96]."""
+        p = self.p
+        x = img_u8.permute(0, 3, 1, 2).float() * (1.0 / 255.0) - 0.5          # NCHW, float32 as TF
+        x = x.to(self.dtype)
+        for name, cin, cout, pad, bn in LAYERS:
+            w = p[f"convnet/{name}/kernel"].permute(3, 2, 0, 1)                   # HWIO -> OIHW
+            x = F.conv2d(x, w, p[f"convnet/{name}/bias"], padding=1 if pad == "same" else 0)
+            if bn:
+                pre = f"convnet/{name}/batch_norm"
+                x = F.batch_norm(x, p[pre + "/moving_mean"], p[pre + "/moving_variance"], p[pre + "/gamma"],
+                                 p[pre + "/beta"], training=training, momentum=0.01, eps=1e-3)
+                x = F.max_pool2d(F.relu(x), *POOLS[name])
+            else:
+                x = F.relu(x)
+        h = x[:, :, 0, :].permute(2, 0, 1)                                        # [T, B, 256]
+        for li, H in enumerate(self.rnn_sizes, start=1):
+            outs = []
+            for d, rev in (("fw", False), ("bw", True)):
+                k = p[f"rnn/bdrnn{li}/{d}/lstm_cell/kernel"]
+                b = p[f"rnn/bdrnn{li}/{d}/lstm_cell/bias"]
+                n_in = h.shape[2]
+                gx = h @ k[:n_in] + b                                             # [T, B, 4H] hoisted
+                wh = k[n_in:]
+                hs = h.new_zeros(h.shape[1], H)
+                cs = h.new_zeros(h.shape[1], H)
+                seq = []
+                for t in (range(h.shape[0] - 1, -1, -1) if rev else range(h.shape[0])):
+                    z = gx[t] + hs @ wh
+                    i, j, f, o = z.chunk(4, dim=1)
+                    cs = torch.sigmoid(f + 1.0) * cs + torch.sigmoid(i) * torch.tanh(j)
+                    hs = torch.sigmoid(o) * torch.tanh(cs)
+                    seq.append(hs)
+                if rev:
+                    seq.reverse()
+                outs.append(torch.stack(seq))
+            h = torch.cat(outs, dim=2)
+        return F.relu(h @ p["rnn/logits/kernel"] + p["rnn/logits/bias"])
+
+    def loss(self, logits, labels, label_len):
+        """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised)."""
+        T, B, _ = logits.shape
+        lp = F.log_softmax(logits, dim=2)
+        seq = torch.full((B,), T, dtype=torch.long)
+        return F.ctc_loss(lp, labels, seq, label_len, blank=logits.shape[2] - 1, reduction="sum") / B
+
+    def train_step(self, img_u8, labels, label_len, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8):
+        """Forward, backward and one TF1 Adam update; returns the loss."""
+        for k in self.train_names:
+            self.p[k].grad = None
+        loss = self.loss(self.forward(img_u8, True), labels, label_len)
+        loss.backward()
+        self.step_count += 1
+        t = self.step_count
+        lr_t = lr * math.sqrt(1 - beta2 ** t) / (1 - beta1 ** t)
+        with torch.no_grad():
+            for k in self.train_names:
+                g = self.p[k].grad
+                self.m[k].mul_(beta1).add_(g, alpha=1 - beta1)
+                self.v[k].mul_(beta2).addcmul_(g, g, value=1 - beta2)
+                self.p[k].sub_(lr_t * self.m[k] / (self.v[k].sqrt() + eps))
+        return float(loss.detach())
+
+    def greedy(self, img_u8):
+        """validate._get_output (validate.py:81-92) on CPU: INFER forward +
+        greedy decode (first max, merge repeats, drop blank)."""
+        with torch.no_grad():
+            logits = self.forward(img_u8, training=False)
+        best = logits.argmax(dim=2).t()                                           # [B, T]
+        blank = logits.shape[2] - 1
+        out = []
+        for row in best.tolist():
+            seq, prev = [], -1
+            for k in row:
+                if k != blank and k != prev:
+                    seq.append(k)
+                prev = k
+            out.append(seq)
+        return out

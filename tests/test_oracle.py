@@ -425,3 +425,37 @@ def test_train_step_runs_and_updates():
     assert np.isfinite(loss)
     assert not np.allclose(newp["rnn/logits/kernel"], params["rnn/logits/kernel"])
     assert not np.allclose(newp["convnet/conv2/batch_norm/moving_mean"], 0)
+
+
+def test_torch_cpu_restatement_matches_oracle():
+    """oracle/torch_ref.py (the timed CPU baseline of bench.py) computes the
+    oracle's graph: TRAIN-mode loss, logits-layer and conv1 gradients, and one
+    TF1 Adam update, at a small full-width shape."""
+    import torch
+
+    from oracle.torch_ref import TorchRef
+    rng = np.random.default_rng(9)
+    sizes = (32, 32)
+    vals = M.init_params(seed=3, rnn_sizes=sizes)
+    for k in vals:
+        if "lstm_cell/kernel" in k:
+            vals[k] = (vals[k] * 20).astype(np.float32)
+    B, W = 3, 64
+    img = rng.integers(0, 256, (B, 32, W, 1)).astype(np.uint8)
+    widths = np.full(B, W, np.int32)
+    labels = [list(rng.integers(0, 95, n)) for n in (3, 5, 4)]
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", sizes)
+    loss_ref, grads_ref, _, logits_ref, _ = ref.loss_and_grads(G.preprocess(img).astype(np.float64), widths, labels)
+    tr = TorchRef(vals, sizes, dtype=torch.float64)
+    lab = torch.zeros(B, 5, dtype=torch.long)
+    for i, l in enumerate(labels):
+        lab[i, :len(l)] = torch.tensor(l)
+    ln = torch.tensor([len(l) for l in labels])
+    logits = tr.forward(torch.from_numpy(img), True)
+    np.testing.assert_allclose(logits.detach().numpy(), logits_ref, rtol=1e-9, atol=1e-9)
+    loss = tr.loss(logits, lab, ln)
+    loss.backward()
+    assert abs(loss.item() - loss_ref) < 1e-9 * abs(loss_ref)
+    for name in ("rnn/logits/kernel", "rnn/bdrnn1/bw/lstm_cell/kernel", "convnet/conv8/batch_norm/gamma",
+                 "convnet/conv1/kernel"):
+        np.testing.assert_allclose(tr.p[name].grad.numpy(), grads_ref[name], rtol=1e-7, atol=1e-10, err_msg=name)
