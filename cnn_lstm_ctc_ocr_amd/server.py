@@ -139,6 +139,8 @@ class LocalServer:
             self.buckets.insert(0, Bucket(bucket_max_time, bucket_size, (0, BUCKET_STEP)))
         self.maxclientid = 0
         self.batches_run = 0
+        self._inflight = {}                # batch id -> infos (asynchronous recognizers)
+        self._next_batch = 0
 
     def _queue(self):
         return self.manager.Queue() if self.manager is not None else queue.Queue()
@@ -168,21 +170,46 @@ class LocalServer:
             got = True
         return got
 
+    def _deliver(self, infos, texts):
+        for (clientid, imgid), txt in zip(infos, texts):
+            if clientid == "-1":
+                continue
+            self.client_outputs[clientid].put((imgid, txt), block=False)
+
     def flush_buckets(self, now=None):
-        """Run every bucket that is ready; returns the number of batches run."""
+        """Run every bucket that is ready; returns the number of batches run
+        (submitted, for an asynchronous recognizer such as ReplicaPool)."""
         n = 0
-        for bucket in self.buckets:
+        for bi, bucket in enumerate(self.buckets):
             b = bucket.getBatch(now)
             if b is None:
                 continue
             infos, batch, widths = fill_batch(*b, self.bucket_size)
-            texts = self.recognizer(batch, widths)
-            for (clientid, imgid), txt in zip(infos, texts):
-                if clientid == "-1":
-                    continue
-                self.client_outputs[clientid].put((imgid, txt), block=False)
+            if hasattr(self.recognizer, "submit"):
+                bid = self._next_batch
+                self._next_batch += 1
+                self._inflight[bid] = infos
+                self.recognizer.submit(bi, bid, batch, widths)
+            else:
+                self._deliver(infos, self.recognizer(batch, widths))
             n += 1
         self.batches_run += n
+        self.collect()
+        return n
+
+    def collect(self, block=False):
+        """Forward the results an asynchronous recognizer has finished
+        (block=True: wait until every submitted batch is back)."""
+        if not hasattr(self.recognizer, "poll"):
+            return 0
+        n = 0
+        while self._inflight:
+            done = self.recognizer.poll(block=block)
+            if not done:
+                break
+            for bid, texts in done:
+                self._deliver(self._inflight.pop(bid), texts)
+                n += 1
         return n
 
     def run(self, states=None, logger=None, stop=None, idle_sleep=0.1):
@@ -195,10 +222,116 @@ class LocalServer:
             try:
                 self.poll_inputs(idle_sleep)
                 self.flush_buckets()
+                self.collect()
             except Exception:
                 if logger is None:
                     raise
                 logger.exception("SERVER ERROR")
+
+
+# ------------------------------------------------------- multi-GPU replicas
+def _replica_main(rank, device, make_recognizer, inq, outq):
+    """Worker process of a ReplicaPool: one recognizer on one device; batches
+    in, (batch id, texts) out, until a None item arrives."""
+    rec = make_recognizer(device)
+    outq.put(("ready", rank))
+    while True:
+        item = inq.get()
+        if item is None:
+            break
+        bid, batch, widths = item
+        try:
+            outq.put((bid, list(rec(batch, widths))))
+        except Exception as e:                        # reported to the server, which raises
+            outq.put((bid, e))
+    outq.put(("exit", rank))
+
+
+def gpu_recognizer(cfg=None, checkpoint=None, seed=0, decoder="greedy", beam_width=16):
+    """A make_recognizer for ReplicaPool: a Recognizer whose ParamStore is
+    built on the replica's device (restored from a TF1 checkpoint, or the
+    reference initialisers with `seed`). Picklable (spawn)."""
+    return _GpuRecognizerFactory(cfg, checkpoint, seed, decoder, beam_width)
+
+
+class _GpuRecognizerFactory:
+    def __init__(self, cfg, checkpoint, seed, decoder, beam_width):
+        self.cfg, self.checkpoint, self.seed, self.decoder, self.beam_width = cfg, checkpoint, seed, decoder, beam_width
+
+    def __call__(self, device):
+        from .config import ModelConfig
+        from .params import ParamStore
+        store = ParamStore(self.cfg or ModelConfig(dtype=torch.float32), device=device, seed=self.seed)
+        if self.checkpoint:
+            from . import checkpoint as ckpt
+            ckpt.restore(store, self.checkpoint)
+        return Recognizer(store, decoder=self.decoder, beam_width=self.beam_width)
+
+
+class ReplicaPool:
+    """Data-parallel recognise step over several GPUs (inference and
+    decode are replicas, no exchange), one worker PROCESS per device. The
+    LocalServer stays the single bucketing front end (server.py:59-145, with
+    the page workers as its clients, ocr-app.py:186-193); each ready batch is
+    sent whole to replica (bucket index mod replicas), so a width bucket -- one
+    input shape -- always lands on the same GPU. submit / poll make the
+    LocalServer asynchronous: batches of different buckets run on their GPUs
+    concurrently. `devices`: e.g. ["cuda:0", ..., "cuda:7"]."""
+
+    def __init__(self, devices, make_recognizer, start_method="spawn", timeout=600.0):
+        import multiprocessing as mp
+        ctx = mp.get_context(start_method)
+        self.devices = list(devices)
+        self.outq = ctx.Queue()
+        self.inqs = [ctx.Queue() for _ in self.devices]
+        self.procs = [ctx.Process(target=_replica_main, args=(r, d, make_recognizer, self.inqs[r], self.outq),
+                                  daemon=True) for r, d in enumerate(self.devices)]
+        for pr in self.procs:
+            pr.start()
+        ready = 0
+        while ready < len(self.procs):
+            tag, _ = self.outq.get(timeout=timeout)
+            if tag == "ready":
+                ready += 1
+        self.assigned = {}                                   # batch id -> replica (diagnostics)
+
+    def replica_of(self, bucket_index):
+        return bucket_index % len(self.procs)
+
+    def submit(self, bucket_index, batch_id, batch, widths):
+        r = self.replica_of(bucket_index)
+        self.assigned[batch_id] = r
+        self.inqs[r].put((batch_id, np.ascontiguousarray(batch), np.asarray(widths, np.int32)))
+
+    def poll(self, block=False, timeout=600.0):
+        """Finished (batch id, texts) pairs (waits for one when block)."""
+        out = []
+        try:
+            item = self.outq.get(timeout=timeout) if block else self.outq.get_nowait()
+        except queue.Empty:
+            return out
+        while True:
+            bid, texts = item
+            if isinstance(texts, Exception):
+                raise RuntimeError(f"replica {self.assigned.get(bid)} failed on batch {bid}") from texts
+            out.append((bid, texts))
+            try:
+                item = self.outq.get_nowait()
+            except queue.Empty:
+                return out
+
+    def close(self):
+        for q in self.inqs:
+            q.put(None)
+        for pr in self.procs:
+            pr.join(timeout=60)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
 
 def predict_signature(store, images, width, beam_width=128, top_paths=3, merge_repeated=False):

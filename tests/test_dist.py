@@ -63,3 +63,56 @@ def test_single_process_scale_is_one():
     from cnn_lstm_ctc_ocr_amd.train import allreduce_mean_scale
     t = torch.ones(4)
     assert allreduce_mean_scale(t) == 1.0 and torch.equal(t, torch.ones(4))
+
+
+def _bucket_worker(rank, world, port, out):
+    """The Trainer's bucketed all-reduce over a real ParamStore flat layout:
+    the recurrent bucket is started mid-"backward" (the hook), the conv
+    bucket after it; the result and the Adam grad_scale must equal the mean
+    gradient of the concatenated batch."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(32, 32), dtype=torch.float32), device="cpu", seed=1)
+    tr = Trainer(store)
+    g = store.flat_grad
+    split = tr.buckets.split
+    rng = np.random.default_rng(500 + rank)
+    rnn_part = torch.from_numpy(rng.standard_normal(g.numel() - split).astype(np.float32))
+    conv_part = torch.from_numpy(rng.standard_normal(split).astype(np.float32))
+    g[split:].copy_(rnn_part)                   # the recurrent + logits backward wrote its bucket ...
+    tr.buckets.rnn_ready()                      # ... the hook starts its all-reduce
+    g[:split].copy_(conv_part)                  # the conv tower's backward
+    scale = tr.reduce_gradients()
+    out[rank] = (g.numpy().copy(), scale, split, store.offsets["rnn/bdrnn1/fw/lstm_cell/kernel"][1])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_over_paramstore_layout():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, port, out), nprocs=world, join=True)
+    g0, s0, split, first_rnn = out[0]
+    g1, s1, _, _ = out[1]
+    assert split == first_rnn                   # the conv tower sits in front of the recurrent bucket
+    parts = []
+    for r in range(world):
+        rng = np.random.default_rng(500 + r)
+        rnn = rng.standard_normal(g0.size - split).astype(np.float32)
+        conv = rng.standard_normal(split).astype(np.float32)
+        parts.append(np.concatenate([conv, rnn]))
+    total = sum(parts)
+    np.testing.assert_allclose(g0, total, rtol=1e-6)
+    np.testing.assert_allclose(g1, total, rtol=1e-6)
+    assert s0 == s1 == 0.5
+    # Adam (the kernel receives grad_scale) on the summed gradient == Adam on the global mean
+    mean = sum(p.astype(np.float64) for p in parts) / world
+    p_ = np.zeros_like(mean)
+    a, _, _ = G.adam_update(p_.copy(), total.astype(np.float64) * s0, np.zeros_like(mean), np.zeros_like(mean),
+                            1e-4, 1)
+    b, _, _ = G.adam_update(p_.copy(), mean, np.zeros_like(mean), np.zeros_like(mean), 1e-4, 1)
+    np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-12)

@@ -68,3 +68,34 @@ def test_service_end_to_end_on_gpu(cuda):
         x = np.zeros((1, 32, bw, 1), np.uint8)
         x[0, :, :w, 0] = c
         assert rec(x, np.array([w], np.int32))[0] == got[i], i
+
+
+def test_replica_pool_on_gpu_matches_single_recognizer(cuda):
+    """Two replica PROCESSES (both on cuda:0 here; one per GPU in production)
+    behind one LocalServer give the single in-process Recognizer's strings."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig
+    from cnn_lstm_ctc_ocr_amd.server import LocalServer, Recognizer, ReplicaPool, gpu_recognizer
+    cfg = ModelConfig(rnn_sizes=SIZES, dtype=torch.float32)
+    rng = np.random.default_rng(8)
+    widths = [int(w) for w in rng.integers(40, 300, 24)]
+    crops = [rng.integers(0, 256, (32, w), dtype=np.uint8) for w in widths]
+
+    def serve(rec):
+        srv = LocalServer(rec, bucket_size=4, bucket_max_time=0.0)
+        cid, _, outq = srv.register()
+        for i, c in enumerate(crops):
+            srv.addImage(cid, i, 0.0, c)
+        for k in range(12):
+            srv.flush_buckets(now=1e9 + k)
+        srv.collect(block=True)
+        got = {}
+        while not outq.empty():
+            i, t = outq.get()
+            got[i] = t
+        return got
+
+    from cnn_lstm_ctc_ocr_amd import ParamStore
+    single = serve(Recognizer(ParamStore(cfg, device=cuda, seed=4)))
+    with ReplicaPool(["cuda:0", "cuda:0"], gpu_recognizer(cfg, seed=4)) as pool:
+        multi = serve(pool)
+    assert sorted(single) == list(range(len(crops))) and multi == single

@@ -88,3 +88,43 @@ def test_service_round_trip_with_stand_in_recogniser():
     for shape, widths in seen:
         assert shape[0] == 4 and len(widths) == 4
         assert shape[2] % 32 == 0 and all(shape[2] - 32 < w <= shape[2] for w in widths)
+
+
+class _FakeRecognizerFactory:
+    """Picklable make_recognizer for ReplicaPool on CPU: the 'text' of a crop
+    encodes its true width and the replica's device, so the test can check
+    routing and delivery without a GPU."""
+
+    def __call__(self, device):
+        def rec(batch, widths):
+            return [f"{device}:{int(w)}" for w in widths]
+        return rec
+
+
+def test_replica_pool_routes_whole_buckets_and_delivers():
+    """Multi-replica recognise step (one worker process per device; whole
+    width buckets per replica): every crop's result reaches its
+    client, and a bucket always maps to the same replica."""
+    import numpy as np
+
+    from cnn_lstm_ctc_ocr_amd.server import LocalServer, ReplicaPool
+    rng = np.random.default_rng(3)
+    with ReplicaPool(["dev0", "dev1", "dev2"], _FakeRecognizerFactory()) as pool:
+        srv = LocalServer(pool, bucket_size=4, bucket_max_time=0.0)
+        cid, inq, outq = srv.register()
+        widths = [int(w) for w in rng.integers(33, 400, 40)]
+        for i, w in enumerate(widths):
+            srv.addImage(cid, i, 0.0, rng.integers(0, 256, (32, w), dtype=np.uint8))
+        for k in range(20):                              # the clock advances (bucket release, server.py:45,52)
+            srv.flush_buckets(now=1e9 + k)
+        srv.collect(block=True)
+        got = {}
+        while not outq.empty():
+            imgid, txt = outq.get()
+            got[imgid] = txt
+        assert sorted(got) == list(range(len(widths)))
+        for i, w in enumerate(widths):
+            dev, tw = got[i].split(":")
+            assert int(tw) == w
+            bucket = (w - 1) // 32 - 1                      # buckets (w, w+32] from w = 32
+            assert dev == f"dev{pool.replica_of(bucket)}"
