@@ -79,6 +79,10 @@ int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
 // -1 when it does not cover the call. OCRK_GEMM_PP=0 disables it.
 int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
+// 8-wave ping-pong engine for A_COLK x B_KN weight gradients (gemm_pptn.hip),
+// f32 C or split-K partials, M, N >= 256. -1 when not covered (OCRK_GEMM_PPTN=0).
+int gemm_pptn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+
 // Plain A_ROWK x B_NK bf16 GEMMs with a bf16 C and at most a bias epilogue
 // on hipBLASLt (blaslt.hip). Returns -1 when not covered. OCRK_BLASLT=0 disables it.
 int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);

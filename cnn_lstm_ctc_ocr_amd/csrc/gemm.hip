@@ -435,6 +435,7 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     const int lt = gemm_blaslt(p, amode, bmode, dtype, stream);     // whole K in one library call
     if (lt >= 0) return lt;
     nt = gemm_nt(p, amode, bmode, dtype, stream);
+    if (nt < 0) nt = gemm_pptn(p, amode, bmode, dtype, stream);
     if (nt < 0) nt = gemm_tn(p, amode, bmode, dtype, stream);
     if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     if (dtype == OCRK_BF16) return dispatch_modes<bf16>(p, amode, bmode, stream);

@@ -314,6 +314,13 @@ class _BiGRU(torch.autograd.Function):
 
 
 def _splits(M, N, Kdim):
+    """K slices for a weight-gradient GEMM (f32 partials + a fixed-order
+    reduce): enough items for the chip. M, N >= 256 run on the 256 x 256
+    ping-pong TN engine (one item per CU, slices of >= 1024 rows), smaller
+    outputs on the 128 x 128 engine (~2 items per CU, >= 2048 rows)."""
+    if M >= 256 and N >= 256:
+        tiles = -(-M // 256) * -(-N // 256)
+        return int(max(1, min(-(-256 // tiles), Kdim // 1024)))
     tiles = -(-M // 128) * -(-N // 128)
     return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
 

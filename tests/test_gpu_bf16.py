@@ -100,18 +100,24 @@ def test_bf16_plain_gemms_bias_bf16_out(cuda, M_, N, K, tag):
     assert np.all(err <= 2 ** -8 * np.abs(ref) + 1e-3 * np.abs(ref).max()), tag
 
 
-def test_bf16_tn_weight_gradient_recurrent_shape(cuda):
-    """dW_x = x^T . dG over T*B rows (split-K TN engine, f32 accumulate)."""
+@pytest.mark.parametrize("R,n_in,G4,splits,col", [(8000, 1024, 2048, 4, 0), (8000, 512, 2048, 8, 2048),
+                                                   (8000, 256, 2048, 1, 0), (8000, 1024, 96, 3, 0),
+                                                   (1000, 264, 296, 2, 8)])
+def test_bf16_tn_weight_gradient_recurrent_shape(cuda, R, n_in, G4, splits, col):
+    """dW = x^T . dG[:, col:col+G4] over T*B rows (the weight-gradient TN
+    engines: ping-pong 256 x 256 for M, N >= 256, else 128-wide), split K and
+    in-place f32 accumulation, ragged edges."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    rng = np.random.default_rng(3)
-    R, n_in, G4 = 8000, 1024, 2048
+    rng = np.random.default_rng(3 + n_in)
+    ld = max(2 * G4, col + G4)
     x = _bf(rng.standard_normal((R, n_in)))
-    dG = _bf(rng.standard_normal((R, 2 * G4)))
-    ref = x.astype(np.float64).T @ dG[:, :G4].astype(np.float64)
-    gk = torch.zeros(n_in, G4, device=cuda)
+    dG = _bf(rng.standard_normal((R, ld)))
+    prev = rng.standard_normal((n_in, G4)).astype(np.float32)
+    ref = prev + x.astype(np.float64).T @ dG[:, col:col + G4].astype(np.float64)
+    gk = torch.from_numpy(prev).to(cuda)
     xd, dGd = torch.from_numpy(x).to(cuda).bfloat16(), torch.from_numpy(dG).to(cuda).bfloat16()
-    Kn.gemm(xd, dGd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in, ldb=2 * G4, ldc=G4,
-            splits=4)
+    Kn.gemm(xd, dGd[:, col:], trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in, ldb=ld, ldc=G4,
+            splits=splits)
     assert _rel(gk.cpu().numpy(), ref) < 1e-5
 
 

@@ -8,8 +8,8 @@ tag=${1:?tag}
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-cmd=(python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline)
-pmc=(python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline)
+cmd=(python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cer)
+pmc=(python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-cer)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- "${cmd[@]}" \
     > "$out/trace.log" 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- "${pmc[@]}" \
