@@ -98,7 +98,10 @@ def _cpu_batch(rng, B, W):
     return img, lab.long(), ln.long()
 
 
-def cpu_baseline(sample, warmup=3, steps=10):
+RNN_SIZES = {"lstm": (512, 512), "gru": (512, 256)}     # model_bu.py (bench default) / model.py
+
+
+def cpu_baseline(sample, warmup=3, steps=10, cell="lstm"):
     """BASELINE.md CPU-baseline plan: the reference graph's train step (conv ->
     BiLSTM 512/512 -> CTC -> TF1 Adam) as the PyTorch-CPU restatement
     (oracle/torch_ref.py, checked against the NumPy oracle in
@@ -111,7 +114,8 @@ def cpu_baseline(sample, warmup=3, steps=10):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        ref = TorchRef(M.init_params(seed=0), (512, 512))
+        sizes = RNN_SIZES[cell]
+        ref = TorchRef(M.init_params(seed=0, cell=cell, rnn_sizes=sizes), sizes, cell=cell)
         img, lab, ln = _cpu_batch(np.random.default_rng(20260), sample, 256)
         for _ in range(warmup):
             ref.train_step(img, lab, ln)
@@ -126,7 +130,7 @@ def cpu_baseline(sample, warmup=3, steps=10):
     return {"value": round(sample * steps / dt, 3), "unit": "line-crops/sec", "cores": threads, "kind": "port",
             "cpu": model,
             "sample": f"reference graph on CPU (PyTorch restatement oracle/torch_ref.py; TF1 unavailable): "
-                      f"{warmup} warm-up + {steps} timed train steps (fp32, LSTM 512/512, Adam) on {sample} "
+                      f"{warmup} warm-up + {steps} timed train steps (fp32, {cell.upper()} {sizes[0]}/{sizes[1]}, Adam) on {sample} "
                       f"synthetic 32x256 crops, {threads} threads, {dt:.1f} s"}
 
 
@@ -322,6 +326,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
                     help="c3: the headline train step (default); c2: B=64 fp32 fwd+CTC+greedy; "
                          "c5: bucketed 32x{64..512} crops, beam-16 decode")
+    ap.add_argument("--cell", default="lstm", choices=["lstm", "gru"],
+                    help="lstm: model_bu.py's BiLSTM 512/512 (BASELINE.json's config); gru: model.py's BiGRU 512/256")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
@@ -354,7 +360,8 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     B, W = args.batch, args.width
     T = (W - 2) // 2 - 2
-    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=dtype), device=device, seed=0)
+    sizes = RNN_SIZES[args.cell]
+    store = ParamStore(ModelConfig(cell=args.cell, rnn_sizes=sizes, dtype=dtype), device=device, seed=0)
     trainer = Trainer(store)
     rng = np.random.default_rng(1234 + rank)                # per-rank seed = base + rank
     img, widths, labels = synthetic_batch(rng, B, W, T, device)
@@ -455,7 +462,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
         "data": "synthetic (uint8 crops U{0..255}, labels len U{2..19}; random-init weights, reference initialisers)",
-        "config": {"workload": "C3: train step (conv+BiLSTM+CTC grad+Adam), LSTM 512/512 (model_bu.py)",
+        "config": {"workload": "C3: train step (conv+BiLSTM+CTC grad+Adam), LSTM 512/512 (model_bu.py)"
+                   if args.cell == "lstm" else
+                   "C3 with model.py's cell: train step (conv+BiGRU+CTC grad+Adam), GRU 512/256 (model.py)",
                    "execution": "hipGraph replay of fwd+bwd, eager all-reduce + Adam" if args.mode == "graph"
                    else "eager launches",
                    "global_batch": B * world, "per_gpu_batch": B, "image": f"32x{W}", "seq_len": T,
@@ -475,11 +484,12 @@ def main():
         result["roofline"]["traffic"] = pmc["bytes_per_launch"]
         result["roofline"]["traffic_unit"] = "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
         result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
-    if rank == 0 and not args.no_cer:
+    if rank == 0 and not args.no_cer and args.cell == "lstm":      # the golden decodes are of the LSTM model
         result["cer_vs_ref"] = cer_vs_ref(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample)
-        result["c1_latency"] = c1_latency(device)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, cell=args.cell)
+        if args.cell == "lstm":
+            result["c1_latency"] = c1_latency(device)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

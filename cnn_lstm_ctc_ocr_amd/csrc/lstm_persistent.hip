@@ -30,25 +30,12 @@
 // the kernel records an error word and runs to completion (no hang).
 #include "common.h"
 #include "mfma_util.h"
+#include "persist.h"
 #include "recur.h"
 
 using namespace ocrk;
 
 namespace {
-
-constexpr int PBR = 32, PHU = 32;          // batch rows, hidden units per workgroup
-typedef __attribute__((address_space(1))) unsigned gu32;            // hand-off words: global, never flat
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-// polls (with s_sleep) before a hand-off wait gives up: OCRK_LSTM_SPIN_LIMIT
-// (tests force tiny limits), default 1 << 22; the launch passes it in.
-
-__device__ __forceinline__ unsigned short bf16_bits(float x) {
-    bf16 b = (bf16)x;
-    return __builtin_bit_cast(unsigned short, b);
-}
-__device__ __forceinline__ float bits_f(unsigned short u) {
-    return __uint_as_float((unsigned)u << 16);
-}
 
 // diagnostics (ocrk_lstm_debug_stamps): thread 0 stamps step 64 (slots 0-5) and the top of step 65 (slot 6)
 __device__ __forceinline__ void pstamp(long long* dbg, int s, int i) {
@@ -56,84 +43,11 @@ __device__ __forceinline__ void pstamp(long long* dbg, int s, int i) {
         dbg[(int64_t)blockIdx.x * 8 + (s == 65 ? 6 : i)] = __builtin_amdgcn_s_memrealtime();
 }
 
-// workgroup -> (group, member): members of a group share blockIdx % 8 when the
-// grid allows it (speed only)
-__device__ __forceinline__ void persistent_role(int ngroups, int nu, int& group, int& member) {
-    const int id = blockIdx.x, grid = ngroups * nu;
-    if (grid % 8 == 0 && (grid / 8) % nu == 0) {
-        const int per = grid / 8, j = id / 8;
-        group = (id % 8) * (per / nu) + j / nu;
-        member = j % nu;
-    } else {
-        group = id / nu;
-        member = id % nu;
-    }
-}
-
-// Are all members of this workgroup's group on ONE XCD? Each workgroup posts
-// its HW_REG_XCC_ID (+1) once per launch (sc1), wave 0 waits for the group's
-// posts and compares. Placement is the dispatcher's choice: it is measured
-// here, never assumed. On one XCD the group's hand-offs stay in that XCD's L2
-// (plain stores keep the lines in L2; nt loads bypass only the reader's L1);
-// otherwise they use the placement-independent sc1 form.
-__device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member, unsigned* err, unsigned spin_limit,
-                                                 int* s_flag) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) {
-        unsigned x;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-        __hip_atomic_store(xtab + member, (x & 15u) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < 64) {
-        unsigned v = 1u, spins = 0;
-        while (true) {
-            if (lane < nu) v = __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__all(v != 0u)) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > spin_limit) {
-                if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_CENSUS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        const unsigned first = __shfl(v, 0, 64);
-        const bool same = __all(lane >= nu || v == first);
-        if (lane == 0) *s_flag = same ? 1 : 0;
-    }
-    __syncthreads();
-    return *s_flag != 0;
-}
-
-// The two hand-off forms (see group_on_one_xcd): flag poll, flag raise,
-// 8-B payload store, 16-B payload load.
-__device__ __forceinline__ unsigned poll_word(gu32* p, bool local) {
-    if (local) {
-        asm volatile("" ::: "memory");
-        return __builtin_nontemporal_load(p);
-    }
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void raise_flag(gu32* p, unsigned v, bool local) {
-    if (local) *p = v;
-    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void put8(gu64* p, unsigned long long v, bool local) {
-    if (local) *p = v;
-    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32x4 get16(__amdgpu_buffer_rsrc_t r, int off, bool local) {
-    return local ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2))     // nt
-                 : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));   // sc1
-}
-
 }  // namespace
 
 extern long long* g_lstm_dbg;
 
-static unsigned lstm_spin_limit() {
-    const char* e = getenv("OCRK_LSTM_SPIN_LIMIT");      // read per launch: tests force tiny limits
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (unsigned)v : (1u << 22);
-}
+static unsigned lstm_spin_limit() { return recur_spin_limit(); }
 
 // KS = H / 32 k-steps
 template <int KS>

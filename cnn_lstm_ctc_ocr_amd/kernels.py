@@ -297,12 +297,40 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
 
 
 # ------------------------------------------------------------------- GRU
+_GRU_PERSISTENT = {}
+
+
+def gru_persistent_ok(B, H, dtype):
+    """Run the bf16 GRU time loops as persistent launches (csrc/gru_persistent.hip)?
+    Same rule and switch as the LSTM: B % 32 == 0, H in {256, 512}, the grid
+    co-resident; OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
+    import os
+    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
+        return False
+    key = (B, H)
+    if key not in _GRU_PERSISTENT:
+        lib = _lib.lib()
+        _GRU_PERSISTENT[key] = bool(lib.ocrk_gru_fwd_persistent_supported(B, H)) and \
+            bool(lib.ocrk_gru_bwd_persistent_supported(B, H))
+    return _GRU_PERSISTENT[key]
+
+
 def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
     """Returns out [T,B,2H], hprev_t, rh_t [T,B,2,H], acts_t [T,B,2,3H] (dtype)."""
     _chk(gx, whgT, whcT, seq_len)
     if gx.dtype != dtype or whgT.dtype != dtype:
         raise TypeError(f"gru_fwd: gx and weights must be {dtype} (got {gx.dtype}, {whgT.dtype})")
     dev = gx.device
+    if gru_persistent_ok(B, H, dtype):
+        out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+        hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+        rh_t = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+        acts = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
+        nb = _lib.lib().ocrk_gru_fwd_persistent_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        call("ocrk_gru_fwd_persistent", ptr(gx), ptr(whgT), ptr(whcT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
+             ptr(rh_t), ptr(acts), ptr(status_word(dev)), ptr(ws), nb, _stream(gx))
+        return out, hprev, rh_t, acts
     h = torch.zeros(2, B, H, dtype=dtype, device=dev)
     rh = torch.empty(2, B, H, dtype=dtype, device=dev)
     out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
@@ -319,6 +347,13 @@ def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H):
     _chk(whg, whc, seq_len, dout, hprev, acts)
     dtype = dout.dtype
     dev = dout.device
+    if gru_persistent_ok(B, H, dtype):
+        dG = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
+        nb = _lib.lib().ocrk_gru_bwd_persistent_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        call("ocrk_gru_bwd_persistent", ptr(whg), ptr(whc), ptr(seq_len), T, B, H, ptr(dout), ptr(hprev), ptr(acts),
+             ptr(dG), ptr(status_word(dev)), ptr(ws), nb, _stream(dout))
+        return dG
     dzg = torch.empty(2, B, 2 * H, dtype=dtype, device=dev)
     dzc = torch.empty(2, B, H, dtype=dtype, device=dev)
     dh_tot = torch.empty(2, B, H, dtype=torch.float32, device=dev)

@@ -229,6 +229,24 @@ int ocrk_gru_fwd(const void* gx, const void* whgT, const void* whcT, void* h, vo
 int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* dzc, float* dh_tot, float* direct,
                  const int* seq_len, int T, int B, int H, const void* dout, const void* hprev_t,
                  const void* acts_t, void* dG_t, int dtype, void* stream);
+/* Persistent GRU time loops (bf16, H in {256, 512}, B % 32 == 0): ONE launch runs
+ * all T steps of both directions (forward) or all T reverse steps (BPTT), the
+ * member's W_h slices in registers. The reset gate multiplies h before the
+ * candidate matmul, so a step has two group-wide exchanges (r*h, then h; in
+ * BPTT dz_c, then dz_r/dz_u). Same outputs as ocrk_gru_fwd / ocrk_gru_bwd
+ * without the state/scratch buffers; err: the device status word
+ * (OCRK_STATUS_LSTM_FWD_TIMEOUT / _BWD_TIMEOUT / _CENSUS, bounded by
+ * OCRK_LSTM_SPIN_LIMIT as for the LSTM loops). */
+int ocrk_gru_fwd_persistent_supported(int B, int H);
+size_t ocrk_gru_fwd_persistent_workspace_size(int B, int H);
+int ocrk_gru_fwd_persistent(const void* gx, const void* whgT, const void* whcT, const int* seq_len, int T, int B,
+                            int H, void* out, void* hprev_t, void* rh_t, void* acts_t, unsigned* err, void* ws,
+                            size_t ws_bytes, void* stream);
+int ocrk_gru_bwd_persistent_supported(int B, int H);
+size_t ocrk_gru_bwd_persistent_workspace_size(int B, int H);
+int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
+                            const void* dout, const void* hprev_t, const void* acts_t, void* dG_t, unsigned* err,
+                            void* ws, size_t ws_bytes, void* stream);
 int ocrk_lstm_fwd(const void* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
                   int T, int B, int H, void* out, void* hprev_t, float* cprev_t, void* acts_t, int dtype,
                   void* stream);

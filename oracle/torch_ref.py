@@ -8,11 +8,14 @@ tests/test_oracle.py, which checks it against the NumPy oracle (ref_model,
 pinned as described in DESIGN.md section 4) at a small shape -- so the timed
 graph is the oracle's graph. Never part of the product path.
 
-Graph (src/weinman/model_bu.py, the LSTM variant the bench times):
+Graph (src/weinman/model_bu.py, the LSTM variant the default bench times;
+cell="gru" restates src/weinman/model.py's GRUCell layers for bench --cell gru):
   preprocess x*(1/255)-0.5 (validate.py:56-68) -> 8 x conv3x3 (model.py:84-109,
   layer_params :47-54) with training-mode BatchNorm eps 1e-3 on conv2/4/6/8
   (:118-123) + ReLU + max-pools (:111-116, :145) -> time-major features ->
-  2 x bidirectional TF1 LSTMCell (i,j,f,o gates, forget bias 1, :167-199) ->
+  2 x bidirectional TF1 LSTMCell (i,j,f,o gates, forget bias 1, :167-199) or
+  GRUCell ([r,u] = sig([x,h] Wg + bg); c = tanh([x, r*h] Wc + bc);
+  h' = u h + (1-u) c; model.py:167-199, 213-214) ->
   dense + ReLU logits (:216-220) -> tf.nn.ctc_loss mean (:224-229, blank 95)
   -> autograd backward -> TF1 Adam (train.py:101-141).
 Sequence-length masking is not restated: the baseline batches are full-width
@@ -33,8 +36,9 @@ class TorchRef:
     """Parameters as torch CPU tensors under the TF variable names (the
     oracle's init_params / the ParamStore layout: kernels HWIO / [in+H, 4H])."""
 
-    def __init__(self, params, rnn_sizes=(512, 512), dtype=torch.float32):
+    def __init__(self, params, rnn_sizes=(512, 512), dtype=torch.float32, cell="lstm"):
         self.rnn_sizes = tuple(rnn_sizes)
+        self.cell = cell
         self.dtype = dtype
         self.p = {k: torch.tensor(v, dtype=dtype) for k, v in params.items()}
         self.train_names = [k for k in self.p if not k.endswith(("moving_mean", "moving_variance"))]
@@ -63,6 +67,9 @@ class TorchRef:
         for li, H in enumerate(self.rnn_sizes, start=1):
             outs = []
             for d, rev in (("fw", False), ("bw", True)):
+                if self.cell == "gru":
+                    outs.append(self._gru_dir(h, f"rnn/bdrnn{li}/{d}/gru_cell/", H, rev))
+                    continue
                 k = p[f"rnn/bdrnn{li}/{d}/lstm_cell/kernel"]
                 b = p[f"rnn/bdrnn{li}/{d}/lstm_cell/bias"]
                 n_in = h.shape[2]
@@ -82,6 +89,25 @@ class TorchRef:
                 outs.append(torch.stack(seq))
             h = torch.cat(outs, dim=2)
         return F.relu(h @ p["rnn/logits/kernel"] + p["rnn/logits/bias"])
+
+    def _gru_dir(self, h, pre, H, rev):
+        """One direction of the GRU layer; the input halves of both matmuls hoisted."""
+        p = self.p
+        n_in = h.shape[2]
+        gk, gb = p[pre + "gates/kernel"], p[pre + "gates/bias"]
+        ck, cb = p[pre + "candidate/kernel"], p[pre + "candidate/bias"]
+        gx = h @ gk[:n_in] + gb                                                  # [T, B, 2H]
+        cx = h @ ck[:n_in] + cb                                                  # [T, B, H]
+        hs = h.new_zeros(h.shape[1], H)
+        seq = []
+        for t in (range(h.shape[0] - 1, -1, -1) if rev else range(h.shape[0])):
+            r, u = torch.sigmoid(gx[t] + hs @ gk[n_in:]).chunk(2, dim=1)
+            c = torch.tanh(cx[t] + (r * hs) @ ck[n_in:])
+            hs = u * hs + (1 - u) * c
+            seq.append(hs)
+        if rev:
+            seq.reverse()
+        return torch.stack(seq)
 
     def loss(self, logits, labels, label_len):
         """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised)."""

@@ -427,7 +427,8 @@ def test_train_step_runs_and_updates():
     assert not np.allclose(newp["convnet/conv2/batch_norm/moving_mean"], 0)
 
 
-def test_torch_cpu_restatement_matches_oracle():
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_torch_cpu_restatement_matches_oracle(cell):
     """oracle/torch_ref.py (the timed CPU baseline of bench.py) computes the
     oracle's graph: TRAIN-mode loss, logits-layer and conv1 gradients, and one
     TF1 Adam update, at a small full-width shape."""
@@ -435,18 +436,18 @@ def test_torch_cpu_restatement_matches_oracle():
 
     from oracle.torch_ref import TorchRef
     rng = np.random.default_rng(9)
-    sizes = (32, 32)
-    vals = M.init_params(seed=3, rnn_sizes=sizes)
+    sizes = (32, 32) if cell == "lstm" else (32, 16)
+    vals = M.init_params(seed=3, cell=cell, rnn_sizes=sizes)
     for k in vals:
-        if "lstm_cell/kernel" in k:
+        if "_cell/" in k and "kernel" in k:
             vals[k] = (vals[k] * 20).astype(np.float32)
     B, W = 3, 64
     img = rng.integers(0, 256, (B, 32, W, 1)).astype(np.uint8)
     widths = np.full(B, W, np.int32)
     labels = [list(rng.integers(0, 95, n)) for n in (3, 5, 4)]
-    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", sizes)
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, cell, sizes)
     loss_ref, grads_ref, _, logits_ref, _ = ref.loss_and_grads(G.preprocess(img).astype(np.float64), widths, labels)
-    tr = TorchRef(vals, sizes, dtype=torch.float64)
+    tr = TorchRef(vals, sizes, dtype=torch.float64, cell=cell)
     lab = torch.zeros(B, 5, dtype=torch.long)
     for i, l in enumerate(labels):
         lab[i, :len(l)] = torch.tensor(l)
@@ -456,6 +457,7 @@ def test_torch_cpu_restatement_matches_oracle():
     loss = tr.loss(logits, lab, ln)
     loss.backward()
     assert abs(loss.item() - loss_ref) < 1e-9 * abs(loss_ref)
-    for name in ("rnn/logits/kernel", "rnn/bdrnn1/bw/lstm_cell/kernel", "convnet/conv8/batch_norm/gamma",
+    rnn = "lstm_cell/kernel" if cell == "lstm" else "gru_cell/candidate/kernel"
+    for name in ("rnn/logits/kernel", "rnn/bdrnn1/bw/" + rnn, "convnet/conv8/batch_norm/gamma",
                  "convnet/conv1/kernel"):
         np.testing.assert_allclose(tr.p[name].grad.numpy(), grads_ref[name], rtol=1e-7, atol=1e-10, err_msg=name)
