@@ -225,6 +225,13 @@ extern "C" int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz,
 
 extern "C" size_t ocrk_conv_stats_tiles(int64_t M) { return (size_t)ocrk::cdiv(M, 128); }
 
+namespace ocrk {   // conv_direct.hip: the narrow-channel layers (returns -1 when the shape is not covered)
+int conv_direct_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,
+                    void* y, int relu, float* stats, hipStream_t s);
+int conv_direct_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                         const void* relu_mask, float* stats, hipStream_t s);
+}
+
 extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,
                                 const float* bias, int cout, void* y, int y_dtype, int relu,
                                 float* stats, int dtype, void* stream) {
@@ -235,6 +242,10 @@ extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, con
     p.bias = bias; p.relu = relu; p.alpha = 1.f; p.stats = stats;
     p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
     p.convH = H; p.convW = W; p.convC = cin;
+    if (dtype == OCRK_BF16 && y_dtype == OCRK_BF16) {
+        const int st = ocrk::conv_direct_fwd(x, B, H, W, cin, w_nk, bias, cout, y, relu, stats, ocrk::as_stream(stream));
+        if (st >= 0) return st;
+    }
     return ocrk::gemm(p, ocrk::A_IM2COL, ocrk::B_NK, dtype, ocrk::as_stream(stream));
 }
 
@@ -265,7 +276,8 @@ extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int co
         p.stats = (float*)ws;
     }
     hipStream_t s = ocrk::as_stream(stream);
-    int st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
+    int st = dtype == OCRK_BF16 ? ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, p.stats, s) : -1;
+    if (st < 0) st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
     if (st || !dbias) return st;
     const int tiles = (int)bwd_data_tiles(B, H, W);
     double* part = (double*)((char*)ws + ((size_t)tiles * 2 * cin * sizeof(float) + 7) / 8 * 8);

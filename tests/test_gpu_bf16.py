@@ -39,9 +39,16 @@ def _rel(a, b):
 BF16_OUT = 4e-3
 
 
-@pytest.mark.parametrize("B,H,W,cin,cout", [(4, 30, 254, 32, 32), (16, 3, 125, 256, 256)])
-def test_bf16_conv_engines_at_layer_shapes(cuda, B, H, W, cin, cout):
+@pytest.mark.parametrize("B,H,W,cin,cout", [(4, 30, 254, 32, 32), (4, 15, 127, 32, 64), (4, 15, 127, 64, 64),
+                                             (4, 7, 126, 64, 128), (16, 3, 125, 256, 256)])
+@pytest.mark.parametrize("direct", ["1", "2"])
+def test_bf16_conv_engines_at_layer_shapes(cuda, monkeypatch, B, H, W, cin, cout, direct):
+    """conv2..conv5 shapes run the direct kernel (conv_direct.hip) forward and
+    backward-data where it is routed (OCRK_CONV_DIRECT=1, the default: Cin 32
+    or dgrad output 32) or wherever it covers the shape (=2), conv8 the
+    implicit GEMM; ragged tails (B*H*W not a multiple of the 128-pixel tile)."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    monkeypatch.setenv("OCRK_CONV_DIRECT", direct)
     rng = np.random.default_rng(cin * 7 + W)
     x = _bf(rng.standard_normal((B, H, W, cin)))
     w = _bf(rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin))
@@ -74,6 +81,9 @@ def test_bf16_conv_engines_at_layer_shapes(cuda, B, H, W, cin, cout):
     assert _rel(dx.float().cpu().numpy(), dmask) < BF16_OUT
     # the bias gradient sums the fp32 values before their bf16 rounding
     assert _rel(dbias.cpu().numpy(), dmask.reshape(-1, cin).sum(0)) < 1e-4
+    # backward-data without mask / bias gradient (the odd layers' dx)
+    dx_plain = Kn.conv3x3_bwd_data(torch.from_numpy(dy).to(cuda).bfloat16(), w_bwd)
+    assert _rel(dx_plain.float().cpu().numpy(), dx_ref) < BF16_OUT
     # TN weight gradient, f32 accumulation over B*H*W pixels
     dw = torch.zeros(3, 3, cin, cout, device=cuda)
     Kn.conv3x3_bwd_weight(xd, torch.from_numpy(dy).to(cuda).bfloat16(), dw, accumulate=False)
