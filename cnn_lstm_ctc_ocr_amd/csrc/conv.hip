@@ -285,7 +285,12 @@ extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int co
 }
 
 static int wgrad_splits(int64_t M, int cin, int cout) {
-    // enough partial tiles to cover the chip ~2x; each split >= 4096 pixels
+    // enough partial tiles to cover the chip ~2x (the 256 x 256 ping-pong
+    // engine: ~1x, one item per CU); each split >= 4096 pixels
+    if (ocrk::gemm_pptn_covers(ocrk::A_IM2COL_T, 9 * cin, cout, cin)) {
+        const int64_t tiles = ocrk::cdiv(9 * cin, 256) * ocrk::cdiv(cout, 256);
+        return (int)std::max<int64_t>(1, std::min<int64_t>(256 / tiles, M / 2048));   // items <= 256: one round
+    }
     int64_t tiles = ocrk::cdiv(9 * cin, 128) * ocrk::cdiv(cout, cout <= 32 ? 32 : (cout <= 64 ? 64 : 128));
     int64_t want = ocrk::cdiv(512, tiles);
     int64_t maxs = std::max<int64_t>(1, M / 4096);

@@ -81,6 +81,7 @@ int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
 
 // 8-wave ping-pong engine for A_COLK x B_KN weight gradients (gemm_pptn.hip),
 // f32 C or split-K partials, M, N >= 256. -1 when not covered (OCRK_GEMM_PPTN=0).
+bool gemm_pptn_covers(int amode, int M, int N, int convC);   // shape test of gemm_pptn (wgrad split choice)
 int gemm_pptn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
 // Plain A_ROWK x B_NK bf16 GEMMs with a bf16 C and at most a bias epilogue

@@ -22,6 +22,13 @@
 //   U1 = {[wn0 q0 | wn1 q0], [wn2 q0 | wn3 q0]}, U2 = the q1 halves.
 // Work items = output tiles x K slices, one per workgroup; split K writes f32
 // partials (reduced by gemm.hip's splitk_finish), else C (+)= in place.
+//
+// AM = A_IM2COL_T: the conv weight gradient dW[(kh,kw,c)][cout] = im2col(x)^T
+// . dy over the B*H*W pixels (model.py:84-109 backward). A k-row of a
+// 64-column A block is then 64 channels of ONE tap at the shifted pixel --
+// 128 contiguous bytes of the NHWC input (Cin % 64 == 0) -- or zeros where
+// the tap leaves the image, so the same LDS-DMA unit layout applies with a
+// per-lane source offset.
 #include "gemm.h"
 #include "mfma_util.h"
 
@@ -41,6 +48,7 @@ __device__ __forceinline__ void tt_barrier() {
     asm volatile("" ::: "memory");
 }
 
+template <int AM>
 __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     constexpr int BM = 256, BN = 256, BK = 64, ROWB = 128, BLK = BK * ROWB;   // 8-KB [64 k][64 col] block
     constexpr int A_BYTES = 4 * BLK, BUF = 8 * BLK;
@@ -70,7 +78,8 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     const int kbeg = zs * p.k_chunk;
     const int kend = min(p.K, kbeg + p.k_chunk);
     const int nk = max(1, (kend - kbeg + BK - 1) / BK);
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, (int64_t)p.K * p.lda * 2);
+    const __amdgpu_buffer_rsrc_t ra =
+        uniform_rsrc(A, (int64_t)p.K * (AM == A_IM2COL_T ? p.convC : p.lda) * 2);
     const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, (int64_t)p.K * p.ldb * 2);
 
     // ---- per-lane DMA geometry: instruction idx = i*8 + wave (i = 0, 1) of a
@@ -84,13 +93,41 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     const int bcols[4] = {bcol(0, 0), bcol(0, 1), bcol(1, 0), bcol(1, 1)};   // [U1 i0, U1 i1, U2 i0, U2 i1]
     const unsigned a_lane = (unsigned)(((int64_t)krow_l * p.lda + m0 + 8 * chunk) * 2);
     const unsigned b_lane = (unsigned)(((int64_t)krow_l * p.ldb + n0) * 2);
+    // IM2COL_T: the tap (dh, dw) and first channel of each A sub-block (uniform per item),
+    // and this lane's pixel (row h, column w) of the K-tile being issued
+    int t_dh[4] = {0, 0, 0, 0}, t_dw[4] = {0, 0, 0, 0}, t_c0[4] = {0, 0, 0, 0};
+    if constexpr (AM == A_IM2COL_T) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int col = min(m0 + acol[s], p.M - 1);
+            const int tap = col / p.convC;
+            t_dh[s] = tap / 3 - 1;
+            t_dw[s] = tap % 3 - 1;
+            t_c0[s] = col - tap * p.convC;
+        }
+    }
+    int pix_h = 0, pix_w = 0;
 
     auto issue = [&](auto U_, int kt, char* buf) {
         constexpr int U = decltype(U_)::value;
         const int k = kbeg + kt * BK + krow_l;
         const bool kok = k < kend;
         const unsigned kst = (unsigned)((int64_t)(kt * BK + kbeg) * (U == 0 || U == 3 ? p.lda : p.ldb) * 2);
-        if constexpr (U == 0 || U == 3) {
+        if constexpr ((U == 0 || U == 3) && AM == A_IM2COL_T) {
+            if constexpr (U == 0) {                        // U3 of the same K-tile follows: same pixel
+                pix_w = k % p.convW;
+                pix_h = (k / p.convW) % p.convH;
+            }
+#pragma unroll
+            for (int i = 0; i < NUA; ++i) {
+                const int s = (U == 0 ? 0 : 2) + i;
+                const int hh = pix_h + t_dh[s], ww = pix_w + t_dw[s];
+                const bool ok = kok && m0 + acol[s] + 8 * chunk < p.M && hh >= 0 && hh < p.convH && ww >= 0 &&
+                                ww < p.convW;
+                const int64_t off = ((int64_t)(k + t_dh[s] * p.convW + t_dw[s]) * p.convC + t_c0[s] + 8 * chunk) * 2;
+                tt_dma16(ra, buf + (acol[s] / 64) * BLK + (wave & 7) * 1024, ok ? (unsigned)off : TT_OOB);
+            }
+        } else if constexpr (U == 0 || U == 3) {
 #pragma unroll
             for (int i = 0; i < NUA; ++i) {
                 const int s = (U == 0 ? 0 : 2) + i;
@@ -248,23 +285,34 @@ bool gemm_pptn_enabled() {
 }
 
 // Runs the ping-pong TN engine when it covers the call; -1 otherwise.
+bool gemm_pptn_covers(int amode, int M, int N, int convC) {
+    if (!gemm_pptn_enabled() || M < 256 || N < 256 || M % 8 != 0 || N % 8 != 0) return false;
+    if (amode == A_COLK) return true;
+    return amode == A_IM2COL_T && convC % 64 == 0;        // a 64-column A block = one tap's channels
+}
+
+// Runs the ping-pong TN engine when it covers the call; -1 otherwise.
 int gemm_pptn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {
-    if (!gemm_pptn_enabled() || dtype != OCRK_BF16 || amode != A_COLK || bmode != B_KN) return -1;
+    if (dtype != OCRK_BF16 || bmode != B_KN || !gemm_pptn_covers(amode, p.M, p.N, p.convC)) return -1;
     if (p.c_bf16 || p.bias || p.relu || p.mask || p.stats) return -1;
-    if (p.M % 8 != 0 || p.N % 8 != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -1;
-    if (p.M < 256 || p.N < 256) return -1;                 // narrow outputs: the 4-wave engine
+    if (p.ldb % 8 != 0 || (amode == A_COLK && p.lda % 8 != 0)) return -1;
     if (p.splits == 1 && (p.ldc % 4 != 0 || (uintptr_t)p.C % 16 != 0 || p.strideC % 4 != 0)) return -1;
     if (p.splits > 1 && (uintptr_t)p.splitk_ws % 16 != 0) return -1;
-    if ((int64_t)p.K * p.lda * 2 >= (1ll << 31) || (int64_t)p.K * p.ldb * 2 >= (1ll << 31)) return -1;
+    const int64_t a_bytes = (int64_t)p.K * (amode == A_COLK ? p.lda : p.convC) * 2;
+    if (a_bytes >= (1ll << 31) || (int64_t)p.K * p.ldb * 2 >= (1ll << 31)) return -1;
+    if (amode == A_IM2COL_T && p.batch != 1) return -1;
     constexpr int LDS = 2 * 8 * 64 * 128;
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pptn_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-        configured = true;
+    const void* kern = amode == A_COLK ? reinterpret_cast<const void*>(&gemm_pptn_kernel<A_COLK>)
+                                       : reinterpret_cast<const void*>(&gemm_pptn_kernel<A_IM2COL_T>);
+    static bool configured[2] = {false, false};
+    if (!configured[amode == A_COLK ? 0 : 1]) {
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        configured[amode == A_COLK ? 0 : 1] = true;
     }
     const int64_t items = cdiv(p.M, 256) * cdiv(p.N, 256) * (int64_t)p.batch * p.splits;
-    gemm_pptn_kernel<<<dim3((unsigned)(cdiv(items, 8) * 8)), 512, LDS, stream>>>(p);
+    const dim3 grid((unsigned)(cdiv(items, 8) * 8));
+    if (amode == A_COLK) gemm_pptn_kernel<A_COLK><<<grid, 512, LDS, stream>>>(p);
+    else gemm_pptn_kernel<A_IM2COL_T><<<grid, 512, LDS, stream>>>(p);
     return launch_status("gemm_pptn");
 }
 

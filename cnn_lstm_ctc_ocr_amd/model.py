@@ -320,7 +320,7 @@ def _splits(M, N, Kdim):
     outputs on the 128 x 128 engine (~2 items per CU, >= 2048 rows)."""
     if M >= 256 and N >= 256:
         tiles = -(-M // 256) * -(-N // 256)
-        return int(max(1, min(-(-256 // tiles), Kdim // 1024)))
+        return int(max(1, min(256 // tiles, Kdim // 1024)))            # <= 256 items: one round on the chip
     tiles = -(-M // 128) * -(-N // 128)
     return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
 

@@ -40,7 +40,7 @@ BF16_OUT = 4e-3
 
 
 @pytest.mark.parametrize("B,H,W,cin,cout", [(4, 30, 254, 32, 32), (4, 15, 127, 32, 64), (4, 15, 127, 64, 64),
-                                             (4, 7, 126, 64, 128), (16, 3, 125, 256, 256)])
+                                             (4, 7, 126, 64, 128), (8, 3, 125, 128, 256), (16, 3, 125, 256, 256)])
 @pytest.mark.parametrize("direct", ["1", "2"])
 def test_bf16_conv_engines_at_layer_shapes(cuda, monkeypatch, B, H, W, cin, cout, direct):
     """conv2..conv5 shapes run the direct kernel (conv_direct.hip) forward and
@@ -84,7 +84,8 @@ def test_bf16_conv_engines_at_layer_shapes(cuda, monkeypatch, B, H, W, cin, cout
     # backward-data without mask / bias gradient (the odd layers' dx)
     dx_plain = Kn.conv3x3_bwd_data(torch.from_numpy(dy).to(cuda).bfloat16(), w_bwd)
     assert _rel(dx_plain.float().cpu().numpy(), dx_ref) < BF16_OUT
-    # TN weight gradient, f32 accumulation over B*H*W pixels
+    # TN weight gradient, f32 accumulation over B*H*W pixels (Cin % 64 == 0 and
+    # 9 Cin, Cout >= 256: the 256 x 256 ping-pong engine's im2col mode)
     dw = torch.zeros(3, 3, cin, cout, device=cuda)
     Kn.conv3x3_bwd_weight(xd, torch.from_numpy(dy).to(cuda).bfloat16(), dw, accumulate=False)
     assert _rel(dw.cpu().numpy(), dw_ref) < 1e-4

@@ -31,7 +31,7 @@ def timed(f, n=10):
     return a.elapsed_time(b) / n * 1e3
 
 
-tot_f = tot_d = 0.0
+tot_f = tot_d = tot_w = 0.0
 for name, H, W, cin, cout, bn in LAYERS:
     M = B * H * W
     x = (torch.rand(B, H, W, cin, device=dev) - 0.5).bfloat16()
@@ -44,10 +44,14 @@ for name, H, W, cin, cout, bn in LAYERS:
     dbias = torch.zeros(cin, device=dev) if (bn and name != "conv2") else None
     tf = timed(lambda: K.conv3x3_fwd(x, w_nk, bias, relu=not bn, stats=stats))
     td = timed(lambda: K.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask, dbias=dbias))
+    dw = torch.zeros(3, 3, cin, cout, device=dev)
+    tw = timed(lambda: K.conv3x3_bwd_weight(x, dy, dw))
     fl = 2.0 * M * cout * 9 * cin
     fb = M * (cin + cout) * 2
     tot_f += tf
     tot_d += td
     print(f"{name} M={M:8d} {cin:3d}->{cout:3d}  fwd {tf:7.1f} us {fl / tf / 1e6:7.1f} TF/s (HBM floor "
-          f"{fb / 8e6:5.1f} us)   dgrad {td:7.1f} us {fl / td / 1e6:7.1f} TF/s", flush=True)
-print(f"total fwd {tot_f:.1f} us  dgrad {tot_d:.1f} us")
+          f"{fb / 8e6:5.1f} us)   dgrad {td:7.1f} us {fl / td / 1e6:7.1f} TF/s   wgrad {tw:7.1f} us "
+          f"{fl / tw / 1e6:7.1f} TF/s", flush=True)
+    tot_w += tw
+print(f"total fwd {tot_f:.1f} us  dgrad {tot_d:.1f} us  wgrad {tot_w:.1f} us")
