@@ -372,11 +372,76 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const GemmParams p)
     }
 }
 
+// Many splits over a small output (the conv weight gradients: 100+ slices of
+// a 288 x 32 .. 2304 x 256 tile set): 16 output quads x 16 split-parts per
+// workgroup. Part q sums splits q, q + 16, ... (two 16-B loads in flight),
+// then the 16 part sums of a quad are added in part order -- a fixed order,
+// so the result is reproducible run to run (it differs from the serial
+// order in rounding only).
+__global__ void __launch_bounds__(256) splitk_reduce4p_kernel(const GemmParams p) {
+    const int64_t MN = (int64_t)p.M * p.N, n4 = MN / 4;
+    const int zb = blockIdx.y;
+    const float4* ws = reinterpret_cast<const float4*>(p.splitk_ws + (int64_t)zb * p.splits * MN);
+    const int part = threadIdx.x >> 4, ql = threadIdx.x & 15;
+    const int64_t e = (int64_t)blockIdx.x * 16 + ql;
+    __shared__ float4 red[16][16];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < n4) {
+        int s = part;
+        for (; s + 16 < p.splits; s += 32) {
+            const float4 u0 = ws[s * n4 + e], u1 = ws[(s + 16) * n4 + e];
+            v.x += u0.x; v.y += u0.y; v.z += u0.z; v.w += u0.w;
+            v.x += u1.x; v.y += u1.y; v.z += u1.z; v.w += u1.w;
+        }
+        if (s < p.splits) {
+            const float4 u = ws[s * n4 + e];
+            v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+    }
+    red[part][ql] = v;
+    __syncthreads();
+    if (part != 0 || e >= n4) return;
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const float4 u = red[q][ql];
+        r[0] += u.x; r[1] += u.y; r[2] += u.z; r[3] += u.w;
+    }
+    const float* bias = p.bias ? p.bias + zb * p.strideBias : nullptr;
+    const int64_t e0 = e * 4;
+    const int row = (int)(e0 / p.N), col = (int)(e0 - (int64_t)row * p.N);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        r[j] = p.alpha * r[j] + (bias ? bias[col + j] : 0.f);
+        if (p.relu) r[j] = fmaxf(r[j], 0.f);
+    }
+    const int64_t off = zb * p.strideC + (int64_t)row * p.ldc + col;
+    if (p.c_bf16) {
+        union { uint2 q; bf16 h[4]; } o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o.h[j] = (bf16)r[j];
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(p.C) + off) = o.q;
+    } else {
+        float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
+        float4 c = make_float4(r[0], r[1], r[2], r[3]);
+        if (p.accumulate) {
+            const float4 o = *C;
+            c = make_float4(o.x + r[0], o.y + r[1], o.z + r[2], o.w + r[3]);
+        }
+        *C = c;
+    }
+}
+
 static int splitk_finish(const GemmParams& p, hipStream_t stream) {
     if (p.splits <= 1) return OCRK_OK;
     int64_t MN = (int64_t)p.M * p.N;
     const bool v4 = p.N % 4 == 0 && p.ldc % 4 == 0 && p.strideC % 4 == 0 &&
                     (uintptr_t)p.C % 16 == 0 && (uintptr_t)p.splitk_ws % 16 == 0;
+    if (v4 && p.splits >= 8) {
+        dim3 rg((unsigned)cdiv(MN / 4, 16), (unsigned)p.batch);
+        splitk_reduce4p_kernel<<<rg, 256, 0, stream>>>(p);
+        return launch_status("gemm splitk reduce");
+    }
     if (v4) {
         dim3 rg((unsigned)std::min<int64_t>(cdiv(MN / 4, 256), 4096), (unsigned)p.batch);
         splitk_reduce4_kernel<<<rg, 256, 0, stream>>>(p);
