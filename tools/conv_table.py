@@ -1,0 +1,93 @@
+"""Per-layer table of the conv2-conv8 forward launches of the bench step:
+duration (rocprofv3 --kernel-trace), TFLOP/s and MFMA fraction, and HBM
+bytes from the PMC passes (FETCH_SIZE x2 per the gfx950 correction +
+WRITE_SIZE) against the algorithmic bytes (input + output activations +
+weights, bf16). Dispatches are matched by kernel name and assigned to layers
+in issue order (7 per step).
+
+    python tools/conv_table.py --trace DIR --fetch DIR --write DIR --out FILE.md
+"""
+import argparse
+import csv
+import glob
+import os
+import re
+from collections import defaultdict
+
+FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48]>")
+B = 256
+LAYERS = [("conv2", 30, 254, 32, 32), ("conv3", 15, 127, 32, 64), ("conv4", 15, 127, 64, 64),
+          ("conv5", 7, 126, 64, 128), ("conv6", 7, 126, 128, 128), ("conv7", 3, 125, 128, 256),
+          ("conv8", 3, 125, 256, 256)]
+PEAK = 2500.0   # dense bf16 TFLOP/s, MI355X_MICROARCH.md
+
+
+def rows(root, name):
+    out = []
+    for f in glob.glob(os.path.join(root, "**", name), recursive=True):
+        with open(f, newline="") as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def short(n):
+    n = n.replace("ocrk::", "").replace("(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"\(.*", "", n)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    tr = sorted((r for r in rows(a.trace, "*kernel_trace.csv") if FWD.search(r["Kernel_Name"])),
+                key=lambda r: int(r["Start_Timestamp"]))
+    dur = defaultdict(list)
+    names = {}
+    for i, r in enumerate(tr):
+        layer = LAYERS[i % 7][0]
+        dur[layer].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        names[layer] = short(r["Kernel_Name"])
+
+    def pmc(root, counter):
+        per = defaultdict(float)
+        order = {}
+        for r in rows(root, "*counter_collection.csv"):
+            if r["Counter_Name"] == counter and FWD.search(r["Kernel_Name"]):
+                key = int(r["Dispatch_Id"])
+                per[key] += float(r["Counter_Value"])
+                order[key] = int(r["Start_Timestamp"])
+        keys = sorted(per, key=lambda k: order[k])
+        out = defaultdict(list)
+        for i, k in enumerate(keys):
+            out[LAYERS[i % 7][0]].append(per[k] * 1024)
+        return out
+
+    fetch, write = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
+    lines = ["| layer | kernel | us | TFLOP/s | MFMA frac | algorithmic MB | counter MB | counter / algorithmic |",
+             "|---|---|---|---|---|---|---|---|"]
+    tot_us = tot_fl = 0.0
+    for name, H, W, cin, cout in LAYERS:
+        M = B * H * W
+        fl = 2.0 * M * 9 * cin * cout
+        alg = (M * cin + M * cout + 9 * cin * cout) * 2
+        us = sum(dur[name]) / max(len(dur[name]), 1)
+        rd = 2 * sum(fetch[name]) / max(len(fetch[name]), 1)
+        wr = sum(write[name]) / max(len(write[name]), 1)
+        tf = fl / us / 1e6
+        tot_us += us
+        tot_fl += fl
+        lines.append(f"| {name} {cin}->{cout} | `{names.get(name, '?')}` | {us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | "
+                     f"{alg / 1e6:.1f} | {(rd + wr) / 1e6:.1f} | {(rd + wr) / alg:.2f} |")
+    tf = tot_fl / tot_us / 1e6
+    lines.append(f"| all | | {tot_us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | | | |")
+    txt = "\n".join(lines) + "\n"
+    with open(a.out, "w") as fh:
+        fh.write(txt)
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
