@@ -9,10 +9,11 @@
 // (thread = one pooled pixel x 8 channels) and can write the last pool
 // (pool8) straight into the time-major [T, B, C] feature layout the RNN reads
 // (model.py:147 squeeze + :212 transpose folded away).
-// Backward: thread = one pre-pool pixel x 8 channels; it re-derives which
-// pooling windows route their gradient to it ([TF1] MaxPoolGrad: first max of
-// the window), applies the ReLU mask, and a deterministic two-pass
-// (partials -> ordered sum -> apply) BN backward.
+// Backward: the routed gradient ([TF1] MaxPoolGrad: first max of the
+// window, ReLU mask) is re-derived from z, never stored as an argmax; a
+// deterministic two-pass BN backward (partials -> ordered sum -> apply). For
+// the path's pools both passes walk the pooling windows (bn_bwd_route_kernel;
+// the apply pass repeats the walk instead of reading a staged gradient image).
 #include "common.h"
 #include "reduce.h"
 
@@ -230,12 +231,20 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
 // PRE = (KW-1)/SW windows left of the range that still reach into it are
 // re-evaluated (their own columns are not retired here). Rows below the last
 // pooling window, and columns right of it, receive no gradient: zeros.
-template <typename T, int KH, int KW, int SW, int SEG>
+//
+// APPLY = pass 2 of the same window walk: instead of staging the routed
+// gradient da for a streaming apply pass (2 x |z| more bytes), the walk is
+// repeated and each retired column goes straight to
+// dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n), its per-block
+// column sums (the conv bias gradient) into `slab` (C per block). Pixels no
+// window covers (rows below the last window) have da = 0 but a non-zero dz.
+template <typename T, int KH, int KW, int SW, int SEG, bool APPLY = false>
 __global__ void __launch_bounds__(256)
 bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
                     const float* __restrict__ mean, const float* __restrict__ invstd,
                     const float* __restrict__ gamma, const float* __restrict__ beta, int dp_time_major,
-                    int nseg, int tasks_per_block, float* __restrict__ slab, T* __restrict__ da_out) {
+                    int nseg, int tasks_per_block, float* __restrict__ slab, T* __restrict__ da_out,
+                    const float* __restrict__ dsum = nullptr) {
     static_assert(SW >= 1 && SW <= KW, "stride <= window");
     constexpr int PRE = (KW - 1) / SW;
     __shared__ float red[256][17];
@@ -244,13 +253,16 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
     const int tasks = B * Ho * nseg * G;
     const int g = threadIdx.x % G;
     const int c0 = g * 8;
-    float sc[8], sf[8], mu[8], is[8];
+    float sc[8], sf[8], mu[8], is[8], am[8], bm[8];
+    const float inv_n = 1.f / (float)((int64_t)B * H * W);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         is[i] = invstd[c0 + i];
         mu[i] = mean[c0 + i];
         sc[i] = gamma[c0 + i] * is[i];
         sf[i] = beta[c0 + i] - mu[i] * sc[i];
+        am[i] = APPLY ? dsum[c0 + i] * inv_n : 0.f;
+        bm[i] = APPLY ? dsum[C + c0 + i] * inv_n : 0.f;
     }
     float s1[8], s2[8];
 #pragma unroll
@@ -277,17 +289,34 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const float d = fmaf(zc[dh][i], sc[i], sf[i]) > 0.f ? dc[dh][i] : 0.f;
-                    s1[i] += d;
-                    s2[i] += d * ((zc[dh][i] - mu[i]) * is[i]);
-                    o.v[i] = d;
+                    const float xh = (zc[dh][i] - mu[i]) * is[i];
+                    if constexpr (APPLY) {
+                        o.v[i] = sc[i] * (d - am[i] - xh * bm[i]);
+                        s1[i] += o.v[i];
+                    } else {
+                        s1[i] += d;
+                        s2[i] += d * xh;
+                        o.v[i] = d;
+                    }
                 }
-                store8(drow + ((int64_t)dh * W + x) * C, o);
+                if (APPLY || da_out) store8(drow + ((int64_t)dh * W + x) * C, o);
             }
-            if (tail_rows) {
-                F8 zero;
+            if (tail_rows && (APPLY || da_out)) {
+                for (int h = Ho * KH; h < H; ++h) {
+                    F8 o;
+                    if constexpr (APPLY) {
+                        const F8 zt = load8(z + (((int64_t)b * H + h) * W + x) * C + c0);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) zero.v[i] = 0.f;
-                for (int h = Ho * KH; h < H; ++h) store8(da_out + (((int64_t)b * H + h) * W + x) * C + c0, zero);
+                        for (int i = 0; i < 8; ++i) {
+                            o.v[i] = sc[i] * (-am[i] - (zt.v[i] - mu[i]) * is[i] * bm[i]);
+                            s1[i] += o.v[i];
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) o.v[i] = 0.f;
+                    }
+                    store8(da_out + (((int64_t)b * H + h) * W + x) * C + c0, o);
+                }
             }
         };
         const int wfirst = max(0, wa - PRE);
@@ -355,22 +384,29 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
         for (int j = SW; j < KW; ++j) retire(xl + j, zr[j], dr[j]);
         for (int x = max(xl + KW, own0); x < own1; ++x) {
-            float zc[KH][8], dc[KH][8];                     // no gradient: z is not needed
+            float zc[KH][8], dc[KH][8];                     // no gradient (z matters only for APPLY's dz)
 #pragma unroll
-            for (int dh = 0; dh < KH; ++dh)
+            for (int dh = 0; dh < KH; ++dh) {
+                F8 zt;
+                if constexpr (APPLY) zt = load8(zrow + ((int64_t)dh * W + x) * C);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) zc[dh][i] = dc[dh][i] = 0.f;
+                for (int i = 0; i < 8; ++i) {
+                    zc[dh][i] = APPLY ? zt.v[i] : 0.f;
+                    dc[dh][i] = 0.f;
+                }
+            }
             retire(x, zc, dc);
         }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
     __syncthreads();
-    for (int o = threadIdx.x; o < 2 * C; o += 256) {
+    const int nout = APPLY ? C : 2 * C;
+    for (int o = threadIdx.x; o < nout; o += 256) {
         int which = o / C, c = o % C, gg = c / 8, ci = c % 8;
         float s = 0.f;
         for (int q = gg; q < 256; q += G) s += red[q][which * 8 + ci];
-        slab[(int64_t)blockIdx.x * 2 * C + o] = s;
+        slab[(int64_t)blockIdx.x * nout + o] = s;
     }
 }
 
@@ -527,15 +563,17 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
         if (dtype == OCRK_BF16) {
             const bf16 *zz = (const bf16*)z, *pp = (const bf16*)dp;
             bf16* dd = (bf16*)da;
-            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            // pass 1 stages da only for the overlapping 2x2/[2,1] pools (their pass 2
+            // streams it: measured faster than re-walking the windows); else pass 2 re-walks
+            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
             else if (rk == 2) bn_bwd_route_kernel<bf16, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
-            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
         } else {
             const float *zz = (const float*)z, *pp = (const float*)dp;
             float* dd = (float*)da;
-            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
             else if (rk == 2) bn_bwd_route_kernel<float, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
-            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
+            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
         }
 #undef ROUTE_ARGS
     } else if (dtype == OCRK_BF16) {
@@ -547,6 +585,30 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
     if (st) return st;
     st = slab_sum(slab, nr, 2 * C, part, dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
     if (st) return st;
+    if (rk == 1 || rk == 3) {
+        // pass 2 repeats the window walk (no staged da image): dz and the conv-bias partial sums
+        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
+        const int nseg = (int)ocrk::cdiv(Wo, BN_ROUTE_SEG);
+        const int64_t tasks = (int64_t)B * Ho * nseg * (C / 8);
+        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
+        const int tpb = (int)(ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
+#define APPLY_ARGS B, H, W, C, mean, invstd, gamma, beta, dp_time_major, nseg, tpb, bslab
+        if (dtype == OCRK_BF16) {
+            const bf16 *zz = (const bf16*)z, *pp = (const bf16*)dp;
+            bf16* dd = (bf16*)dz;
+            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+        } else {
+            const float *zz = (const float*)z, *pp = (const float*)dp;
+            float* dd = (float*)dz;
+            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+        }
+#undef APPLY_ARGS
+        st = ocrk::launch_status("ocrk_bn_relu_pool_bwd apply (window walk)");
+        if (st || !dbias) return st;
+        return slab_sum(bslab, nr, C, part, nullptr, dbias, nullptr, C, accumulate, s);
+    }
     float* bs = dbias ? bslab : nullptr;
     if (dtype == OCRK_BF16)
         bn_bwd_apply_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)da, npix, C, mean, invstd, gamma, dsum, (int)ipb, (bf16*)dz, bs);

@@ -106,14 +106,19 @@ class _ConvBlock(torch.autograd.Function):
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
                                 dbias=G[pe + "/bias"])                  # conv bias grad fused
         B, H, W, C = dz.shape
-        with _conv_side(store, y_odd, dz):                 # overlaps the data-gradient GEMM below
-            K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
+        if k > 1:
+            with _conv_side(store, y_odd, dz):             # overlaps the data-gradient GEMM below
+                K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None)
         dx = None
         if k == 1:
-            K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
+            # the step's tail: conv1's weight gradient joins the side stream (behind
+            # conv3's) while conv2's runs here, so the two streams end together
+            with _conv_side(store, x, dy_odd):
+                K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
+            K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
             store.join()                                   # side-stream weight gradients are in
         else:
             with _conv_side(store, x, dy_odd):
