@@ -437,7 +437,11 @@ static int splitk_finish(const GemmParams& p, hipStream_t stream) {
     int64_t MN = (int64_t)p.M * p.N;
     const bool v4 = p.N % 4 == 0 && p.ldc % 4 == 0 && p.strideC % 4 == 0 &&
                     (uintptr_t)p.C % 16 == 0 && (uintptr_t)p.splitk_ws % 16 == 0;
-    if (v4 && p.splits >= 8) {
+    // many slices of a small output: split the slices over the threads; a
+    // few slices of a large output (the recurrent dW, 8-31 slices of 0.5-2 M
+    // values): one thread per quad keeps the grid small (it shares the CUs
+    // with the persistent BPTT)
+    if (v4 && (p.splits >= 32 || (p.splits >= 8 && MN / 4 < 65536))) {
         dim3 rg((unsigned)cdiv(MN / 4, 16), (unsigned)p.batch);
         splitk_reduce4p_kernel<<<rg, 256, 0, stream>>>(p);
         return launch_status("gemm splitk reduce");
