@@ -27,6 +27,7 @@
 #include <climits>
 
 #include "common.h"
+#include "gemm.h"
 #include "mfma_util.h"
 
 namespace ocrk {
@@ -335,6 +336,178 @@ conv3x3_direct_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, co
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------ weight gradient
+// dW[kh][kw][ci][co] = sum over pixels of x[px + (dh, dw)][ci] * dy[px][co],
+// Cin = 32 (conv2, conv3). Same persistent chunk walk as the forward: per
+// 128-pixel chunk the 3 tap-row runs of x (3 x 130 pixels) and the dy chunk
+// are staged by LDS-DMA, and the k = pixel reduction runs on MFMA with both
+// operands read k-transposed (ds_read_b64_tr_b16: a lane gets pixels
+// 4g..4g+3 and 16+4g..16+4g+3 of a 32-pixel k-step, one channel). Off-image
+// taps: the x run of tap row dh = -1 (+1) drops pixels of the image's last
+// (first) row AT THE DMA (every product such a pixel enters belongs to an
+// output pixel in the first (last) row); the dy fragment of tap column
+// dw = -1 (+1) is masked in registers where its pixel is in the first (last)
+// column. The workgroup keeps its dW partial in registers over its chunk
+// range and writes it once; the split-K reduce sums the partials.
+template <int CO>
+struct WgCfg {
+    static constexpr int CI = 32, PXB = 64;
+    static constexpr int NTN = CO / 16;             // N tiles (16 output channels)
+    static constexpr int WN = NTN;                  // waves along N: one N tile each
+    static constexpr int WM = 4 / WN;               // waves along M
+    static constexpr int MT = 9 * CI / 16;          // 18 M tiles of (tap, 16 ci)
+    static constexpr int MTW = MT / WM;             // M tiles per wave (9 or 18)
+    static constexpr int XRB = (CM + 2) * PXB;      // x tap-row run
+    static constexpr int DYB = CM * CO * 2;         // the dy chunk
+    static constexpr int NXP = 3 * XRB / 16;        // x pieces
+    static constexpr int NDP = DYB / 16;            // dy pieces
+    static constexpr int XBLK = (NXP + 63) / 64;    // x blocks: a wave's DMA block is all x or all dy
+    static constexpr int NBLK = XBLK + (NDP + 63) / 64;   // (a uniform buffer descriptor per instruction)
+    static constexpr int NDW = (NBLK + 3) / 4;
+    static constexpr int SBA = NBLK * 1024;
+    // two stages when two workgroups then fit a CU, else three when they fit
+    static constexpr int NBUF = 2 * SBA + 1024 <= 80 * 1024 ? 2 : (3 * SBA + 1024 <= 160 * 1024 ? 3 : 2);
+    static constexpr int PD = NBUF - 1;             // prefetch distance
+    static constexpr int TRASH_OFF = NBUF * SBA;
+    static constexpr int LDS = TRASH_OFF + 1024;
+    static constexpr int PER_CU = LDS <= 80 * 1024 ? 2 : 1;
+    static_assert(MT % WM == 0 && 4 % WN == 0, "wave split");
+    static_assert(NDW * (PD - 1) < 64 && LDS <= 160 * 1024, "vmcnt immediate / LDS");
+};
+
+template <int CO>
+__global__ void __launch_bounds__(256)
+conv3x3_wgrad_direct_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
+                            int M, int H, int W, int nchunks, int cpw) {
+    using C = WgCfg<CO>;
+    extern __shared__ __attribute__((aligned(1024))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % C::WM, wn = wave / C::WM;
+    const int i16 = lane & 15, g = lane >> 4;
+
+    const int nb = gridDim.x;
+    const int bid = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+    const int c_begin = bid * cpw;
+    const int c_end = min(nchunks, c_begin + cpw);
+    float* out = part + (size_t)blockIdx.x * 9 * C::CI * CO;
+
+    floatx4 acc[C::MTW];
+#pragma unroll
+    for (int t = 0; t < C::MTW; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if (c_begin < c_end) {
+        const int xbytes = M * C::PXB, ybytes = M * CO * 2;
+        const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x, (int64_t)xbytes);
+        const __amdgpu_buffer_rsrc_t rd = uniform_rsrc(dy, (int64_t)ybytes);
+        const int HW = H * W;
+        // per DMA slot: pixel offset from the chunk's first pixel, byte offset
+        // within the pixel, the tap row (x slots) and the pixel's (row, col), walked per chunk
+        int s_dpx[C::NDW], s_boff[C::NDW], s_kind[C::NDW], s_row[C::NDW], s_col[C::NDW];
+#pragma unroll
+        for (int i = 0; i < C::NDW; ++i) {
+            const int blk = i * 4 + wave;
+            const int q = blk * 64 + lane;
+            int dpx = 0, boff = 0, kind = -1;                 // kind: 0..2 x tap row, 3 dy, -1 none
+            if (blk < C::XBLK && q < C::NXP) {
+                const int r = q / (C::XRB / 16), w16 = q - r * (C::XRB / 16);
+                dpx = (r - 1) * W - 1 + w16 / (C::PXB / 16);
+                boff = (w16 % (C::PXB / 16)) * 16;
+                kind = r;
+            } else if (blk >= C::XBLK && blk < C::NBLK && q - C::XBLK * 64 < C::NDP) {
+                const int w16 = q - C::XBLK * 64;
+                dpx = w16 / (CO * 2 / 16);
+                boff = (w16 % (CO * 2 / 16)) * 16;
+                kind = 3;
+            }
+            s_dpx[i] = dpx; s_boff[i] = boff; s_kind[i] = kind;
+            const int pp = (((c_begin * CM + dpx) % HW) + HW) % HW;   // periodic in the image: negatives too
+            s_row[i] = pp / W;
+            s_col[i] = pp % W;
+        }
+        // the slots' (row, col) advance by one chunk per issue: issue chunks in order from c_begin
+        auto issue = [&](int chunk, int buf) {
+            const bool live = chunk < c_end;
+            char* base = smem + buf * C::SBA;
+#pragma unroll
+            for (int i = 0; i < C::NDW; ++i) {
+                const int blk = i * 4 + wave;
+                const int k = s_kind[i];
+                const int pix = chunk * CM + s_dpx[i];
+                bool ok = live && k >= 0 && pix >= 0 && pix < M;
+                if (k == 0) ok = ok && s_row[i] != H - 1;          // tap row -1: not the last row
+                if (k == 2) ok = ok && s_row[i] != 0;              // tap row +1: not the first row
+                const bool isx = blk < C::XBLK;                   // wave-uniform: one descriptor per instruction
+                const unsigned off = (unsigned)(isx ? pix * C::PXB : pix * CO * 2) + (unsigned)s_boff[i];
+                dma16(isx ? rx : rd, blk < C::NBLK ? base + blk * 1024 : smem + C::TRASH_OFF, ok ? off : DOOB);
+                s_col[i] += CM;
+                while (s_col[i] >= W) {
+                    s_col[i] -= W;
+                    s_row[i] = s_row[i] == H - 1 ? 0 : s_row[i] + 1;
+                }
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < C::PD; ++d) issue(c_begin + d, d);
+        for (int ch = c_begin; ch < c_end; ++ch) {
+            const int k = ch - c_begin;
+            const int buf = k % C::NBUF;
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NDW * (C::PD - 1)) : "memory");
+            lds_barrier();
+            issue(ch + C::PD, (k + C::PD) % C::NBUF);
+            const char* st = smem + buf * C::SBA;
+            const char* xs = st;                                 // [3][130 px][32 ci]
+            const char* ds = st + C::XBLK * 1024;                // [128 px][CO]
+            const int cq = 4 * (i16 & 3);
+            const int colbase = (ch * CM) % W;                   // column of the chunk's first pixel
+#pragma unroll
+            for (int kk = 0; kk < CM / 32; ++kk) {
+                const int pr = kk * 32 + 4 * g + (i16 >> 2);     // this lane's k-row (pixel) of the read
+                // dy fragment: elements e hold pixels 32 kk + 4 g + (e & 3) + 16 (e >> 2); masked
+                // copies for the tap columns -1 (first column dropped) and +1 (last column dropped)
+                const bf16x8 bv = frag_tr(reinterpret_cast<const unsigned short*>(ds + pr * CO * 2 + (wn * 16 + cq) * 2),
+                                          16 * CO);
+                u32x4 mlo, mhi;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    unsigned lo = 0u, hi = 0u;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int e = 2 * d + h;
+                        int c = colbase + kk * 32 + 4 * g + (e & 3) + 16 * (e >> 2);
+                        while (c >= W) c -= W;
+                        const unsigned half = 0xffffu << (16 * h);
+                        if (c != 0) lo |= half;
+                        if (c != W - 1) hi |= half;
+                    }
+                    mlo[d] = lo;
+                    mhi[d] = hi;
+                }
+                const u32x4 bq = __builtin_bit_cast(u32x4, bv);
+                const bf16x8 bfr[3] = {__builtin_bit_cast(bf16x8, bq & mlo), bv, __builtin_bit_cast(bf16x8, bq & mhi)};
+#pragma unroll
+                for (int t = 0; t < C::MTW; ++t) {
+                    // M tile t of this wave: tap compile-time (WM = 2: the wave's ci tile is wm)
+                    const int tap = C::WM == 2 ? t : t / 2, ct = C::WM == 2 ? wm : t % 2;
+                    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+                    const bf16x8 afr = frag_tr(reinterpret_cast<const unsigned short*>(
+                                                   xs + (dh + 1) * C::XRB + (pr + dw + 1) * C::PXB + (ct * 16 + cq) * 2),
+                                               16 * C::PXB / 2);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[dw + 1], afr, acc[t], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // lane holds dW[tap][ci = ct*16 + i16][co = wn*16 + 4g .. +3]
+#pragma unroll
+    for (int t = 0; t < C::MTW; ++t) {
+        const int tap = C::WM == 2 ? t : t / 2, ct = C::WM == 2 ? wm : t % 2;
+        float* o = out + ((size_t)tap * C::CI + ct * 16 + i16) * CO + wn * 16 + 4 * g;
+        *reinterpret_cast<floatx4*>(o) = acc[t];
+    }
+}
+
 template <int CI, int NO, int WN, bool FLIP, bool STATS, bool MASK>
 int launch_direct(const bf16* x, const bf16* w, const float* bias, const bf16* mask, bf16* y, float* stats,
                   int relu, int B, int H, int W, hipStream_t s) {
@@ -389,6 +562,50 @@ int conv_direct_fwd(const void* x, int B, int H, int W, int cin, const void* w_n
     OCRK_DF(64, 128, 4)
 #undef OCRK_DF
     return -1;
+}
+
+// weight gradient for Cin = 32: per-workgroup partials [grid][9][32][cout] in ws, then the split-K reduce
+size_t conv_direct_wgrad_ws_bytes(int B, int H, int W, int cin, int cout) {
+    if (cin != 32 || (cout != 32 && cout != 64)) return 0;
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int per_cu = cout == 32 ? WgCfg<32>::PER_CU : WgCfg<64>::PER_CU;
+    return (size_t)per_cu * (ncu > 0 ? ncu : 256) * 9 * cin * cout * sizeof(float);
+}
+
+int conv_direct_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw,
+                      int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+    const int mode = conv_direct_mode();
+    if (mode == 0 || cin != 32 || (cout != 32 && cout != 64)) return -1;
+    if (mode == 1 && cout != 32) return -1;           // conv3 (32 -> 64): the TN engine measured faster
+    if ((int64_t)B * H * W * (cout > cin ? cout : cin) * 2 > 0x7fffffffLL) return -1;
+    if (ws_bytes < conv_direct_wgrad_ws_bytes(B, H, W, cin, cout) || (uintptr_t)ws % 16 != 0) return -1;
+    const int M = B * H * W;
+    const int nchunks = (int)cdiv(M, CM);
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    int grid = (cout == 32 ? WgCfg<32>::PER_CU : WgCfg<64>::PER_CU) * ncu;   // co-resident
+    if (grid > nchunks) grid = nchunks;
+    const int cpw = (int)cdiv(nchunks, grid);
+    grid = (int)cdiv(nchunks, cpw);
+    if (cout == 32) {
+        static bool cfg = false;
+        if (!cfg) { (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<32>), hipFuncAttributeMaxDynamicSharedMemorySize, WgCfg<32>::LDS); cfg = true; }
+        conv3x3_wgrad_direct_kernel<32><<<grid, 256, WgCfg<32>::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, M, H, W, nchunks, cpw);
+    } else {
+        static bool cfg = false;
+        if (!cfg) { (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<64>), hipFuncAttributeMaxDynamicSharedMemorySize, WgCfg<64>::LDS); cfg = true; }
+        conv3x3_wgrad_direct_kernel<64><<<grid, 256, WgCfg<64>::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, M, H, W, nchunks, cpw);
+    }
+    int st = launch_status("conv3x3_wgrad_direct");
+    if (st) return st;
+    GemmParams p = {};
+    p.M = 9 * cin; p.N = cout; p.K = M; p.batch = 1;
+    p.C = dw; p.ldc = cout; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+    p.splits = grid; p.splitk_ws = (float*)ws;
+    return splitk_finish(p, s);
 }
 
 // backward-data: dx = conv_flip(dy) (x ReLU mask of the producer), optional tile column statistics

@@ -68,6 +68,9 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
 
 // Split-K GEMM: partials into p.splitk_ws, then a reduce applying the epilogue.
 size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits);
+// Sum p.splits f32 partials [splits][M][N] (p.splitk_ws) into C with the epilogue
+// (alpha, bias, relu, accumulate) -- also used by kernels that leave their own partials.
+int splitk_finish(const GemmParams& p, hipStream_t stream);
 
 // Pipelined LDS-DMA engine for bf16 A_ROWK / A_IM2COL / A_IM2COL_FLIP x B_NK
 // (gemm_nt.hip). Returns -1 when it does not cover the call (the caller then

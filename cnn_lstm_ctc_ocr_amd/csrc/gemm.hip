@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(256) splitk_reduce4p_kernel(const GemmParams p
     }
 }
 
-static int splitk_finish(const GemmParams& p, hipStream_t stream) {
+int splitk_finish(const GemmParams& p, hipStream_t stream) {
     if (p.splits <= 1) return OCRK_OK;
     int64_t MN = (int64_t)p.M * p.N;
     const bool v4 = p.N % 4 == 0 && p.ldc % 4 == 0 && p.strideC % 4 == 0 &&
