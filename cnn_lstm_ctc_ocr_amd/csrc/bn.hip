@@ -21,46 +21,48 @@ using ocrk::slab_sum;
 using ocrk::SLAB_P;
 
 // --------------------------------------------------------------- finalize
-// One block per channel: Chan-merge the per-tile (sum, M2) partials.
+// One block per channel: merge the per-tile (sum, M2) partials in double.
+// M2 of the union = sum(M2_b) + sum(s_b^2 / n_b) - S^2 / N (the between-tile
+// term, exact in double at these magnitudes): plain sums per thread -- no
+// dependent divisions in the tile loop, loads of 4 tiles in flight -- then a
+// fixed-order tree over the block (deterministic).
 __global__ void __launch_bounds__(256)
 bn_finalize_kernel(const float* __restrict__ stats, int tiles, int64_t M, int tile_rows, int C,
                    float eps, float momentum, float* __restrict__ mean_out, float* __restrict__ invstd_out,
                    float* __restrict__ moving_mean, float* __restrict__ moving_var) {
-    __shared__ double sn[256], smean[256], sm2[256];
+    __shared__ double ss[256], sq[256], sw[256];
     const int c = blockIdx.x;
-    double n = 0, mean = 0, m2 = 0;
+    const int full = (int)(M / tile_rows);                 // tiles with tile_rows rows
+    const double inv_full = 1.0 / (double)tile_rows;
+    double S = 0, Q = 0, W2 = 0;
+#pragma unroll 4
     for (int t = threadIdx.x; t < tiles; t += 256) {
-        double nb = (double)min<int64_t>(tile_rows, M - (int64_t)t * tile_rows);
-        double sb = stats[(int64_t)t * 2 * C + c];
-        double m2b = stats[(int64_t)t * 2 * C + C + c];
-        double mb = sb / nb;
-        double nt = n + nb, d = mb - mean;
-        mean += d * nb / nt;
-        m2 += m2b + d * d * n * nb / nt;
-        n = nt;
+        const double sb = stats[(int64_t)t * 2 * C + c];
+        const double m2b = stats[(int64_t)t * 2 * C + C + c];
+        const double inv_nb = t < full ? inv_full : 1.0 / (double)(M - (int64_t)t * tile_rows);
+        S += sb;
+        Q += sb * sb * inv_nb;
+        W2 += m2b;
     }
-    sn[threadIdx.x] = n; smean[threadIdx.x] = mean; sm2[threadIdx.x] = m2;
+    ss[threadIdx.x] = S; sq[threadIdx.x] = Q; sw[threadIdx.x] = W2;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
         if (threadIdx.x < s) {
-            double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
-            double nt = na + nb;
-            if (nb > 0) {
-                double d = smean[threadIdx.x + s] - smean[threadIdx.x];
-                smean[threadIdx.x] += d * nb / nt;
-                sm2[threadIdx.x] += sm2[threadIdx.x + s] + d * d * na * nb / nt;
-                sn[threadIdx.x] = nt;
-            }
+            ss[threadIdx.x] += ss[threadIdx.x + s];
+            sq[threadIdx.x] += sq[threadIdx.x + s];
+            sw[threadIdx.x] += sw[threadIdx.x + s];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        double nt = sn[0], mu = smean[0], var = sm2[0] / nt;
+        const double nt = (double)M, mu = ss[0] / nt;
+        const double m2 = fmax(sw[0] + sq[0] - ss[0] * mu, 0.0);
+        const double var = m2 / nt;
         mean_out[c] = (float)mu;
         invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
         if (moving_mean) {
             float dec = 1.f - momentum;
-            double var_u = nt > 1 ? sm2[0] / (nt - 1) : var;
+            double var_u = nt > 1 ? m2 / (nt - 1) : var;
             moving_mean[c] = moving_mean[c] - (moving_mean[c] - (float)mu) * dec;
             moving_var[c] = moving_var[c] - (moving_var[c] - (float)var_u) * dec;
         }

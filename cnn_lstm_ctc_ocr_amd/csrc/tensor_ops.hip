@@ -204,6 +204,64 @@ extern "C" int ocrk_strided_copy(const float* in, int64_t rows, int64_t cols, in
     return ocrk::launch_status("ocrk_strided_copy");
 }
 
+// All weight images of a parameter version in ONE launch: a table of 2-D
+// copies out[r*out_rs + c] = in[r*in_rs + c] (plain) or out[c*out_rs + r] =
+// in[r*in_rs + c] (transposed), f32 -> dtype, cut into 32 x 32 tiles. A
+// workgroup finds its job by binary search over the tiles' prefix offsets,
+// stages the tile in LDS and writes it back row-contiguous either way (the
+// per-image strided copies wrote one side 2 bytes at a time).
+struct CopyJob {
+    const float* src;
+    void* dst;
+    int64_t rows, cols, in_rs, out_rs, tile0;
+    int transpose, dtype;
+};
+static_assert(sizeof(CopyJob) == 8 * 8, "job layout (include/ocrk.h)");
+
+__global__ void __launch_bounds__(256) copy_batch_kernel(const CopyJob* __restrict__ jobs, int njobs) {
+    __shared__ float tile[32][33];
+    const int64_t t = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {                                   // last job with tile0 <= t
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].tile0 <= t) lo = mid; else hi = mid - 1;
+    }
+    const CopyJob j = jobs[lo];
+    const int64_t lt = t - j.tile0, tc = (j.cols + 31) / 32;
+    const int64_t r0 = (lt / tc) * 32, c0 = (lt % tc) * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;      // 32 x 8
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t r = r0 + ty + 8 * k, c = c0 + tx;
+        tile[ty + 8 * k][tx] = (r < j.rows && c < j.cols) ? j.src[r * j.in_rs + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int64_t orow, ocol;
+        float v;
+        if (j.transpose) {                              // out row = input column
+            orow = c0 + ty + 8 * k; ocol = r0 + tx;
+            v = tile[tx][ty + 8 * k];
+            if (orow >= j.cols || ocol >= j.rows) continue;
+        } else {
+            orow = r0 + ty + 8 * k; ocol = c0 + tx;
+            v = tile[ty + 8 * k][tx];
+            if (orow >= j.rows || ocol >= j.cols) continue;
+        }
+        const int64_t o = orow * j.out_rs + ocol;
+        if (j.dtype == OCRK_BF16) reinterpret_cast<bf16*>(j.dst)[o] = (bf16)v;
+        else reinterpret_cast<float*>(j.dst)[o] = v;
+    }
+}
+
+extern "C" int ocrk_copy_batch(const void* jobs, int njobs, int64_t total_tiles, void* stream) {
+    OCRK_REQUIRE(njobs >= 1 && total_tiles >= 1 && total_tiles < (1ll << 31), "ocrk_copy_batch: njobs=%d tiles=%lld",
+                 njobs, (long long)total_tiles);
+    copy_batch_kernel<<<(unsigned)total_tiles, 256, 0, ocrk::as_stream(stream)>>>((const CopyJob*)jobs, njobs);
+    return ocrk::launch_status("ocrk_copy_batch");
+}
+
 // x[i] *= s[0]  (upstream scalar gradient applied on device, no host sync)
 __global__ void __launch_bounds__(256) mul_scalar_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ s) {
     const float v = s[0];

@@ -379,6 +379,13 @@ def permute3(x, d0, d1, d2, dtype, out=None):
     return out
 
 
+def copy_batch(table, njobs, total_tiles, stream_of):
+    """One launch of the 2-D copy jobs in `table` (int64 device tensor [njobs, 8],
+    include/ocrk.h ocrk_copy_batch): the weight images of a parameter version."""
+    _chk(table, stream_of)
+    call("ocrk_copy_batch", ptr(table), int(njobs), int(total_tiles), _stream(stream_of))
+
+
 def strided_copy(src, rows, cols, in_rs, in_cs, out, out_rs, out_cs, out_offset=0, in_offset=0):
     """out.flat[out_offset + r*out_rs + c*out_cs] = src.flat[in_offset + r*in_rs + c*in_cs]."""
     _chk(src, out)

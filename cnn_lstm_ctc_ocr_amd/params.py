@@ -9,6 +9,8 @@ tensors are views. The compute-dtype weight images the kernels read (GEMM
 layouts, bf16 casts) are derived from the master copy once per parameter
 version (see `images()`).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -181,15 +183,111 @@ class ParamStore:
         """The master values changed: derived weight images are stale."""
         self.version += 1
         self._images.clear()
+        self._plan_fresh = False
 
     # ---------------------------------------------------- weight images
     def images(self, key, builder):
-        """Cache of compute-dtype weight layouts, rebuilt once per version."""
+        """Compute-dtype weight layouts, rebuilt once per parameter version. The
+        model's images in its compute dtype are stable buffers refreshed together
+        by ONE batched launch (ocrk_copy_batch, the job table built once);
+        other keys fall back to `builder`."""
+        plan = self._plan_for(key)
+        if plan is not None:
+            if not self._plan_fresh:
+                K.copy_batch(plan["table"], plan["njobs"], plan["tiles"], self.flat)
+                self._plan_fresh = True
+            return plan["images"][key]
         img = self._images.get(key)
         if img is None:
             img = builder()
             self._images[key] = img
         return img
+
+    def _plan_for(self, key):
+        if self.device.type != "cuda" or os.environ.get("OCRK_BATCHED_IMAGES", "1") == "0":
+            return None
+        dtype = key[-1]
+        if dtype != self.cfg.dtype:
+            return None
+        plan = getattr(self, "_plan", None)
+        if plan is None:
+            plan = self._plan = self._build_plan(dtype)
+            self._plan_fresh = False
+        return plan if key in plan["images"] else None
+
+    def _build_plan(self, dtype):
+        """Allocate every weight image once and the copy-job table (rows of
+        src, dst, rows, cols, in_rs, out_rs, first tile, transpose | dtype << 32)."""
+        dev = self.device
+        esz = torch.empty(0, dtype=dtype).element_size()
+        code = K.dtype_code(dtype)
+        jobs, images = [], {}
+
+        def job(src, s_off, rows, cols, in_rs, dst, d_off, out_rs, transpose):
+            jobs.append([src.data_ptr() + 4 * s_off, dst.data_ptr() + esz * d_off, rows, cols, in_rs, out_rs, 0,
+                         int(transpose) | (code << 32)])
+
+        for li in range(2, 9):
+            w = self.params[f"convnet/conv{li}/kernel"]                      # [3][3][Cin][Cout]
+            kh, kw, cin, cout = w.shape
+            w_nk = torch.empty(cout, kh * kw * cin, dtype=dtype, device=dev)
+            w_bwd = torch.empty(cin, kh * kw * cout, dtype=dtype, device=dev)
+            job(w, 0, kh * kw * cin, cout, cout, w_nk, 0, kh * kw * cin, True)
+            for t in range(kh * kw):
+                job(w, t * cin * cout, cin, cout, cout, w_bwd, t * cout, kh * kw * cout, False)
+            images[("conv", f"conv{li}", dtype)] = (w_nk, w_bwd)
+        for layer in range(1, len(self.cfg.rnn_sizes) + 1):
+            pre = f"rnn/bdrnn{layer}"
+            if self.cfg.cell == "lstm":
+                kf = self.params[f"{pre}/fw/lstm_cell/kernel"]
+                rows, G = kf.shape
+                H = G // 4
+                n_in = rows - H
+                wxT = torch.empty(2 * G, n_in, dtype=dtype, device=dev)
+                wx = torch.empty(n_in, 2 * G, dtype=dtype, device=dev)
+                whT = torch.empty(2, G, H, dtype=dtype, device=dev)
+                wh = torch.empty(2, H, G, dtype=dtype, device=dev)
+                for d, dn in enumerate(("fw", "bw")):
+                    k = self.params[f"{pre}/{dn}/lstm_cell/kernel"]
+                    job(k, 0, n_in, G, G, wxT, d * G * n_in, n_in, True)
+                    job(k, 0, n_in, G, G, wx, d * G, 2 * G, False)
+                    job(k, n_in * G, H, G, G, whT, d * G * H, H, True)
+                    job(k, n_in * G, H, G, G, wh, d * H * G, G, False)
+                images[("lstm", layer, dtype)] = (wxT, wx, whT, wh, self.flat_bias_pair(layer))
+            else:
+                gk = self.params[f"{pre}/fw/gru_cell/gates/kernel"]
+                rows, G2 = gk.shape
+                H = G2 // 2
+                n_in = rows - H
+                G3 = 3 * H
+                wxT = torch.empty(2 * G3, n_in, dtype=dtype, device=dev)
+                wx = torch.empty(n_in, 2 * G3, dtype=dtype, device=dev)
+                whgT = torch.empty(2, G2, H, dtype=dtype, device=dev)
+                whcT = torch.empty(2, H, H, dtype=dtype, device=dev)
+                whg = torch.empty(2, H, G2, dtype=dtype, device=dev)
+                whc = torch.empty(2, H, H, dtype=dtype, device=dev)
+                for d, dn in enumerate(("fw", "bw")):
+                    g = self.params[f"{pre}/{dn}/gru_cell/gates/kernel"]
+                    c = self.params[f"{pre}/{dn}/gru_cell/candidate/kernel"]
+                    job(g, 0, n_in, G2, G2, wxT, d * G3 * n_in, n_in, True)
+                    job(c, 0, n_in, H, H, wxT, (d * G3 + G2) * n_in, n_in, True)
+                    job(g, 0, n_in, G2, G2, wx, d * G3, 2 * G3, False)
+                    job(c, 0, n_in, H, H, wx, d * G3 + G2, 2 * G3, False)
+                    job(g, n_in * G2, H, G2, G2, whgT, d * G2 * H, H, True)
+                    job(c, n_in * H, H, H, H, whcT, d * H * H, H, True)
+                    job(g, n_in * G2, H, G2, G2, whg, d * H * G2, G2, False)
+                    job(c, n_in * H, H, H, H, whc, d * H * H, H, False)
+                images[("gru", layer, dtype)] = (wxT, wx, whgT, whcT, whg, whc, self.gru_bias_cat(layer))
+        lk = self.params["rnn/logits/kernel"]
+        limg = torch.empty(lk.shape, dtype=dtype, device=dev)
+        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limg, 0, lk.shape[1], False)
+        images[("logits", dtype)] = limg
+        tiles = 0
+        for j in jobs:
+            j[6] = tiles
+            tiles += -(-j[2] // 32) * -(-j[3] // 32)
+        table = torch.tensor(jobs, dtype=torch.int64).to(dev)
+        return {"table": table, "njobs": len(jobs), "tiles": tiles, "images": images}
 
     def conv_images(self, name, dtype):
         """conv2..8: w_nk [Cout][3][3][Cin] (forward), w_bwd [Cin][3][3][Cout]."""

@@ -273,6 +273,14 @@ int ocrk_gemm(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
 int ocrk_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_t, float beta1,
               float beta2, float eps, float grad_scale, void* stream);
 
+/* Batched weight images: ONE launch for a table of 2-D copies (device array of
+ * `njobs` records of 8 x 8 bytes: {const float* src; void* dst; int64 rows, cols,
+ * in_rs, out_rs, tile0; int32 transpose, dtype}), tile0 = the job's first 32x32
+ * tile (prefix sum, ascending), total_tiles = all jobs' tiles. Plain:
+ * dst[r*out_rs + c] = src[r*in_rs + c]; transposed: dst[c*out_rs + r] =
+ * src[r*in_rs + c]; f32 -> dtype. Replaces the per-image ocrk_strided_copy /
+ * ocrk_permute3 launches of a parameter version (ParamStore.refresh_images). */
+int ocrk_copy_batch(const void* jobs, int njobs, int64_t total_tiles, void* stream);
 /* -------------------------------------------------------------- utilities */
 int ocrk_cast(const void* in, int in_dtype, void* out, int out_dtype, int64_t n, void* stream);
 int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d2, void* out, int out_dtype,
