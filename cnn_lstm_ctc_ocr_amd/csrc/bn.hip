@@ -21,28 +21,68 @@ using ocrk::slab_sum;
 using ocrk::SLAB_P;
 
 // --------------------------------------------------------------- finalize
-// One block per channel: merge the per-tile (sum, M2) partials in double.
+// Merge the per-tile (sum, M2) partials of the [tiles][2C] table in double:
 // M2 of the union = sum(M2_b) + sum(s_b^2 / n_b) - S^2 / N (the between-tile
-// term, exact in double at these magnitudes): plain sums per thread -- no
-// dependent divisions in the tile loop, loads of 4 tiles in flight -- then a
-// fixed-order tree over the block (deterministic).
+// term; exact in double at these magnitudes). Every row of the table holds
+// all channels, so a block per channel would drag every cache line of the
+// table through each of C CUs; instead pass 1 (bn_stats_partial_kernel)
+// sums row ranges across all columns with row-contiguous loads, pass 2
+// (bn_finalize_kernel, a block per channel) adds the ranges in a fixed tree
+// order (deterministic) and finalizes.
+constexpr int BN_PARTS = 256;
 __global__ void __launch_bounds__(256)
-bn_finalize_kernel(const float* __restrict__ stats, int tiles, int64_t M, int tile_rows, int C,
-                   float eps, float momentum, float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                   float* __restrict__ moving_mean, float* __restrict__ moving_var) {
+bn_stats_partial_kernel(const float* __restrict__ stats, int tiles, int64_t M, int tile_rows, int C, int rpb,
+                        double* __restrict__ part) {
+    __shared__ double sacc[3 * 256];                    // [lanes][3][C] with lanes * C <= 256 ... see below
+    const int NC = 2 * C;
+    const int lanes = NC <= 256 ? 256 / NC : 1;         // table rows read at once
+    const int full = (int)(M / tile_rows);
+    const double inv_full = 1.0 / (double)tile_rows;
+    const int t0 = blockIdx.x * rpb, t1 = min(tiles, t0 + rpb);
+    double a[2] = {0, 0}, q[2] = {0, 0};
+    const int lr = NC <= 256 ? threadIdx.x / NC : 0;
+    const int j0 = NC <= 256 ? threadIdx.x % NC : threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = j0 + 256 * h;
+        if (j >= NC || (h == 1 && NC <= 256)) continue;
+        for (int t = t0 + lr; t < t1; t += lanes) {
+            const double v = stats[(int64_t)t * NC + j];
+            a[h] += v;
+            if (j < C) q[h] += v * v * (t < full ? inv_full : 1.0 / (double)(M - (int64_t)t * tile_rows));
+        }
+    }
+    // lane partials -> shared [3][C] in lane order (lanes * NC == 256 when NC <= 256)
+    for (int l = 0; l < lanes; ++l) {
+        if (lr == l) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = j0 + 256 * h;
+                if (j >= NC || (h == 1 && NC <= 256)) continue;
+                if (j < C) {
+                    sacc[j] = (l == 0 ? 0.0 : sacc[j]) + a[h];
+                    sacc[C + j] = (l == 0 ? 0.0 : sacc[C + j]) + q[h];
+                } else {
+                    sacc[2 * C + (j - C)] = (l == 0 ? 0.0 : sacc[2 * C + (j - C)]) + a[h];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (int k = threadIdx.x; k < 3 * C; k += 256) part[(int64_t)blockIdx.x * 3 * C + k] = sacc[k];
+}
+
+__global__ void __launch_bounds__(256)
+bn_finalize_kernel(const double* __restrict__ part, int nparts, int64_t M, int C, float eps, float momentum,
+                   float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ moving_mean,
+                   float* __restrict__ moving_var) {
     __shared__ double ss[256], sq[256], sw[256];
     const int c = blockIdx.x;
-    const int full = (int)(M / tile_rows);                 // tiles with tile_rows rows
-    const double inv_full = 1.0 / (double)tile_rows;
     double S = 0, Q = 0, W2 = 0;
-#pragma unroll 4
-    for (int t = threadIdx.x; t < tiles; t += 256) {
-        const double sb = stats[(int64_t)t * 2 * C + c];
-        const double m2b = stats[(int64_t)t * 2 * C + C + c];
-        const double inv_nb = t < full ? inv_full : 1.0 / (double)(M - (int64_t)t * tile_rows);
-        S += sb;
-        Q += sb * sb * inv_nb;
-        W2 += m2b;
+    for (int b = threadIdx.x; b < nparts; b += 256) {
+        S += part[(int64_t)b * 3 * C + c];
+        Q += part[(int64_t)b * 3 * C + C + c];
+        W2 += part[(int64_t)b * 3 * C + 2 * C + c];
     }
     ss[threadIdx.x] = S; sq[threadIdx.x] = Q; sw[threadIdx.x] = W2;
     __syncthreads();
@@ -465,12 +505,24 @@ bn_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ da_in, int np
 }
 
 // ------------------------------------------------------------------ C ABI
-extern "C" int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps,
-                                float momentum, float* mean, float* invstd, float* moving_mean,
-                                float* moving_var, void* stream) {
-    OCRK_REQUIRE(tiles >= 1 && C >= 1 && M >= 1, "ocrk_bn_finalize: bad sizes");
-    bn_finalize_kernel<<<C, 256, 0, ocrk::as_stream(stream)>>>(stats, tiles, M, 128, C, eps, momentum, mean,
-                                                               invstd, moving_mean, moving_var);
+extern "C" size_t ocrk_bn_finalize_workspace_size(int tiles, int C) {
+    return (size_t)std::min(BN_PARTS, std::max(1, tiles)) * 3 * C * sizeof(double);
+}
+
+extern "C" int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
+                                float* mean, float* invstd, float* moving_mean, float* moving_var, void* ws,
+                                size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(tiles >= 1 && C >= 1 && C <= 256 && M >= 1, "ocrk_bn_finalize: bad sizes");
+    OCRK_REQUIRE(ws && ws_bytes >= ocrk_bn_finalize_workspace_size(tiles, C), "ocrk_bn_finalize: workspace too small");
+    hipStream_t s = ocrk::as_stream(stream);
+    const int np0 = std::min(BN_PARTS, tiles);
+    const int rpb = (tiles + np0 - 1) / np0;
+    const int np = (tiles + rpb - 1) / rpb;
+    bn_stats_partial_kernel<<<np, 256, 0, s>>>(stats, tiles, M, 128, C, rpb, (double*)ws);
+    int st = ocrk::launch_status("ocrk_bn_finalize partial sums");
+    if (st) return st;
+    bn_finalize_kernel<<<C, 256, 0, s>>>((const double*)ws, np, M, C, eps, momentum, mean, invstd, moving_mean,
+                                         moving_var);
     return ocrk::launch_status("ocrk_bn_finalize");
 }
 

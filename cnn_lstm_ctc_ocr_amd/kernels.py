@@ -129,8 +129,10 @@ def bn_finalize(stats, M, C, eps, momentum, moving_mean=None, moving_var=None):
     tiles = stats.shape[0]
     mean = torch.empty(C, dtype=torch.float32, device=stats.device)
     invstd = torch.empty_like(mean)
+    nb = _lib.lib().ocrk_bn_finalize_workspace_size(tiles, C)
+    ws = _ws(nb, stats.device)
     call("ocrk_bn_finalize", ptr(stats), tiles, M, C, float(eps), float(momentum), ptr(mean), ptr(invstd),
-         ptr(moving_mean), ptr(moving_var), _stream(stats))
+         ptr(moving_mean), ptr(moving_var), ptr(ws), nb, _stream(stats))
     return mean, invstd
 
 

@@ -337,8 +337,8 @@ class _Logits(torch.autograd.Function):
     def forward(ctx, x, store, *variables):
         dt = store.cfg.dtype
         T, B, D = x.shape
-        w = store.logits_image(dt)
-        logits = K.gemm(x.view(T * B, D), w, bias=store.params["rnn/logits/bias"], relu=True)
+        wT = store.logits_image_t(dt)                                   # [C][D]: the NT engine's operand
+        logits = K.gemm(x.view(T * B, D), wT, trans_b=True, bias=store.params["rnn/logits/bias"], relu=True)
         logits = logits.view(T, B, -1)
         ctx.store = store
         ctx.save_for_backward(x, logits)

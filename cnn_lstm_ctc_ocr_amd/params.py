@@ -278,10 +278,13 @@ class ParamStore:
                     job(g, n_in * G2, H, G2, G2, whg, d * H * G2, G2, False)
                     job(c, n_in * H, H, H, H, whc, d * H * H, H, False)
                 images[("gru", layer, dtype)] = (wxT, wx, whgT, whcT, whg, whc, self.gru_bias_cat(layer))
-        lk = self.params["rnn/logits/kernel"]
+        lk = self.params["rnn/logits/kernel"]                               # [D][C]
         limg = torch.empty(lk.shape, dtype=dtype, device=dev)
+        limgT = torch.empty(lk.shape[1], lk.shape[0], dtype=dtype, device=dev)
         job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limg, 0, lk.shape[1], False)
+        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limgT, 0, lk.shape[0], True)
         images[("logits", dtype)] = limg
+        images[("logitsT", dtype)] = limgT
         tiles = 0
         for j in jobs:
             j[6] = tiles
@@ -396,3 +399,9 @@ class ParamStore:
         def build():
             return K.cast(self.params["rnn/logits/kernel"].contiguous(), dtype)
         return self.images(("logits", dtype), build)
+
+    def logits_image_t(self, dtype):
+        """[C][D]: the logits weight transposed (the forward GEMM's B_NK operand)."""
+        def build():
+            return K.cast(self.params["rnn/logits/kernel"].t().contiguous(), dtype)
+        return self.images(("logitsT", dtype), build)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 2
+#define OCRK_ABI_VERSION 3
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -148,8 +148,10 @@ int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, 
  * (:111-116, :145-146). bn_finalize: TRAIN-mode batch statistics from the conv
  * epilogue partials (mean, 1/sqrt(var+eps)) and the [TF1] moving averages
  * (moving_mean/var may be NULL = no update). bn_infer_params: INFER mode. */
+size_t ocrk_bn_finalize_workspace_size(int tiles, int C);
 int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
-                     float* mean, float* invstd, float* moving_mean, float* moving_var, void* stream);
+                     float* mean, float* invstd, float* moving_mean, float* moving_var, void* ws, size_t ws_bytes,
+                     void* stream);   /* ws: ocrk_bn_finalize_workspace_size bytes (row-range partial sums) */
 int ocrk_bn_infer_params(const float* moving_mean, const float* moving_var, int C, float eps,
                          float* mean, float* invstd, void* stream);
 /* out = maxpool(relu(gamma (z-mean) invstd + beta)), window kh x kw, stride
