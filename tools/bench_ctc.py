@@ -1,6 +1,8 @@
 """CTC loss (+ gradient) kernel timing at the bench shape (diagnostic).
 
     python tools/bench_ctc.py        # T=125, B=256, C=96, labels of 2..19 symbols
+    python tools/bench_ctc.py --long # T=600, labels of 100..200 symbols (S up to 401:
+                                     # the R = 8 lattice instance)
 Prints per-launch time with the gradient and loss-only, for the lattices in
 LDS (default) and in the global workspace (OCRK_CTC_LDS=0)."""
 import os
@@ -26,12 +28,14 @@ def timed(fn, reps=20):
 
 
 def main():
-    T, B, C = 125, 256, 96
+    long = "--long" in sys.argv
+    T, B, C = (600, 256, 96) if long else (125, 256, 96)
+    lo, hi = (100, 201) if long else (2, 20)
     rng = np.random.default_rng(0)
     dev = torch.device("cuda")
     logits = torch.from_numpy(np.maximum(rng.standard_normal((T, B, C)) * 3, 0).astype(np.float32)).to(dev)
-    ln = rng.integers(2, 20, B).astype(np.int32)
-    lab = np.zeros((B, 19), np.int32)
+    ln = rng.integers(lo, hi, B).astype(np.int32)
+    lab = np.zeros((B, hi - 1), np.int32)
     for i in range(B):
         lab[i, :ln[i]] = rng.integers(0, C - 1, ln[i])
     lab, ln = torch.from_numpy(lab).to(dev), torch.from_numpy(ln).to(dev)
