@@ -149,6 +149,30 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             pstamp(dbg, s, 1);
             // 2. stage h_{s-1} rows (sc1 loads: the bytes were written through by other CUs)
             const int64_t base = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
+            if constexpr (KS == 16) {
+                // H = 512: one 1-KB row per LDS-DMA wave instruction, 8 rows per wave,
+                // straight into the padded LDS rows (drained before the barrier below)
+                const int wu = __builtin_amdgcn_readfirstlane(w);
+                const unsigned lo = (unsigned)(lane * 16);
+                if (local) {
+#pragma unroll
+                    for (int q = 0; q < PBR / 4; ++q) {
+                        const int r = wu * (PBR / 4) + q;
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
+                            (unsigned)((base + (int64_t)r * H) * 2) + lo, 0, 0, 2);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < PBR / 4; ++q) {
+                        const int r = wu * (PBR / 4) + q;
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
+                            (unsigned)((base + (int64_t)r * H) * 2) + lo, 0, 0, 16);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
             u32x4 hv[PBR * H / 8 / 256];
 #pragma unroll
             for (int v = 0; v < PBR * H / 8 / 256; ++v) {
@@ -162,6 +186,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                 const int idx = tid + 256 * v;
                 const int row = idx / (H / 8), kq = idx % (H / 8);
                 *reinterpret_cast<u32x4*>(&sh[row * LDH + 8 * kq]) = hv[v];
+            }
             }
         }
 #pragma unroll
@@ -369,17 +394,46 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                         acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][ks], acc[mt][j], 0, 0, 0);
                 }
             };
-            u32x4 v0[NI], v1[NI];
-            load_rows(v0, 0);
-            load_rows(v1, 8);
-            store_rows(v0, 0);
-            load_rows(v0, 16);
-            store_rows(v1, 8);
-            load_rows(v1, 24);
-            mma_tile(0);
-            store_rows(v0, 16);
-            store_rows(v1, 24);
-            mma_tile(1);
+            if constexpr (KS == 16) {
+                // H = 512: a dz row of the wave's k-range is 1 KB = one LDS-DMA wave
+                // instruction (16 B per lane) straight into its padded LDS row -- all
+                // 32 rows in flight at once, no VGPR round trip; M-tile 0 multiplies
+                // as soon as its 16 rows have landed (counted vmcnt: everything issued
+                // before the DMAs is older, so vmcnt(16) covers rows 0-15)
+                const int wu = __builtin_amdgcn_readfirstlane(w);
+                unsigned short* sau = sA + wu * PBR * LDA;
+                const int64_t rb = ((int64_t)(((i - 1) & 1) * 2 + dir) * B + b0) * G4 + wu * H;
+                const unsigned lo = (unsigned)(lane * 16);
+                if (local) {
+#pragma unroll
+                    for (int r = 0; r < PBR; ++r)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            zx_rsrc, (__attribute__((address_space(3))) void*)(sau + r * LDA), 16,
+                            (unsigned)((rb + (int64_t)r * G4) * 2) + lo, 0, 0, 2);      // nt
+                } else {
+#pragma unroll
+                    for (int r = 0; r < PBR; ++r)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            zx_rsrc, (__attribute__((address_space(3))) void*)(sau + r * LDA), 16,
+                            (unsigned)((rb + (int64_t)r * G4) * 2) + lo, 0, 0, 16);     // sc1
+                }
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                mma_tile(0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                mma_tile(1);
+            } else {
+                u32x4 v0[NI], v1[NI];
+                load_rows(v0, 0);
+                load_rows(v1, 8);
+                store_rows(v0, 0);
+                load_rows(v0, 16);
+                store_rows(v1, 8);
+                load_rows(v1, 24);
+                mma_tile(0);
+                store_rows(v0, 16);
+                store_rows(v1, 24);
+                mma_tile(1);
+            }
         }
         // 3. the four partial products (one per gate's k-range) meet in LDS
 #pragma unroll
