@@ -1,0 +1,64 @@
+"""bf16 BN -> ReLU -> max-pool backward (csrc/bn.hip: bn_bwd_route_kernel,
+bn_bwd_apply_kernel) against the float64 oracle (oracle/ref_graph.py bn_bwd,
+maxpool_bwd, relu_bwd restating src/weinman/model.py:105-123 with [TF1]
+MaxPoolGrad's first-max routing), on the bench step's four BN layers (pool
+2x2/[2,2], 2x2/[2,1] x2, [3,1]/[3,1] time-major) at a reduced batch, plus
+odd widths / uncovered rows / columns."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_graph as G
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (B, H, W, C, pool)
+    (4, 30, 254, 32, (2, 2, 2, 2)),
+    (4, 15, 127, 64, (2, 2, 2, 1)),
+    (4, 7, 126, 128, (2, 2, 2, 1)),
+    (4, 3, 125, 256, (3, 1, 3, 1)),
+    (3, 7, 37, 32, (2, 2, 2, 2)),       # odd width: an uncovered column; H = 7: an uncovered row
+    (3, 9, 11, 64, (2, 2, 2, 1)),
+    (2, 3, 9, 512, (3, 1, 3, 1)),
+]
+
+
+def _bf(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).bfloat16().float().numpy()
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:4])) + f"-p{''.join(map(str, c[4]))}")
+def test_bn_bwd_bf16_vs_oracle(cuda, case):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    B, H, W, C, pool = case
+    rng = np.random.default_rng(B * H + W + C)
+    z = _bf(rng.standard_normal((B, H, W, C)) * 1.5 + 0.3)
+    gamma = (rng.random(C) + 0.5).astype(np.float32)
+    beta = (rng.standard_normal(C) * 0.2).astype(np.float32)
+    a, mean, var, _var_u, cache = G.bn_train(z.astype(np.float64), gamma.astype(np.float64), beta.astype(np.float64))
+    tm = pool == (3, 1, 3, 1)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(cuda)   # noqa: E731
+    mean_d = t(mean)
+    inv_d = t(1 / np.sqrt(var + 1e-3))
+    zd = t(z).bfloat16()
+    p = Kn.bn_relu_pool_fwd(zd, mean_d, inv_d, t(gamma), t(beta), pool, time_major=tm)
+    dp = _bf(rng.standard_normal(p.shape))
+    dpd = t(dp).bfloat16()
+
+    dg, db = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    dbias = torch.zeros(C, device=cuda)
+    dz = Kn.bn_relu_pool_bwd(zd, dpd, mean_d, inv_d, t(gamma), t(beta), pool, tm, dg, db, accumulate=False, dbias=dbias)
+    torch.cuda.synchronize()
+    got = dz.float().cpu().numpy(), dg.cpu().numpy(), db.cpu().numpy(), dbias.cpu().numpy()
+    scale = np.abs(got[0]).max()
+
+    # float64 oracle on the same bf16 inputs (the routing is recomputed from the device's bf16 z)
+    y = G.relu(a)
+    dp_nchw = dp.transpose(1, 0, 2)[:, None] if tm else dp
+    dy = G.maxpool_bwd(y, dp_nchw.astype(np.float64), *pool)
+    dz_ref, dg_ref, db_ref = G.bn_bwd(G.relu_bwd(y, dy), cache, gamma.astype(np.float64))
+    rel = lambda x, r: float(np.linalg.norm(x - r) / max(np.linalg.norm(r), 1e-30))   # noqa: E731
+    assert rel(got[0], dz_ref) < 1e-2
+    assert rel(got[1], dg_ref) < 1e-3
+    assert rel(got[2], db_ref) < 1e-3
+    assert np.abs(got[3] - dz_ref.sum(axis=(0, 1, 2))).max() <= 1e-3 * scale * np.sqrt(B * H * W)
