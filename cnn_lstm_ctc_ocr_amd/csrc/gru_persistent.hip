@@ -218,7 +218,13 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
         put8((gu64*)(hx + ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu), pack4(hst), local);
         group_post(gflags + member, 2u * s + 2u, local);
         // 4. layer output and the tensors saved for the backward pass (drain behind the next step)
-        if (valid) st4(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu, hst);
+        {
+            // padded positions (t = s >= len) get this direction's zeros: the caller need not clear out
+            float ov[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = valid ? hst[e] : 0.f;
+            st4(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu, ov);
+        }
         st4(hprev_t + tb * H + u0 + eu, hp);
         st4(rh_t + tb * H + u0 + eu, rh);
         bf16* a = acts_t + tb * G3 + u0 + eu;

@@ -265,7 +265,13 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
         // 7. the layer output and the tensors saved for the backward pass
         //    (time order; they drain behind the next step)
         const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
-        if (valid) st4(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu, hn);
+        {
+            // padded positions (t = s >= len) get this direction's zeros: the caller need not clear out
+            float ov[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ov[e] = valid ? hn[e] : 0.f;
+            st4(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu, ov);
+        }
         st4(hprev_t + tb * H + u0 + eu, hp);
         st4(cprev_t + tb * H + u0 + eu, cp);
 #pragma unroll

@@ -260,7 +260,7 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
         raise TypeError(f"lstm_fwd: gx and whT must be {dtype} (got {gx.dtype}, {whT.dtype})")
     dev = gx.device
     if lstm_persistent_ok(B, H, dtype):
-        out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+        out = torch.empty(T, B, 2 * H, dtype=dtype, device=dev)       # padded steps written as zeros by the kernel
         hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
         cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
         acts = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
@@ -324,7 +324,7 @@ def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
         raise TypeError(f"gru_fwd: gx and weights must be {dtype} (got {gx.dtype}, {whgT.dtype})")
     dev = gx.device
     if gru_persistent_ok(B, H, dtype):
-        out = torch.zeros(T, B, 2 * H, dtype=dtype, device=dev)
+        out = torch.empty(T, B, 2 * H, dtype=dtype, device=dev)       # padded steps written as zeros by the kernel
         hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
         rh_t = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
         acts = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
