@@ -224,25 +224,37 @@ conv3x3_direct_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, co
         for (int i = 0; i < C::MTW; ++i)
 #pragma unroll
             for (int j = 0; j < C::NTW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // the A fragments of a tap row (3 taps) are read ahead of its MFMAs, so the
+        // LDS latency is paid once per tap row instead of once per fragment
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int kh = tap / 3, kw = tap % 3;
-            const int dh = FLIP ? 1 - kh : kh - 1, dw = FLIP ? 1 - kw : kw - 1;
+        for (int kh = 0; kh < 3; ++kh) {
+            bf16x8 af[3][C::MTW][C::KB];
 #pragma unroll
-            for (int i = 0; i < C::MTW; ++i) {
-                const bool ok = (dh < 0 ? prow[i] != 0 : (dh > 0 ? prow[i] != H - 1 : true)) &&
-                                (dw < 0 ? pcol[i] != 0 : (dw > 0 ? pcol[i] != W - 1 : true));
-                const char* a = ok ? st + (dh + 1) * C::RB + sx[i][dw + 1] : zero + 16 * g;
+            for (int kw = 0; kw < 3; ++kw) {
+                const int dh = FLIP ? 1 - kh : kh - 1, dw = FLIP ? 1 - kw : kw - 1;
 #pragma unroll
-                for (int kb = 0; kb < C::KB; ++kb) {
-                    // logical piece 4 kb + g: ((P / PPB) % PP ^ g) ^ 4 kb  ->  byte offset ^ 64 kb
-                    const char* ak = ok ? (const char*)((uintptr_t)a ^ (uintptr_t)(64 * kb)) : a;
-                    const bf16x8 af = *reinterpret_cast<const bf16x8*>(ak);
+                for (int i = 0; i < C::MTW; ++i) {
+                    const bool ok = (dh < 0 ? prow[i] != 0 : (dh > 0 ? prow[i] != H - 1 : true)) &&
+                                    (dw < 0 ? pcol[i] != 0 : (dw > 0 ? pcol[i] != W - 1 : true));
+                    const char* a = ok ? st + (dh + 1) * C::RB + sx[i][dw + 1] : zero + 16 * g;
 #pragma unroll
-                    for (int j = 0; j < C::NTW; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][tap * C::KB + kb], af, acc[i][j], 0, 0, 0);
+                    for (int kb = 0; kb < C::KB; ++kb) {
+                        // logical piece 4 kb + g: ((P / PPB) % PP ^ g) ^ 4 kb  ->  byte offset ^ 64 kb
+                        const char* ak = ok ? (const char*)((uintptr_t)a ^ (uintptr_t)(64 * kb)) : a;
+                        af[kw][i][kb] = *reinterpret_cast<const bf16x8*>(ak);
+                    }
                 }
             }
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                for (int i = 0; i < C::MTW; ++i)
+#pragma unroll
+                    for (int kb = 0; kb < C::KB; ++kb)
+#pragma unroll
+                        for (int j = 0; j < C::NTW; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][(kh * 3 + kw) * C::KB + kb],
+                                                                                 af[kw][i][kb], acc[i][j], 0, 0, 0);
         }
 
         // ------------------------------------------------ epilogue
@@ -289,6 +301,7 @@ conv3x3_direct_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, co
                     for (int r = 0; r < 4; ++r) red[wm * NO + (wn * C::NTW + j) * 16 + 4 * g + r] = ts[j][r];
             lds_barrier();
             float* red2 = red + C::WM * NO;
+            const float inv_valid = 1.f / (float)valid;     // exact for full tiles (128 = 2^7)
 #pragma unroll
             for (int j = 0; j < C::NTW; ++j)
 #pragma unroll
@@ -298,7 +311,7 @@ conv3x3_direct_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, co
 #pragma unroll
                     for (int q = 0; q < C::WM; ++q) s += red[q * NO + col];
                     ts[j][r] = s;
-                    const float mean = s / (float)valid;
+                    const float mean = s * inv_valid;
                     float d2 = 0.f;
 #pragma unroll
                     for (int i = 0; i < C::MTW; ++i) {
