@@ -34,40 +34,53 @@ using namespace ocrk;
 namespace {
 
 // acc[mt][j] += rows[16 mt + i][k] . bw[j][k] over this wave's k-range: the
-// group's published rows (row stride ld elements, from rbase) are staged per
-// 16-row M tile (full rows per wave instruction, second tile's loads in
-// flight while the first tile multiplies).
+// group's published rows (row stride ld elements, from rbase) are staged by
+// LDS-DMA straight into the wave's LDS block (rows of KR elements, 16-B
+// pieces XOR-swizzled per row so the 16 rows of an operand read hit distinct
+// bank groups), all 32 rows in flight at once; M tile 0 multiplies as soon as
+// its 16 rows have landed (counted vmcnt: nothing else is issued in between).
+__device__ __forceinline__ int stage_swz(int r, int lpr) { return lpr >= 8 ? (r & 7) : ((r >> 2) & 3); }
+
 template <int KR, int NT>
 __device__ __forceinline__ void stage_mma(__amdgpu_buffer_rsrc_t rs, int64_t rbase, int ld, bool local,
-                                          unsigned short* sa, const bf16x8 (&bw)[NT][KR / 32],
+                                          unsigned short* sA, int wstride, const bf16x8 (&bw)[NT][KR / 32],
                                           floatx4 (&acc)[2][NT]) {
-    constexpr int LDA = KR + 8, LPR = KR / 8, RPI = 64 / LPR, NI = 16 / RPI;
-    static_assert(LPR <= 64 && 16 % RPI == 0, "row staging");
+    constexpr int LPR = KR / 8, RPI = 64 / LPR, NI = PBR / RPI;     // NI 1-KB DMA instructions per wave
+    static_assert(LPR >= 4 && 64 % LPR == 0 && NI % 2 == 0 && NI / 2 < 16, "row staging");
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const int lrow = lane / LPR, lcol = 8 * (lane % LPR);
-    u32x4 v0[NI], v1[NI];
+    const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned short* sa = sA + wu * wstride;                          // wave-uniform LDS base (M0)
+    const int lr = lane / LPR, slot = lane % LPR;
+    if (local) {
 #pragma unroll
-    for (int q = 0; q < NI; ++q)
-        v0[q] = get16(rs, (int)((rbase + (int64_t)(q * RPI + lrow) * ld + lcol) * 2), local);
+        for (int q = 0; q < NI; ++q) {
+            const int r = q * RPI + lr;
+            const unsigned off = (unsigned)((rbase + (int64_t)r * ld + 8 * (slot ^ stage_swz(r, LPR))) * 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(sa + q * 512), 16,
+                                                     off, 0, 0, 2);           // nt
+        }
+    } else {
 #pragma unroll
-    for (int q = 0; q < NI; ++q)
-        v1[q] = get16(rs, (int)((rbase + (int64_t)(16 + q * RPI + lrow) * ld + lcol) * 2), local);
+        for (int q = 0; q < NI; ++q) {
+            const int r = q * RPI + lr;
+            const unsigned off = (unsigned)((rbase + (int64_t)r * ld + 8 * (slot ^ stage_swz(r, LPR))) * 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(sa + q * 512), 16,
+                                                     off, 0, 0, 16);          // sc1
+        }
+    }
     auto mma_tile = [&](int mt) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        const int R = 16 * mt + c;
 #pragma unroll
         for (int kk = 0; kk < KR / 32; ++kk) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(&sa[(16 * mt + c) * LDA + kk * 32 + 8 * g]);
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(&sa[R * KR + 8 * ((4 * kk + g) ^ stage_swz(R, LPR))]);
 #pragma unroll
             for (int j = 0; j < NT; ++j)
                 acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kk], acc[mt][j], 0, 0, 0);
         }
     };
-#pragma unroll
-    for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(&sa[(q * RPI + lrow) * LDA + lcol]) = v0[q];
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI / 2) : "memory");
     mma_tile(0);
-#pragma unroll
-    for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(&sa[(16 + q * RPI + lrow) * LDA + lcol]) = v1[q];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mma_tile(1);
 }
 
@@ -154,7 +167,6 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
     const int xbytes = 2 * 2 * B * H * 2;
     const auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, xbytes, 0x00020000);
     const auto rhx_rsrc = __builtin_amdgcn_make_buffer_rsrc(rhx, 0, xbytes, 0x00020000);
-    unsigned short* sa = sA + w * PBR * LDA;
 
     for (int s = 0; s < T; ++s) {
         const bool valid = s < elen;
@@ -177,7 +189,8 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KR, 4>(hx_rsrc, ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sa, bg, acc);
+            stage_mma<KR, 4>(hx_rsrc, ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sA, PBR * LDA,
+                             bg, acc);
             spill_partial<4>(acc, sPg, LDG);
             __syncthreads();
             sum_partials(sPg, LDG, er, eu, zr);
@@ -200,7 +213,8 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KR, 2>(rhx_rsrc, ((int64_t)((s & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sa, bc, acc);
+            stage_mma<KR, 2>(rhx_rsrc, ((int64_t)((s & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sA, PBR * LDA,
+                             bc, acc);
             spill_partial<2>(acc, sPc, LDC);
             __syncthreads();
             sum_partials(sPc, LDC, er, eu, zc);
@@ -289,7 +303,6 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
     float dh[4] = {0.f, 0.f, 0.f, 0.f};
     const auto zxc_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxc, 0, 2 * 2 * B * H * 2, 0x00020000);
     const auto zxg_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxg, 0, 2 * 2 * B * 2 * H * 2, 0x00020000);
-    unsigned short* sa = sA + w * PBR * LDA;
 
     for (int i = 0; i < T; ++i) {
         const int s = T - 1 - i;
@@ -323,7 +336,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KRC, 2>(zxc_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * H + w * KRC, H, local, sa, bc, acc);
+            stage_mma<KRC, 2>(zxc_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * H + w * KRC, H, local, sA, PBR * LDA, bc,
+                              acc);
             spill_partial<2>(acc, sP1, LDP);
             __syncthreads();
             sum_partials(sP1, LDP, er, eu, drh);
@@ -347,8 +361,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KRG, 2>(zxg_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * 2 * H + w * KRG, 2 * H, local, sa, bg,
-                              acc);
+            stage_mma<KRG, 2>(zxg_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * 2 * H + w * KRG, 2 * H, local, sA,
+                              PBR * LDA, bg, acc);
             spill_partial<2>(acc, sP2, LDP);
             __syncthreads();
             float rec[4];
