@@ -17,160 +17,201 @@
 #include "reduce.h"
 
 // ----------------------------------------------------------------- conv1 fwd
-// G = COUT/8 lanes per output pixel, 8 channels each: a wave's 16-B stores
-// cover 64/G consecutive pixels' whole channel rows (contiguous NHWC bytes)
-// instead of one 16-B piece of 64 different pixels; the G lanes of a pixel
-// read the same 9 input bytes (one cache line). Same fma order per channel.
+// A workgroup owns one output strip: (image b, C1_WR rows, C1_PX consecutive
+// output columns). The C1_WR + 2 input rows it needs (C1_PX + 2 values each)
+// are preprocessed once into LDS; a thread keeps the 72 weights + 8 biases of its
+// channel group (c0 = 8 (tid % G)) in registers and produces G (pixel, group)
+// items, item = tid + 256 j -> pixel item / G: a wave's 16-B stores cover
+// 64/G consecutive pixels' whole channel rows (1 KB contiguous). No per-pixel
+// 64-bit index arithmetic, one byte load per input value per workgroup.
+// Same fma order per channel as the oracle's sum (bias, then taps row-major).
+constexpr int C1_PX = 256;   // output columns per strip
+constexpr int C1_WR = 6;     // output rows per strip
+
+template <typename TIn>
+__device__ __forceinline__ float conv1_in(TIn v) {
+    if constexpr (sizeof(TIn) == 1) {
+#pragma clang fp contract(off)
+        return (float)v * (1.0f / 255.0f) - 0.5f;                        // validate.py:61-62
+    } else {
+        return to_f32(v);
+    }
+}
+
+// the ROWS input rows of a strip into LDS (preprocessed): every load of the
+// workgroup's share is issued before the first is used (fixed trip count)
+template <typename TIn, int ROWS>
+__device__ __forceinline__ void conv1_stage(const TIn* __restrict__ x, int H, int W, int b, int h0, int wo0,
+                                            float (*sx)[C1_PX + 2]) {
+    constexpr int N = ROWS * (C1_PX + 2), IT = (N + 255) / 256;
+    TIn v[IT];
+    bool ok[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int i = threadIdx.x + 256 * q;
+        const int r = i / (C1_PX + 2), col = i - r * (C1_PX + 2);
+        const int xc = wo0 + col, h = h0 + r;
+        ok[q] = i < N && xc < W && h < H;
+        v[q] = ok[q] ? x[((int64_t)b * H + h) * W + xc] : TIn(0);
+    }
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int i = threadIdx.x + 256 * q;
+        if (i < N) {
+            const int r = i / (C1_PX + 2), col = i - r * (C1_PX + 2);
+            sx[r][col] = ok[q] ? conv1_in(v[q]) : 0.f;
+        }
+    }
+}
+
 template <typename TIn, typename TOut, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __restrict__ w,
                  const float* __restrict__ bias, TOut* __restrict__ y) {
-    constexpr int G = COUT / 8, PPB = 256 / G;
+    constexpr int G = COUT / 8;
     static_assert(COUT % 8 == 0 && 256 % G == 0, "channel groups");
-    __shared__ float sw[9 * COUT];
-    __shared__ float sb[COUT];
-    for (int i = threadIdx.x; i < 9 * COUT; i += 256) sw[i] = w[i];
-    for (int i = threadIdx.x; i < COUT; i += 256) sb[i] = bias[i];
-    __syncthreads();
+    __shared__ float sx[C1_WR + 2][C1_PX + 2];
     const int Ho = H - 2, Wo = W - 2;
-    const int64_t npix = (int64_t)B * Ho * Wo;
+    const int nch = (Wo + C1_PX - 1) / C1_PX, nrg = (Ho + C1_WR - 1) / C1_WR;
+    const int chunk = blockIdx.x % nch;
+    const int t = blockIdx.x / nch;
+    const int rg = t % nrg, b = t / nrg;
+    const int ho0 = rg * C1_WR, wo0 = chunk * C1_PX;
+    const int nrows = min(C1_WR, Ho - ho0);
     const int c0 = 8 * (threadIdx.x % G);
-    for (int64_t pix = (int64_t)blockIdx.x * PPB + threadIdx.x / G; pix < npix; pix += (int64_t)gridDim.x * PPB) {
-        int wo = (int)(pix % Wo);
-        int64_t t = pix / Wo;
-        int ho = (int)(t % Ho);
-        int b = (int)(t / Ho);
-        float px[9];
+    float wr[9][8], br[8];
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+    for (int k = 0; k < 9; ++k)
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                TIn v = x[((int64_t)b * H + ho + kh) * W + wo + kw];
-                if constexpr (sizeof(TIn) == 1) {
-#pragma clang fp contract(off)
-                    px[kh * 3 + kw] = (float)v * (1.0f / 255.0f) - 0.5f;   // validate.py:61-62
-                } else {
-                    px[kh * 3 + kw] = to_f32(v);
-                }
+        for (int c = 0; c < 8; ++c) wr[k][c] = w[k * COUT + c0 + c];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) br[c] = bias[c0 + c];
+    conv1_stage<TIn, C1_WR + 2>(x, H, W, b, ho0, wo0, sx);
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+        TOut* yrow = y + (((int64_t)b * Ho + ho0 + r) * Wo + wo0) * COUT + c0;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int p = (threadIdx.x + 256 * j) / G;
+            if (wo0 + p >= Wo) break;
+            float px[9];
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) px[kh * 3 + kw] = sx[r + kh][p + kw];
+            F8 o;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                float acc = br[c];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc = fmaf(px[k], wr[k][c], acc);
+                o.v[c] = fmaxf(acc, 0.f);
             }
-        F8 o;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            float acc = sb[c0 + c];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) acc = fmaf(px[k], sw[k * COUT + c0 + c], acc);
-            o.v[c] = fmaxf(acc, 0.f);
+            store8(yrow + (int64_t)p * COUT, o);
         }
-        store8(y + pix * COUT + c0, o);
     }
 }
 
 // ------------------------------------------------------- conv1 weight grad
 // dw[k][c] = sum_pix x(pix + tap k) * dz[pix][c]; db[c] = sum_pix dz[pix][c].
-// Each block reduces a pixel range into a [10][COUT] partial (slab); a second
-// kernel sums the slabs in a fixed order (deterministic). A thread (8
-// channels) keeps U pixels' loads in flight per pass; the lanes of a wave
-// that share a channel group are combined with a fixed xor-shuffle tree, so
-// the block needs only a [waves][groups][80] scratch and several blocks fit
-// on a CU (the former [256][81] scratch allowed one: one wave per SIMD,
-// latency-bound).
+// A workgroup owns C1_WR output rows x C1_PX columns of one image: the
+// C1_WR + 2 input rows are preprocessed into LDS once, then per row every
+// thread loads its G items' 16-B dz pieces (all in flight) and accumulates
+// [10][8] partials for its fixed channel group. Lanes of a wave that share a
+// group are combined with a fixed xor-shuffle tree, the 4 waves in a fixed
+// order -> one [10][COUT] slab row per workgroup; slab_sum adds the rows in
+// a fixed order (deterministic).
 template <typename TIn, typename TG, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B, int H, int W,
-                    int64_t pix_per_block, float* __restrict__ slab) {
+                    float* __restrict__ slab) {
     constexpr int G = COUT / 8;              // channel groups of 8
-    constexpr int P = 256 / G;               // pixels processed in parallel
-    constexpr int U = 4;                     // pixels per thread per pass
     static_assert(64 % G == 0, "groups within a wave");
+    __shared__ float sx[C1_WR + 2][C1_PX + 2];
     __shared__ float red[4][G][10 * 8 + 1];
     const int Ho = H - 2, Wo = W - 2;
-    const int64_t npix = (int64_t)B * Ho * Wo;
-    const int cg = threadIdx.x % G, pl = threadIdx.x / G;
+    const int nch = (Wo + C1_PX - 1) / C1_PX, nrg = (Ho + C1_WR - 1) / C1_WR;
+    const int chunk = blockIdx.x % nch;
+    const int t = blockIdx.x / nch;
+    const int rg = t % nrg, b = t / nrg;
+    const int ho0 = rg * C1_WR, wo0 = chunk * C1_PX;
+    const int nrows = min(C1_WR, Ho - ho0);
+    const int cg = threadIdx.x % G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    conv1_stage<TIn, C1_WR + 2>(x, H, W, b, ho0, wo0, sx);
     float acc[10][8];
 #pragma unroll
     for (int k = 0; k < 10; ++k)
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[k][c] = 0.f;
-    const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
-    const int64_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
-    for (int64_t q0 = p0 + pl; q0 < p1; q0 += (int64_t)P * U) {
-        F8 g[U];
-        float xv[U][9];
+    __syncthreads();
+    // the G 16-B dz pieces of row r + 1 are in flight while row r is accumulated
+    auto load_row = [&](F8 (&g)[G], int r) {
+        const TG* drow = dz + (((int64_t)b * Ho + ho0 + r) * Wo + wo0) * COUT + cg * 8;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t pix = q0 + (int64_t)u * P;
-            if (pix < p1) {
-                const int wo = (int)(pix % Wo);
-                const int64_t t = pix / Wo;
-                const int ho = (int)(t % Ho);
-                const int b = (int)(t / Ho);
-                g[u] = load8(dz + pix * COUT + cg * 8);
+        for (int j = 0; j < G; ++j) {
+            const int p = (threadIdx.x + 256 * j) / G;
+            if (r < nrows && wo0 + p < Wo) g[j] = load8(drow + (int64_t)p * COUT);
+            else {
 #pragma unroll
-                for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-                    for (int kw = 0; kw < 3; ++kw) {
-                        const TIn v = x[((int64_t)b * H + ho + kh) * W + wo + kw];
-                        if constexpr (sizeof(TIn) == 1) {
-#pragma clang fp contract(off)
-                            xv[u][kh * 3 + kw] = (float)v * (1.0f / 255.0f) - 0.5f;
-                        } else {
-                            xv[u][kh * 3 + kw] = to_f32(v);
-                        }
-                    }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) g[u].v[c] = 0.f;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) xv[u][k] = 0.f;
+                for (int c = 0; c < 8; ++c) g[j].v[c] = 0.f;
             }
         }
+    };
+    F8 gn[G];
+    load_row(gn, 0);
+    for (int r = 0; r < nrows; ++r) {
+        F8 g[G];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int j = 0; j < G; ++j) g[j] = gn[j];
+        load_row(gn, r + 1);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int p = (threadIdx.x + 256 * j) / G;
+            float px[9];
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) px[kh * 3 + kw] = sx[r + kh][p + kw];
 #pragma unroll
             for (int k = 0; k < 9; ++k)
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[k][c] = fmaf(xv[u][k], g[u].v[c], acc[k][c]);
+                for (int c = 0; c < 8; ++c) acc[k][c] = fmaf(px[k], g[j].v[c], acc[k][c]);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc[9][c] += g[u].v[c];
+            for (int c = 0; c < 8; ++c) acc[9][c] += g[j].v[c];
         }
     }
-    // lanes l, l ^ G, l ^ 2G, ... of a wave hold the same channel group
+    // lanes l, l ^ G, l ^ 2G, ... of a wave hold the same channel group: a
+    // reduce-scatter butterfly over those lanes (each level keeps half of the
+    // values and trades the other half: 40 + 20 + 10 + 5 independent shuffles
+    // instead of 4 x 80 dependent ones); a lane ends with 5 sums, values
+    // base .. base + 4 of its group
+    static_assert(G == 4, "the butterfly below is laid out for 4 groups (COUT = 32)");
+    float a[80];
 #pragma unroll
     for (int k = 0; k < 10; ++k)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            float v = acc[k][c];
+        for (int c = 0; c < 8; ++c) a[k * 8 + c] = acc[k][c];
+    int base = 0;
 #pragma unroll
-            for (int o = G; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-            if (lane < G) red[wave][lane][k * 8 + c] = v;
-        }
+    for (int lvl = 0, half = 40; lvl < 4; ++lvl, half >>= 1) {
+        const int m = G << lvl;
+        const bool hi = lane & m;
+        float t[40];
+#pragma unroll
+        for (int i = 0; i < half; ++i) t[i] = __shfl_xor(hi ? a[i] : a[i + half], m, 64);
+#pragma unroll
+        for (int i = 0; i < half; ++i) a[i] = (hi ? a[i + half] : a[i]) + t[i];
+        base += hi ? half : 0;
+    }
+    // lanes with (lane & (G - 1)) == group hold disjoint 5-value pieces of its 80 sums
+#pragma unroll
+    for (int i = 0; i < 5; ++i) red[wave][lane & (G - 1)][base + i] = a[i];
     __syncthreads();
     for (int o = threadIdx.x; o < 10 * COUT; o += 256) {
         const int k = o / COUT, c = o % COUT, gg = c / 8, ci = c % 8;
         slab[(int64_t)blockIdx.x * 10 * COUT + o] =
             ((red[0][gg][k * 8 + ci] + red[1][gg][k * 8 + ci]) + red[2][gg][k * 8 + ci]) + red[3][gg][k * 8 + ci];
-    }
-}
-
-// out0 <- first n0 columns of sum_i slab[i][:], out1 <- the rest (fixed order)
-__global__ void __launch_bounds__(256)
-sum_slabs_kernel(const float* __restrict__ slab, int nslab, int width, float* __restrict__ out0,
-                 int n0, float* __restrict__ out1, int accumulate) {
-    __shared__ double part[4][64];
-    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int o = blockIdx.x * 64 + cl;
-    double s = 0.0;
-    if (o < width) {
-#pragma unroll 8
-        for (int i = q; i < nslab; i += 4) s += slab[(int64_t)i * width + o];
-    }
-    part[q][cl] = s;
-    __syncthreads();
-    if (q == 0 && o < width) {
-        float t = (float)(part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl]);
-        if (o < n0) out0[o] = accumulate ? out0[o] + t : t;
-        else if (out1) out1[o - n0] = accumulate ? out1[o - n0] + t : t;
     }
 }
 
@@ -180,8 +221,9 @@ extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, c
     OCRK_REQUIRE(B >= 0 && H >= 3 && W >= 3, "ocrk_conv1_fwd: bad shape B=%d H=%d W=%d", B, H, W);
     OCRK_REQUIRE(cout == 32, "ocrk_conv1_fwd: Cout=%d (this build carries the model.py:47 Cout=32)", cout);
     if (B == 0) return OCRK_OK;
-    int64_t npix = (int64_t)B * (H - 2) * (W - 2);
-    dim3 grid((unsigned)std::min<int64_t>(ocrk::cdiv(npix, 256 / (32 / 8)), 65535));   // 64 pixels per block pass
+    const int64_t blocks = (int64_t)B * ocrk::cdiv(H - 2, C1_WR) * ocrk::cdiv(W - 2, C1_PX);
+    OCRK_REQUIRE(blocks < (1ll << 31), "ocrk_conv1_fwd: too many rows");
+    dim3 grid((unsigned)blocks);
     hipStream_t s = ocrk::as_stream(stream);
     if (x_is_u8) {
         if (dtype == OCRK_BF16) conv1_fwd_kernel<uint8_t, bf16, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (bf16*)y);
@@ -193,11 +235,14 @@ extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, c
     return ocrk::launch_status("ocrk_conv1_fwd");
 }
 
-static int64_t conv1_blocks(int64_t npix) { return std::max<int64_t>(1, std::min<int64_t>(1024, ocrk::cdiv(npix, 2048))); }
+static int64_t conv1_blocks(int B, int H, int W) {
+    return std::max<int64_t>(1, (int64_t)B * ocrk::cdiv(H - 2, C1_WR) * ocrk::cdiv(W - 2, C1_PX));
+}
 
 extern "C" size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout) {
-    int64_t npix = (int64_t)B * (H - 2) * (W - 2);
-    return (size_t)conv1_blocks(npix) * 10 * cout * sizeof(float);
+    // slab [blocks][10 cout] f32 | part [SLAB_P][10 cout] double (slab_sum's two-stage form)
+    return ((size_t)conv1_blocks(B, H, W) * 10 * cout * sizeof(float) + 15) / 16 * 16 +
+           (size_t)ocrk::SLAB_P * 10 * cout * sizeof(double);
 }
 
 extern "C" int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W,
@@ -205,22 +250,22 @@ extern "C" int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz,
                                      size_t ws_bytes, int dtype, void* stream) {
     OCRK_REQUIRE(cout == 32, "ocrk_conv1_bwd_weight: Cout=%d unsupported", cout);
     OCRK_REQUIRE(ws_bytes >= ocrk_conv1_wgrad_workspace_size(B, H, W, cout), "ocrk_conv1_bwd_weight: workspace too small");
-    int64_t npix = (int64_t)B * (H - 2) * (W - 2);
-    int64_t nb = conv1_blocks(npix);
-    int64_t per = ocrk::cdiv(npix, nb);
+    OCRK_REQUIRE(B >= 1 && H >= 3 && W >= 3, "ocrk_conv1_bwd_weight: bad shape B=%d H=%d W=%d", B, H, W);
+    const int64_t nb = conv1_blocks(B, H, W);
+    OCRK_REQUIRE(nb < (1ll << 31), "ocrk_conv1_bwd_weight: too many rows");
     hipStream_t s = ocrk::as_stream(stream);
     float* slab = (float*)ws;
     if (x_is_u8) {
-        if (dtype == OCRK_BF16) conv1_wgrad_partial<uint8_t, bf16, 32><<<nb, 256, 0, s>>>((const uint8_t*)x, (const bf16*)dz, B, H, W, per, slab);
-        else conv1_wgrad_partial<uint8_t, float, 32><<<nb, 256, 0, s>>>((const uint8_t*)x, (const float*)dz, B, H, W, per, slab);
+        if (dtype == OCRK_BF16) conv1_wgrad_partial<uint8_t, bf16, 32><<<nb, 256, 0, s>>>((const uint8_t*)x, (const bf16*)dz, B, H, W, slab);
+        else conv1_wgrad_partial<uint8_t, float, 32><<<nb, 256, 0, s>>>((const uint8_t*)x, (const float*)dz, B, H, W, slab);
     } else {
-        if (dtype == OCRK_BF16) conv1_wgrad_partial<bf16, bf16, 32><<<nb, 256, 0, s>>>((const bf16*)x, (const bf16*)dz, B, H, W, per, slab);
-        else conv1_wgrad_partial<float, float, 32><<<nb, 256, 0, s>>>((const float*)x, (const float*)dz, B, H, W, per, slab);
+        if (dtype == OCRK_BF16) conv1_wgrad_partial<bf16, bf16, 32><<<nb, 256, 0, s>>>((const bf16*)x, (const bf16*)dz, B, H, W, slab);
+        else conv1_wgrad_partial<float, float, 32><<<nb, 256, 0, s>>>((const float*)x, (const float*)dz, B, H, W, slab);
     }
     int st = ocrk::launch_status("ocrk_conv1_bwd_weight");
     if (st) return st;
-    sum_slabs_kernel<<<(10 * cout + 63) / 64, 256, 0, s>>>(slab, (int)nb, 10 * cout, dw, 9 * cout, db, accumulate);
-    return ocrk::launch_status("ocrk_conv1_bwd_weight reduce");
+    double* part = (double*)((char*)ws + ((size_t)nb * 10 * cout * sizeof(float) + 15) / 16 * 16);
+    return ocrk::slab_sum(slab, (int)nb, 10 * cout, part, nullptr, dw, db, 9 * cout, accumulate, s);
 }
 
 extern "C" size_t ocrk_conv_stats_tiles(int64_t M) { return (size_t)ocrk::cdiv(M, 128); }

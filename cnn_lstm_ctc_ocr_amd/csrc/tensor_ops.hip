@@ -4,6 +4,7 @@
 // gradients) and the ReLU-mask product of the logits layer backward.
 #include "common.h"
 #include "reduce.h"
+#include "mfma_util.h"
 
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
@@ -29,9 +30,56 @@ namespace ocrk {
 namespace {
 
 // Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
-// accumulation, in two stages so the ~2k slab rows are spread over many
-// workgroups: stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
+// accumulation. One launch: a 256-thread workgroup per 64 columns, 16 column
+// quads x 16 row groups; a thread's rows are loaded 8 at a time (16-B loads,
+// all in flight) and added in row order, then the 16 row groups meet in LDS
+// in a fixed order. The slab tables here are <= ~2k rows x a few hundred
+// columns (a few hundred KB): one launch beats the two-stage form's two on the
+// step's critical path, and a 4-wave workgroup still finds a CU slot beside
+// the other stream's GEMMs (a 16-wave one waited behind them). Rows not a
+// multiple of 4 columns wide (or unaligned) take the two-stage form below.
+__global__ void __launch_bounds__(256)
+slab_sum_fused(const float* __restrict__ slab, int nslab, int NC, int ld, float* __restrict__ res,
+               float* __restrict__ dst_lo, float* __restrict__ dst_hi, int split, int accumulate) {
+    constexpr int RG = 16;
+    __shared__ double red[RG][65];
+    const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int c0 = blockIdx.x * 64 + 4 * cq;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    if (c0 < NC) {
+        const float* col = slab + c0;
+        int i = rg;
+        for (; i + 7 * RG < nslab; i += 8 * RG) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(col + (int64_t)(i + u * RG) * ld);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[e] += v[u][e];
+        }
+        for (; i < nslab; i += RG) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(col + (int64_t)i * ld);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[e] += v[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[rg][4 * cq + e] = s[e];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int c = blockIdx.x * 64 + threadIdx.x;
+        if (c >= NC) return;
+        double t = 0.0;
+        for (int y = 0; y < RG; ++y) t += red[y][threadIdx.x];
+        const float v = (float)t;
+        if (res) res[c] = v;
+        float* d = c < split ? (dst_lo ? dst_lo + c : nullptr) : (dst_hi ? dst_hi + (c - split) : nullptr);
+        if (d) *d = accumulate ? *d + v : v;
+    }
+}
 
+// Two-stage form (any NC / ld): stage 1 -> part [SLAB_P][NC] doubles, stage 2 -> the result.
 __global__ void __launch_bounds__(256)
 slab_sum_stage1(const float* __restrict__ slab, int nslab, int NC, int ld, double* __restrict__ part) {
     __shared__ double red[4][64];
@@ -65,6 +113,11 @@ slab_sum_stage2(const double* __restrict__ part, int NC, float* __restrict__ res
 
 int slab_sum(const float* slab, int nslab, int NC, double* part, float* res, float* dst_lo, float* dst_hi,
              int split, int accumulate, hipStream_t s, int ld) {
+    const int l = ld > 0 ? ld : NC;
+    if (NC % 4 == 0 && l % 4 == 0 && ((uintptr_t)slab & 15) == 0) {
+        slab_sum_fused<<<(NC + 63) / 64, 256, 0, s>>>(slab, nslab, NC, l, res, dst_lo, dst_hi, split, accumulate);
+        return ocrk::launch_status("slab sum");
+    }
     slab_sum_stage1<<<dim3((NC + 63) / 64, SLAB_P), 256, 0, s>>>(slab, nslab, NC, ld > 0 ? ld : NC, part);
     int st = ocrk::launch_status("slab sum 1");
     if (st) return st;

@@ -54,10 +54,13 @@ def test_gemm_accumulate_and_bf16_out(cuda):
 
 
 # --------------------------------------------------------------------- conv
-def test_conv1_fwd_and_wgrad(cuda):
+@pytest.mark.parametrize("H,W", [(32, 40), (32, 259), (10, 600)])
+def test_conv1_fwd_and_wgrad(cuda, H, W):
+    """Row-strip workgroups: one strip, a second strip holding one pixel,
+    three strips and a partial row group (Ho = 8 = 6 + 2)."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     rng = np.random.default_rng(1)
-    img = rng.integers(0, 256, (3, 32, 40)).astype(np.uint8)
+    img = rng.integers(0, 256, (3, H, W)).astype(np.uint8)
     w = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
     b = rng.standard_normal(32).astype(np.float32)
     x = G.preprocess(img)[..., None]
