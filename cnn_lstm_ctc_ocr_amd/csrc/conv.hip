@@ -15,6 +15,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "reduce.h"
+#include "mfma_util.h"
 
 // ----------------------------------------------------------------- conv1 fwd
 // A workgroup owns one output strip: (image b, C1_WR rows, C1_PX consecutive
@@ -114,71 +115,91 @@ conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __
 
 // ------------------------------------------------------- conv1 weight grad
 // dw[k][c] = sum_pix x(pix + tap k) * dz[pix][c]; db[c] = sum_pix dz[pix][c].
-// A workgroup owns C1_WR output rows x C1_PX columns of one image: the
-// C1_WR + 2 input rows are preprocessed into LDS once, then per row every
-// thread loads its G items' 16-B dz pieces (all in flight) and accumulates
-// [10][8] partials for its fixed channel group. Lanes of a wave that share a
-// group are combined with a fixed xor-shuffle tree, the 4 waves in a fixed
-// order -> one [10][COUT] slab row per workgroup; slab_sum adds the rows in
-// a fixed order (deterministic).
+// A workgroup owns C1_GR output rows x C1_PX columns of one image: the
+// C1_GR + 2 input rows are preprocessed into LDS once, then per row every
+// thread accumulates its G items' dz pieces into [10][8] partials for its
+// fixed channel group while the raw pieces of the next two rows are in flight
+// (kept as loaded -- 16 B per item for bf16 -- and widened at use). Lanes of a
+// wave that share a group are combined with a reduce-scatter butterfly, the 4
+// waves in a fixed order -> one [10][COUT] slab row per workgroup; slab_sum
+// adds the rows in a fixed order (deterministic).
+constexpr int C1_GR = 15;    // output rows per weight-gradient strip (2 strips per 32-row crop: one round at 2 per CU)
+
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> {
+    ocrk::u32x4 q;
+    __device__ __forceinline__ void load(const bf16* p) { q = *reinterpret_cast<const ocrk::u32x4*>(p); }
+    __device__ __forceinline__ void zero() { q = ocrk::u32x4{0u, 0u, 0u, 0u}; }
+    __device__ __forceinline__ float at(int i) const { return __uint_as_float((q[i >> 1] >> (16 * (i & 1))) << 16); }
+};
+template <> struct Raw8<float> {
+    F8 f;
+    __device__ __forceinline__ void load(const float* p) { f = load8(p); }
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f.v[i] = 0.f;
+    }
+    __device__ __forceinline__ float at(int i) const { return f.v[i]; }
+};
+
 template <typename TIn, typename TG, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B, int H, int W,
                     float* __restrict__ slab) {
     constexpr int G = COUT / 8;              // channel groups of 8
     static_assert(64 % G == 0, "groups within a wave");
-    __shared__ float sx[C1_WR + 2][C1_PX + 2];
+    __shared__ float sx[C1_GR + 2][C1_PX + 2];
     __shared__ float red[4][G][10 * 8 + 1];
     const int Ho = H - 2, Wo = W - 2;
-    const int nch = (Wo + C1_PX - 1) / C1_PX, nrg = (Ho + C1_WR - 1) / C1_WR;
+    const int nch = (Wo + C1_PX - 1) / C1_PX, nrg = (Ho + C1_GR - 1) / C1_GR;
     const int chunk = blockIdx.x % nch;
     const int t = blockIdx.x / nch;
     const int rg = t % nrg, b = t / nrg;
-    const int ho0 = rg * C1_WR, wo0 = chunk * C1_PX;
-    const int nrows = min(C1_WR, Ho - ho0);
+    const int ho0 = rg * C1_GR, wo0 = chunk * C1_PX;
+    const int nrows = min(C1_GR, Ho - ho0);
     const int cg = threadIdx.x % G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    conv1_stage<TIn, C1_WR + 2>(x, H, W, b, ho0, wo0, sx);
+    auto load_row = [&](Raw8<TG> (&g)[G], int r) {
+        const TG* drow = dz + (((int64_t)b * Ho + ho0 + r) * Wo + wo0) * COUT + cg * 8;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int p = (threadIdx.x + 256 * j) / G;
+            if (r < nrows && wo0 + p < Wo) g[j].load(drow + (int64_t)p * COUT);
+            else g[j].zero();
+        }
+    };
+    // rows 0 and 1 in flight with the input staging
+    Raw8<TG> g0[G], g1[G];
+    load_row(g0, 0);
+    load_row(g1, 1);
+    conv1_stage<TIn, C1_GR + 2>(x, H, W, b, ho0, wo0, sx);
     float acc[10][8];
 #pragma unroll
     for (int k = 0; k < 10; ++k)
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[k][c] = 0.f;
     __syncthreads();
-    // the G 16-B dz pieces of row r + 1 are in flight while row r is accumulated
-    auto load_row = [&](F8 (&g)[G], int r) {
-        const TG* drow = dz + (((int64_t)b * Ho + ho0 + r) * Wo + wo0) * COUT + cg * 8;
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            const int p = (threadIdx.x + 256 * j) / G;
-            if (r < nrows && wo0 + p < Wo) g[j] = load8(drow + (int64_t)p * COUT);
-            else {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) g[j].v[c] = 0.f;
-            }
-        }
-    };
-    F8 gn[G];
-    load_row(gn, 0);
     for (int r = 0; r < nrows; ++r) {
-        F8 g[G];
+        Raw8<TG> g[G];
 #pragma unroll
-        for (int j = 0; j < G; ++j) g[j] = gn[j];
-        load_row(gn, r + 1);
+        for (int j = 0; j < G; ++j) { g[j] = g0[j]; g0[j] = g1[j]; }
+        load_row(g1, r + 2);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const int p = (threadIdx.x + 256 * j) / G;
-            float px[9];
+            float px[9], gv[8];
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw) px[kh * 3 + kw] = sx[r + kh][p + kw];
 #pragma unroll
+            for (int c = 0; c < 8; ++c) gv[c] = g[j].at(c);
+#pragma unroll
             for (int k = 0; k < 9; ++k)
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[k][c] = fmaf(px[k], g[j].v[c], acc[k][c]);
+                for (int c = 0; c < 8; ++c) acc[k][c] = fmaf(px[k], gv[c], acc[k][c]);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc[9][c] += g[j].v[c];
+            for (int c = 0; c < 8; ++c) acc[9][c] += gv[c];
         }
     }
     // lanes l, l ^ G, l ^ 2G, ... of a wave hold the same channel group: a
@@ -236,7 +257,7 @@ extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, c
 }
 
 static int64_t conv1_blocks(int B, int H, int W) {
-    return std::max<int64_t>(1, (int64_t)B * ocrk::cdiv(H - 2, C1_WR) * ocrk::cdiv(W - 2, C1_PX));
+    return std::max<int64_t>(1, (int64_t)B * ocrk::cdiv(H - 2, C1_GR) * ocrk::cdiv(W - 2, C1_PX));
 }
 
 extern "C" size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout) {
