@@ -27,7 +27,7 @@
 // 64-bit index arithmetic, one byte load per input value per workgroup.
 // Same fma order per channel as the oracle's sum (bias, then taps row-major).
 constexpr int C1_PX = 256;   // output columns per strip
-constexpr int C1_WR = 6;     // output rows per strip
+constexpr int C1_WR = 8;     // output rows per strip (4 strips per 32-row crop: one round at 4 per CU)
 
 template <typename TIn>
 __device__ __forceinline__ float conv1_in(TIn v) {
