@@ -11,7 +11,7 @@ LIB   := cnn_lstm_ctc_ocr_amd/libocrk.so
 all: $(LIB)
 
 $(LIB): $(OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 build/%.o: $(CSRC)/%.hip $(HDR)
 	@mkdir -p build

@@ -12,6 +12,8 @@ labels already resident in HBM. Rank 0 prints ONE JSON line.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -309,6 +311,111 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
                        "parallelism": f"replicas x{world} (whole buckets per rank)"}}, elapsed, n_crops
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, timeout=None):
+    """`bench.py --gpus N` (N > 1) started WITHOUT a launcher (no WORLD_SIZE in
+    the environment): start N fresh child processes of this script, one per
+    GPU, BEFORE anything here touches the GPU (this parent never initialises
+    HIP). Each child gets RANK = LOCAL_RANK = r, WORLD_SIZE = N and a
+    127.0.0.1 rendezvous, binds cuda:LOCAL_RANK and joins the process group
+    (RCCL; gloo in --selftest). Rank 0 prints the one aggregated JSON line on
+    the inherited stdout. If a rank fails, the others are terminated (they
+    would block in the next collective) and the parent exits non-zero.
+    SURVEY 8e / DESIGN 7: one process per GPU, no exchange beyond the
+    gradient all-reduce."""
+    import threading
+    port = _free_port()
+    procs, pumps = [], []
+
+    def pump(rank, pipe):
+        # stdout carries exactly one line: rank 0's JSON result; library chatter
+        # (gloo / RCCL banners) and every other rank's output go to stderr
+        for line in iter(pipe.readline, ""):
+            out = sys.stdout if (rank == 0 and line.lstrip().startswith("{")) else sys.stderr
+            out.write(line)
+            out.flush()
+        pipe.close()
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                             stdout=subprocess.PIPE, text=True, bufsize=1)
+        procs.append(p)
+        pumps.append(threading.Thread(target=pump, args=(r, p.stdout), daemon=True))
+        pumps[-1].start()
+    t0 = time.time()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"# bench launcher: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        if timeout is not None and time.time() - t0 > timeout and live:
+            print("# bench launcher: timeout; stopping the ranks", file=sys.stderr, flush=True)
+            for q in live:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=10)
+    return rc
+
+
+def selftest(args, world, rank):
+    """--selftest: the multi-rank launch / barrier / max-over-ranks / one-line
+    protocol of this script on the CPU under gloo, with a stand-in host
+    workload instead of the GPU step (tests/test_bench_launcher.py). It is not
+    a benchmark and its line says so."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.ones(1 << 16)
+    x = torch.randn(128, 128)
+
+    def step():
+        for _ in range(4):
+            torch.mm(x, x)
+        if world > 1:
+            dist.all_reduce(g)
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ranks_seen = world
+    if world > 1:
+        t = torch.tensor([elapsed, 1.0], dtype=torch.float64)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, ranks_seen = float(t[0]), int(t[1])
+    if rank == 0:
+        print(json.dumps({"metric": "launcher self-test (CPU stand-in step, not a benchmark)",
+                          "value": round(world * args.batch * args.steps / elapsed, 2), "unit": "items/sec",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1e3 * elapsed / args.steps, 3), "world_size_seen": ranks_seen,
+                          "backend": "gloo", "config": {"global_batch": args.batch * world,
+                                                        "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -335,11 +442,20 @@ def main():
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
                     help="PMC summary (tools/pmc_traffic.py) for roofline.traffic of the conv roofline kernel")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU/gloo check of the multi-rank launch protocol with a stand-in step (no GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one process per GPU here, before any GPU call
+        if not args.selftest and torch.cuda.device_count() < args.gpus:   # device_count does not initialise HIP
+            sys.exit(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPUs visible")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.selftest:
+        return selftest(args, world, rank)
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
@@ -351,6 +467,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         res["value"] = round(work / elapsed, 2)             # whole job over the slowest rank
+        res["ms_per_step"] = round(1e3 * elapsed / (1 if args.config == "c5" else args.steps), 3)
+        res["world_size_seen"] = dist.get_world_size() if world > 1 else 1
         if rank == 0:
             print(json.dumps(res), flush=True)
         if world > 1:
@@ -480,7 +598,10 @@ def main():
                    "execution": "hipGraph replay of fwd+bwd, eager all-reduce + Adam" if args.mode == "graph"
                    else "eager launches",
                    "global_batch": B * world, "per_gpu_batch": B, "image": f"32x{W}", "seq_len": T,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "collective": "one bucketed SUM all-reduce of the flat fp32 gradient per step "
+                                 "(RCCL over xGMI, backend nccl)" if world > 1 else "none"},
+        "world_size_seen": dist.get_world_size() if world > 1 else 1,
         "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_per_step": len(ms) // max(probed, 1), "avg_launch_ms": round(avg_ms, 4),

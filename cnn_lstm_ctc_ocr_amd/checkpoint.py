@@ -306,9 +306,18 @@ def adam_power(beta, updates):
     return np.array(p, np.float32)
 
 
-def save(store, model_dir, global_step=0, trainer=None, name="model.ckpt"):
+def save(store, model_dir, global_step=None, trainer=None, name="model.ckpt"):
     """Saver.save(sess, model_dir/name, global_step): variables, BN moving
-    statistics, Adam slots when a Trainer is given; updates `checkpoint`."""
+    statistics, Adam slots when a Trainer is given; updates `checkpoint`.
+    With a trainer the step is the trainer's (one source for the global_step
+    tensor, the file name and the beta powers); a different explicit
+    global_step is refused, since restore() would then apply the wrong Adam
+    bias correction."""
+    if trainer is not None:
+        if global_step is not None and int(global_step) != int(trainer.global_step):
+            raise ValueError(f"save: global_step={global_step} but the trainer is at step {trainer.global_step}")
+        global_step = trainer.global_step
+    global_step = 0 if global_step is None else int(global_step)
     os.makedirs(model_dir, exist_ok=True)
     tensors = dict(store.state_dict())
     tensors["global_step"] = np.array(global_step, np.int64)

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstddef>
+#include <mutex>
 #include "ocrk.h"
 
 typedef __bf16 bf16;
@@ -17,6 +18,43 @@ int launch_status(const char* what);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Launch configuration that depends on the device -- kernel attributes set
+// with hipFuncSetAttribute, CU counts, occupancy -- is cached PER DEVICE and
+// set up thread-safely: one process may drive several GPUs, one thread each
+// ("a per-device kernel-module cache (thread-safe)").
+constexpr int kMaxDevices = 64;
+inline int current_device() {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    return d < 0 ? 0 : (d >= kMaxDevices ? kMaxDevices - 1 : d);
+}
+struct DeviceOnce {
+    std::once_flag f[kMaxDevices];
+};
+template <typename Fn>
+inline void once_per_device(DeviceOnce& o, Fn&& fn) {
+    std::call_once(o.f[current_device()], fn);
+}
+// CUs of the current device.
+inline int cu_count() {
+    static DeviceOnce o;
+    static int n[kMaxDevices];
+    const int d = current_device();
+    std::call_once(o.f[d], [d] {
+        int v = 0;
+        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d);
+        n[d] = v > 0 ? v : 256;
+    });
+    return n[d];
+}
+// Raise a kernel's dynamic-LDS limit to `bytes`, once per device (call with a
+// function-local `static DeviceOnce`, one per kernel instantiation).
+inline void set_dyn_lds(DeviceOnce& o, const void* kern, int bytes) {
+    once_per_device(o, [kern, bytes] {
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    });
+}
 
 }  // namespace ocrk
 

@@ -526,16 +526,16 @@ int launch_direct(const bf16* x, const bf16* w, const float* bias, const bf16* m
                   int relu, int B, int H, int W, hipStream_t s) {
     using C = DirectCfg<CI, NO, WN>;
     auto kern = conv3x3_direct_kernel<CI, NO, WN, FLIP, STATS, MASK>;
-    static int per_cu = -1, ncu = 0;
-    if (per_cu < 0) {
+    static DeviceOnce once;
+    static int per_cu_dev[kMaxDevices];
+    once_per_device(once, [&] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   C::LDS);
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, C::LDS) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-    }
+        int pc = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 256, C::LDS) != hipSuccess || pc < 1) pc = 1;
+        per_cu_dev[current_device()] = pc;
+    });
+    const int per_cu = per_cu_dev[current_device()], ncu = cu_count();
     const int M = B * H * W;
     const int nchunks = (int)cdiv(M, CM);
     int grid = ncu * per_cu;
@@ -604,12 +604,12 @@ int conv_direct_wgrad(const void* x, const void* dy, int B, int H, int W, int ci
     const int cpw = (int)cdiv(nchunks, grid);
     grid = (int)cdiv(nchunks, cpw);
     if (cout == 32) {
-        static bool cfg = false;
-        if (!cfg) { (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<32>), hipFuncAttributeMaxDynamicSharedMemorySize, WgCfg<32>::LDS); cfg = true; }
+        static DeviceOnce cfg;
+        set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<32>), WgCfg<32>::LDS);
         conv3x3_wgrad_direct_kernel<32><<<grid, 256, WgCfg<32>::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, M, H, W, nchunks, cpw);
     } else {
-        static bool cfg = false;
-        if (!cfg) { (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<64>), hipFuncAttributeMaxDynamicSharedMemorySize, WgCfg<64>::LDS); cfg = true; }
+        static DeviceOnce cfg;
+        set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_direct_kernel<64>), WgCfg<64>::LDS);
         conv3x3_wgrad_direct_kernel<64><<<grid, 256, WgCfg<64>::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, M, H, W, nchunks, cpw);
     }
     int st = launch_status("conv3x3_wgrad_direct");

@@ -438,12 +438,8 @@ extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* 
 #define CTC_LAUNCH(RR)                                                                                      \
     do {                                                                                                    \
         if (in_lds) {                                                                                       \
-            static bool attr = false;                                                                       \
-            if (!attr) {                                                                                    \
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ctc_loss_kernel<RR, true>),        \
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, CTC_LAT_MAX);         \
-                attr = true;                                                                                \
-            }                                                                                               \
+            static ocrk::DeviceOnce attr;                                                                   \
+            ocrk::set_dyn_lds(attr, reinterpret_cast<const void*>(&ctc_loss_kernel<RR, true>), CTC_LAT_MAX); \
             ctc_loss_kernel<RR, true><<<B, CTC_THREADS, lat, s>>>(CTC_ARGS);                                \
         } else {                                                                                            \
             ctc_loss_kernel<RR, false><<<B, CTC_THREADS, 0, s>>>(CTC_ARGS);                                 \

@@ -87,10 +87,6 @@ int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
 bool gemm_pptn_covers(int amode, int M, int N, int convC);   // shape test of gemm_pptn (wgrad split choice)
 int gemm_pptn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
 
-// Plain A_ROWK x B_NK bf16 GEMMs with a bf16 C and at most a bias epilogue
-// on hipBLASLt (blaslt.hip). Returns -1 when not covered. OCRK_BLASLT=0 disables it.
-int gemm_blaslt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
-
 // The same pipeline for the k-major modes A_COLK / A_IM2COL_T x B_KN (conv
 // weight gradients, recurrent / logits weight gradients), gemm_tn.hip.
 // Returns -1 when not covered. OCRK_GEMM_TN=0 disables it.

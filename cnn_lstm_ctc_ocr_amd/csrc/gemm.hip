@@ -501,8 +501,6 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
     int nt = gemm_pp(p, amode, bmode, dtype, stream);
     if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
-    const int lt = gemm_blaslt(p, amode, bmode, dtype, stream);     // whole K in one library call
-    if (lt >= 0) return lt;
     nt = gemm_nt(p, amode, bmode, dtype, stream);
     if (nt < 0) nt = gemm_pptn(p, amode, bmode, dtype, stream);
     if (nt < 0) nt = gemm_tn(p, amode, bmode, dtype, stream);

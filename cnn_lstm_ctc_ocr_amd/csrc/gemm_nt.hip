@@ -339,12 +339,8 @@ int launch_nt(const GemmParams& p, hipStream_t stream) {
         if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
     }
     constexpr int LDS = S * (BM + BN) * BK * 2;
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-        configured = true;
-    }
+    static DeviceOnce configured;
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW>), LDS);
     dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
     gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");

@@ -486,19 +486,9 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmParams p) {
 template <int AM, int BN, bool STATS, bool MASK>
 int launch_pp_k(const GemmParams& p, hipStream_t stream) {
     constexpr int LDS = 2 * (256 + BN) * 128;
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AM, BN, STATS, MASK>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-        configured = true;
-    }
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (ncu <= 0) ncu = 256;
-    }
+    static DeviceOnce configured;
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_pp_kernel<AM, BN, STATS, MASK>), LDS);
+    const int ncu = cu_count();
     const int64_t items = cdiv(p.M, 256) * cdiv(p.N, BN) * (int64_t)p.batch * p.splits;
     // Short K (a few steps per item): persistent, one workgroup per CU, the
     // next item's first K-tile prefetched under the current one. Long K: one

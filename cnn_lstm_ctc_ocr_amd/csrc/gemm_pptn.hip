@@ -304,11 +304,8 @@ int gemm_pptn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t 
     constexpr int LDS = 2 * 8 * 64 * 128;
     const void* kern = amode == A_COLK ? reinterpret_cast<const void*>(&gemm_pptn_kernel<A_COLK>)
                                        : reinterpret_cast<const void*>(&gemm_pptn_kernel<A_IM2COL_T>);
-    static bool configured[2] = {false, false};
-    if (!configured[amode == A_COLK ? 0 : 1]) {
-        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-        configured[amode == A_COLK ? 0 : 1] = true;
-    }
+    static DeviceOnce configured[2];
+    set_dyn_lds(configured[amode == A_COLK ? 0 : 1], kern, LDS);
     const int64_t items = cdiv(p.M, 256) * cdiv(p.N, 256) * (int64_t)p.batch * p.splits;
     const dim3 grid((unsigned)(cdiv(items, 8) * 8));
     if (amode == A_COLK) gemm_pptn_kernel<A_COLK><<<grid, 512, LDS, stream>>>(p);

@@ -234,12 +234,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_tn_kernel(const GemmParams p) {
 template <int BM, int BN, int BK, int S, int WAVES_M, int AM>
 int launch_tn(const GemmParams& p, hipStream_t stream) {
     constexpr int LDS = S * BK * (BM + BN) * 2;
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, BK, S, WAVES_M, AM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-        configured = true;
-    }
+    static DeviceOnce configured;
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, BK, S, WAVES_M, AM>), LDS);
     dim3 grid((unsigned)cdiv(p.M, BM), (unsigned)cdiv(p.N, BN), (unsigned)(p.batch * p.splits));
     gemm_tn_kernel<BM, BN, BK, S, WAVES_M, AM><<<grid, 256, LDS, stream>>>(p);
     return launch_status("gemm_tn");

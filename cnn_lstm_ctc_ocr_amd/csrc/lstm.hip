@@ -553,35 +553,30 @@ extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return
 // GEMM blocks (2 x 64 rows x 2H bytes) + gx tile (8 KB) + c tile (4 KB)
 static constexpr int lstm_fwd_dma_lds(int H) { return 2 * 64 * 2 * H + 64 * 64 * 2 + 64 * 16 * 4; }
 static bool lstm_dma_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_LSTM_DMA");
-        on = (e && e[0] == '0') ? 0 : 1;
-        if (on) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<512>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, lstm_fwd_dma_lds(512));
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<256>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, lstm_fwd_dma_lds(256));
-        }
+    static const bool on = [] { const char* e = getenv("OCRK_LSTM_DMA"); return !(e && e[0] == '0'); }();
+    if (on) {
+        static DeviceOnce a512, a256;
+        set_dyn_lds(a512, reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<512>), lstm_fwd_dma_lds(512));
+        set_dyn_lds(a256, reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<256>), lstm_fwd_dma_lds(256));
     }
-    return on == 1;
+    return on;
 }
 
-// Backward ring + epilogue operands: 138 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it.
+// Backward ring + epilogue operands: 138 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it
+// (and a device that refuses the LDS limit falls back to the VGPR-staged kernel).
 static bool lstm_bwd_dma_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_LSTM_BWD_DMA");
-        on = (e && e[0] == '0') ? 0 : 1;
-        if (on) {
-            hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<512>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
-            hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<256>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
-            if (e1 != hipSuccess || e2 != hipSuccess) on = 0;
-        }
-    }
-    return on == 1;
+    static const bool on = [] { const char* e = getenv("OCRK_LSTM_BWD_DMA"); return !(e && e[0] == '0'); }();
+    if (!on) return false;
+    static DeviceOnce once;
+    static bool ok[kMaxDevices];
+    once_per_device(once, [] {
+        hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<512>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
+        hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_step_dma_kernel<256>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, LSTM_BWD_DMA_LDS);
+        ok[current_device()] = e1 == hipSuccess && e2 == hipSuccess;
+    });
+    return ok[current_device()];
 }
 
 // Tile shapes: bf16 BR=64 x HU=16 (fwd K-chunk 128, bwd 256); f32 BR=32 x HU=8/16.

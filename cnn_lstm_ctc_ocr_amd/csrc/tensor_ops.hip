@@ -361,3 +361,15 @@ extern "C" int ocrk_seq_len(const int* widths, int n, int* out, void* stream) {
     seq_len_kernel<<<(n + 255) / 256, 256, 0, ocrk::as_stream(stream)>>>(widths, n, out);
     return ocrk::launch_status("ocrk_seq_len");
 }
+
+// ------------------------------------------------------------ status word
+__global__ void status_clear_kernel(unsigned* word, unsigned bits) {
+    if (threadIdx.x == 0) atomicAnd(word, ~bits);
+}
+
+extern "C" int ocrk_status_clear(unsigned* status_word, uint32_t bits, void* stream) {
+    OCRK_REQUIRE(status_word != nullptr, "ocrk_status_clear: null status word");
+    if (!bits) return OCRK_OK;
+    status_clear_kernel<<<1, 64, 0, ocrk::as_stream(stream)>>>(status_word, bits);
+    return ocrk::launch_status("ocrk_status_clear");
+}

@@ -240,12 +240,21 @@ def status_word(device):
 lstm_error_word = status_word          # the persistent kernels' bits live in the same word
 
 
+def clear_status(device, bits):
+    """Clear exactly `bits` of the device status word (stream-ordered atomic
+    AND-NOT, ocrk_status_clear): bits set meanwhile by in-flight launches stay."""
+    w = status_word(device)
+    if bits:
+        call("ocrk_status_clear", ptr(w), int(bits) & 0xFFFFFFFF, _stream(w))
+
+
 def read_status(device, reset=True):
-    """Synchronising read of the device status word (optionally cleared)."""
+    """Synchronising read of the device status word (the bits read are cleared
+    when reset)."""
     w = status_word(device)
     v = int(w.item())
     if v and reset:
-        w.zero_()
+        clear_status(device, v)
     return v
 
 

@@ -95,11 +95,20 @@ def fill_batch(infos, batch, widths, bucket_size):
 class Recognizer:
     """The per-batch model step of LocalServer.run (server.py:80-89, 132-138):
     uint8 [bs, 32, W, 1] + widths -> one string per crop. Holds the variables
-    (a ParamStore) on one GPU."""
+    (a ParamStore) on one GPU.
 
-    def __init__(self, store, decoder="greedy", beam_width=16, merge_repeated=True):
+    Serving precision: the reference serves in float32, and only a float32
+    store gives the reference's strings (greedy and beam decodes are identical
+    to the oracle's on the golden MJSynth batch; bf16 differs, CER 0.034 greedy /
+    0.022 beam-16 there -- bench.py's cer_vs_ref). A bf16 store is refused
+    unless allow_bf16=True states that approximate strings are acceptable."""
+
+    def __init__(self, store, decoder="greedy", beam_width=16, merge_repeated=True, allow_bf16=False):
         if decoder not in ("greedy", "beam"):
             raise ValueError("decoder is 'greedy' or 'beam'")
+        if store.cfg.dtype != torch.float32 and not allow_bf16:
+            raise ValueError(f"Recognizer: a {store.cfg.dtype} store does not reproduce the reference's strings "
+                             "(float32 does); pass allow_bf16=True to serve approximate decodes")
         self.store = store
         self.decoder = decoder
         self.beam_width = beam_width
@@ -232,31 +241,42 @@ class LocalServer:
 # ------------------------------------------------------- multi-GPU replicas
 def _replica_main(rank, device, make_recognizer, inq, outq):
     """Worker process of a ReplicaPool: one recognizer on one device; batches
-    in, (batch id, texts) out, until a None item arrives."""
-    rec = make_recognizer(device)
-    outq.put(("ready", rank))
+    in, ("result", batch id, texts) out, until a None item arrives. The
+    replica's GPU is made the CURRENT device before anything else, so every
+    per-device launch setting of libocrk (kernel LDS limits, CU counts, the
+    persistent kernels' co-residency checks) is taken on that GPU and the
+    process never initialises cuda:0 by accident."""
+    try:
+        if isinstance(device, (str, torch.device)) and str(device).startswith("cuda"):
+            torch.cuda.set_device(torch.device(device))
+        rec = make_recognizer(device)
+    except BaseException as e:                       # reported to the pool, which raises
+        outq.put(("init_error", rank, f"{type(e).__name__}: {e}"))
+        return
+    outq.put(("ready", rank, None))
     while True:
         item = inq.get()
         if item is None:
             break
         bid, batch, widths = item
         try:
-            outq.put((bid, list(rec(batch, widths))))
+            outq.put(("result", bid, list(rec(batch, widths))))
         except Exception as e:                        # reported to the server, which raises
-            outq.put((bid, e))
-    outq.put(("exit", rank))
+            outq.put(("error", bid, f"{type(e).__name__}: {e}"))
+    outq.put(("exit", rank, None))
 
 
-def gpu_recognizer(cfg=None, checkpoint=None, seed=0, decoder="greedy", beam_width=16):
+def gpu_recognizer(cfg=None, checkpoint=None, seed=0, decoder="greedy", beam_width=16, allow_bf16=False):
     """A make_recognizer for ReplicaPool: a Recognizer whose ParamStore is
     built on the replica's device (restored from a TF1 checkpoint, or the
     reference initialisers with `seed`). Picklable (spawn)."""
-    return _GpuRecognizerFactory(cfg, checkpoint, seed, decoder, beam_width)
+    return _GpuRecognizerFactory(cfg, checkpoint, seed, decoder, beam_width, allow_bf16)
 
 
 class _GpuRecognizerFactory:
-    def __init__(self, cfg, checkpoint, seed, decoder, beam_width):
+    def __init__(self, cfg, checkpoint, seed, decoder, beam_width, allow_bf16=False):
         self.cfg, self.checkpoint, self.seed, self.decoder, self.beam_width = cfg, checkpoint, seed, decoder, beam_width
+        self.allow_bf16 = allow_bf16
 
     def __call__(self, device):
         from .config import ModelConfig
@@ -265,7 +285,11 @@ class _GpuRecognizerFactory:
         if self.checkpoint:
             from . import checkpoint as ckpt
             ckpt.restore(store, self.checkpoint)
-        return Recognizer(store, decoder=self.decoder, beam_width=self.beam_width)
+        return Recognizer(store, decoder=self.decoder, beam_width=self.beam_width, allow_bf16=self.allow_bf16)
+
+
+class ReplicaError(RuntimeError):
+    """A ReplicaPool worker failed to start, died, or raised on a batch."""
 
 
 class ReplicaPool:
@@ -276,7 +300,13 @@ class ReplicaPool:
     sent whole to replica (bucket index mod replicas), so a width bucket -- one
     input shape -- always lands on the same GPU. submit / poll make the
     LocalServer asynchronous: batches of different buckets run on their GPUs
-    concurrently. `devices`: e.g. ["cuda:0", ..., "cuda:7"]."""
+    concurrently. `devices`: e.g. ["cuda:0", ..., "cuda:7"].
+
+    Failures surface as ReplicaError naming the replica: a recognizer that
+    cannot be built (reported by the worker), a worker process that dies
+    (checked while waiting: its exit code), a batch that raised. The reference
+    server instead logs and leaves its loop (server.py:144-145) and relies on
+    the app's heartbeat watchdog to restart it (ocr-app.py:219-249)."""
 
     def __init__(self, devices, make_recognizer, start_method="spawn", timeout=600.0):
         import multiprocessing as mp
@@ -286,41 +316,102 @@ class ReplicaPool:
         self.inqs = [ctx.Queue() for _ in self.devices]
         self.procs = [ctx.Process(target=_replica_main, args=(r, d, make_recognizer, self.inqs[r], self.outq),
                                   daemon=True) for r, d in enumerate(self.devices)]
+        self.assigned = {}                                   # batch id -> replica (in flight)
+        self._pending = []                                   # results read while waiting for control messages
+        self._closed = False
         for pr in self.procs:
             pr.start()
-        ready = 0
-        while ready < len(self.procs):
-            tag, _ = self.outq.get(timeout=timeout)
+        ready = set()
+        deadline = time.time() + timeout
+        while len(ready) < len(self.procs):
+            msg = self._get(deadline)
+            if msg is None:
+                self._abort()
+                raise ReplicaError(f"replicas {sorted(set(range(len(self.procs))) - ready)} not ready "
+                                   f"after {timeout:.0f} s")
+            tag, who, info = msg
             if tag == "ready":
-                ready += 1
-        self.assigned = {}                                   # batch id -> replica (diagnostics)
+                ready.add(who)
+            elif tag == "init_error":
+                self._abort()
+                raise ReplicaError(f"replica {who} ({self.devices[who]}) failed to start: {info}")
+
+    def _dead(self):
+        """(rank, exit code) of the first worker that exited, if any."""
+        for r, pr in enumerate(self.procs):
+            if not pr.is_alive() and pr.exitcode is not None:
+                return r, pr.exitcode
+        return None
+
+    def _get(self, deadline):
+        """Next message, waiting in short slices while checking that every
+        worker is alive (None at the deadline)."""
+        while True:
+            try:
+                return self.outq.get(timeout=0.2)
+            except queue.Empty:
+                pass
+            dead = self._dead()
+            if dead is not None and not self._closed:
+                try:                                         # a message it sent just before exiting
+                    return self.outq.get_nowait()
+                except queue.Empty:
+                    pass
+                self._abort()
+                raise ReplicaError(f"replica {dead[0]} ({self.devices[dead[0]]}) died with exit code {dead[1]}; "
+                                   f"{len(self.assigned)} batches in flight are lost")
+            if deadline is not None and time.time() > deadline:
+                return None
+
+    def _abort(self):
+        self._closed = True
+        for pr in self.procs:
+            if pr.is_alive():
+                pr.terminate()
 
     def replica_of(self, bucket_index):
         return bucket_index % len(self.procs)
 
     def submit(self, bucket_index, batch_id, batch, widths):
+        dead = self._dead()
+        if dead is not None:
+            self._abort()
+            raise ReplicaError(f"replica {dead[0]} ({self.devices[dead[0]]}) died with exit code {dead[1]}")
         r = self.replica_of(bucket_index)
         self.assigned[batch_id] = r
         self.inqs[r].put((batch_id, np.ascontiguousarray(batch), np.asarray(widths, np.int32)))
 
+    def _take(self, msg, out):
+        tag, bid, payload = msg
+        if tag == "result":
+            self.assigned.pop(bid, None)
+            out.append((bid, payload))
+        elif tag == "error":
+            r = self.assigned.pop(bid, None)
+            raise ReplicaError(f"replica {r} failed on batch {bid}: {payload}")
+        # control messages ("ready", "exit") carry no batch
+
     def poll(self, block=False, timeout=600.0):
-        """Finished (batch id, texts) pairs (waits for one when block)."""
+        """Finished (batch id, texts) pairs (block: wait for at least one)."""
         out = []
-        try:
-            item = self.outq.get(timeout=timeout) if block else self.outq.get_nowait()
-        except queue.Empty:
-            return out
+        if self._pending:
+            for m in self._pending:
+                self._take(m, out)
+            self._pending = []
         while True:
-            bid, texts = item
-            if isinstance(texts, Exception):
-                raise RuntimeError(f"replica {self.assigned.get(bid)} failed on batch {bid}") from texts
-            out.append((bid, texts))
             try:
-                item = self.outq.get_nowait()
+                msg = self.outq.get_nowait()
             except queue.Empty:
-                return out
+                if out or not block or not self.assigned:
+                    return out
+                msg = self._get(time.time() + timeout)
+                if msg is None:
+                    raise ReplicaError(f"no result from the replicas within {timeout:.0f} s "
+                                       f"({len(self.assigned)} batches in flight)")
+            self._take(msg, out)
 
     def close(self):
+        self._closed = True
         for q in self.inqs:
             q.put(None)
         for pr in self.procs:

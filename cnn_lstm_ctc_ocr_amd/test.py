@@ -15,7 +15,10 @@ from .model import ctc_loss_layer, dense_labels
 BEAM_WIDTH = 128       # test.py:86
 
 
-def _get_testing(rnn_logits, sequence_length, label, label_length=None, beam_width=BEAM_WIDTH):
+def _get_testing(rnn_logits, sequence_length, label, label_length=None, beam_width=BEAM_WIDTH, summary=None,
+                 step=0):
+    """summary: a summary.SummaryWriter that receives loss / label_error /
+    sequence_error at `step` (test.py:100-102's tf.summary.scalar calls)."""
     T, B, _ = rnn_logits.shape
     dev = rnn_logits.device
     lab, ln = dense_labels(label, B, dev)
@@ -29,4 +32,6 @@ def _get_testing(rnn_logits, sequence_length, label, label_length=None, beam_wid
         decode.edit_distance(out[0], out_len[0], lab, ln, totals)                    # test.py:90
     label_error = totals[0].to(torch.float32) / totals[2].to(torch.float32)        # test.py:93-96
     sequence_error = totals[1].to(torch.float32) / B                                 # test.py:97-99
+    if summary is not None:
+        summary.scalars(step, loss=loss, label_error=label_error, sequence_error=sequence_error)
     return loss, label_error, sequence_error

@@ -12,7 +12,9 @@ MI355X, backend "nccl") and the Adam kernel divides by world_size -- the mean
 of per-rank means, which equals the global mean for equal shards because the
 loss is a batch mean (model.py:228). BatchNorm statistics stay per rank.
 """
+import collections
 import math
+import time
 
 import torch
 import torch.distributed as dist
@@ -80,6 +82,12 @@ class GradBuckets:
             dist.all_reduce(g[:self.split], op=dist.ReduceOp.SUM, group=self.group)
             self.work.wait()
             self.work = None
+        if g.is_cuda:
+            # every rank gets the same device status word (MAX over ranks) for
+            # this step, so a device error raises on all ranks at the same step
+            # (Trainer.poll_status) instead of one rank raising while its peers
+            # block in the next collective
+            dist.all_reduce(K.status_word(g.device), op=dist.ReduceOp.MAX, group=self.group)
         return 1.0 / world
 
 
@@ -101,12 +109,27 @@ class Trainer:
       InvalidArgumentError and nothing is updated, exactly as in TF;
     * otherwise the CTC kernel and the persistent recurrent kernels set bits in
       the device status word; every step queues a non-blocking copy of it and
-      the next step raises if the copy shows a bit (no sync is added), and
-      check_status() synchronises and raises."""
+      a later step raises if the copy shows a bit (no sync is added), and
+      check_status() synchronises and raises. Unlike TF, the deferred error
+      comes AFTER the bad step's update was applied (its infeasible sequences
+      contributed zero gradient and +inf loss). Only the bits read are cleared
+      (atomic AND-NOT), so errors of steps still in flight are not lost.
+    * data parallel (world_size > 1): the word is MAX-all-reduced with the
+      gradients, and every rank reads the copy of the step `status_lag` (2)
+      steps back, waiting for it if needed -- all ranks raise at the same
+      step, none is left blocking in a collective."""
 
     def __init__(self, store, learning_rate=1e-4, momentum=0.9, decay_rate=0.9, decay_steps=2 ** 16,
-                 decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0):
+                 decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0,
+                 summary=None, summary_every=100):
+        """summary: a summary.SummaryWriter; every `summary_every` steps it gets
+        learning_rate (train.py:139's tf.summary.scalar), the step's loss and
+        the global crops/s since the previous record (no sync: device values
+        are copied asynchronously)."""
         self.store = store
+        self.summary = summary
+        self.summary_every = max(1, int(summary_every))
+        self._summary_mark = None
         self.base_lr = learning_rate
         self.beta1 = momentum
         self.beta2 = beta2
@@ -120,6 +143,8 @@ class Trainer:
         self.v = torch.zeros_like(store.flat)
         self._status_host = None
         self._status_ev = None
+        self._status_ring = collections.deque()     # data parallel: (event, pinned copy) per step
+        self.status_lag = 2
         self.buckets = GradBuckets(store, process_group)
         self.overlap_allreduce = True          # start the recurrent bucket mid-backward (GradBuckets)
 
@@ -172,15 +197,41 @@ class Trainer:
     def step(self, image, width, label):
         """One training iteration; returns the (device) mean CTC loss."""
         self.poll_status()
+        lr = self.learning_rate()
         loss = self.loss_and_grads(image, width, label)
         self.apply_gradients()
         self.post_status()
+        self.summarize(loss, lr, int(image.shape[0]))
         return loss
+
+    def summarize(self, loss, lr, batch):
+        """JSONL scalars every `summary_every` steps (train.py:139)."""
+        if self.summary is None:
+            return
+        now = time.perf_counter()
+        if self._summary_mark is None:
+            self._summary_mark = (self.global_step - 1, now)
+        if self.global_step % self.summary_every:
+            return
+        s0, t0 = self._summary_mark
+        crops = (self.global_step - s0) * batch * self.world_size()
+        vals = {"learning_rate": lr, "loss": loss}
+        if now > t0 and self.global_step > s0:
+            vals["crops_per_sec"] = round(crops / (now - t0), 2)
+        self.summary.scalars(self.global_step, **vals)
+        self._summary_mark = (self.global_step, now)
 
     # ---- device status word (include/ocrk.h, ocrk_device_status)
     def post_status(self):
         """Queue a non-blocking copy of the device status word (after the step's work)."""
         dev = self.store.device
+        if dev.type == "cuda" and self.world_size() > 1:
+            buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            buf.copy_(K.status_word(dev), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._status_ring.append((ev, buf))
+            return
         if dev.type != "cuda" or self._status_ev is not None:
             return
         if self._status_host is None:
@@ -191,18 +242,28 @@ class Trainer:
 
     def poll_status(self):
         """Raise if an earlier step's queued status copy has landed and shows a bit
-        (never waits)."""
+        (single process: never waits; data parallel: the copy of the step
+        `status_lag` steps back, the same step on every rank)."""
+        while len(self._status_ring) > self.status_lag:
+            ev, buf = self._status_ring.popleft()
+            ev.synchronize()
+            v = int(buf[0])
+            if v:
+                self._status_ring.clear()
+                K.clear_status(self.store.device, v)
+                _lib.raise_for_status(v)
         if self._status_ev is None or not self._status_ev.query():
             return
         v = int(self._status_host[0])
         self._status_ev = None
         if v:
-            K.status_word(self.store.device).zero_()
+            K.clear_status(self.store.device, v)
             _lib.raise_for_status(v)
 
     def check_status(self):
         """Synchronise and raise if any step so far set a device status bit."""
         self._status_ev = None
+        self._status_ring.clear()
         if self.store.device.type == "cuda":
             K.check_status(self.store.device)
 
@@ -289,8 +350,10 @@ class GraphedStep:
         """One training iteration on the given batch (or the loaded one);
         returns the graph's device loss tensor (overwritten by the next step)."""
         self.trainer.poll_status()
+        lr = self.trainer.learning_rate()
         self.load(image, width, label)
         self.graph.replay()
         self.trainer.apply_gradients()
         self.trainer.post_status()
+        self.trainer.summarize(self.loss, lr, self.B)
         return self.loss

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 3
+#define OCRK_ABI_VERSION 4
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -57,6 +57,12 @@ enum ocrk_device_status {
     OCRK_STATUS_LSTM_BWD_TIMEOUT = 1 << 5, /* persistent BPTT: a hand-off wait gave up */
     OCRK_STATUS_LSTM_CENSUS = 1 << 6       /* persistent launch: a group's placement census gave up */
 };
+
+/* Clear `bits` of the device status word with a device-side atomic AND-NOT,
+ * stream-ordered: only the bits the caller has read are cleared, so a bit that
+ * a later, still in-flight launch sets is kept (a plain memset would erase it).
+ * No reference counterpart (TF raises synchronously at sess.run). */
+int ocrk_status_clear(unsigned* status_word, uint32_t bits, void* stream);
 
 int ocrk_version(void);
 const char* ocrk_last_error(void);

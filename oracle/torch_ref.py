@@ -32,11 +32,28 @@ LAYERS = [("conv1", 1, 32, "valid", False), ("conv2", 32, 32, "same", True), ("c
 POOLS = {"conv2": ((2, 2), (2, 2)), "conv4": ((2, 2), (2, 1)), "conv6": ((2, 2), (2, 1)), "conv8": ((3, 1), (3, 1))}
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Identity whose forward value AND incoming gradient are rounded to bf16:
+    what bf16 STORAGE of an activation and of its gradient alone does to an
+    otherwise exact (float64) computation (tests/test_gpu_bf16.py bounds)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
 class TorchRef:
     """Parameters as torch CPU tensors under the TF variable names (the
-    oracle's init_params / the ParamStore layout: kernels HWIO / [in+H, 4H])."""
+    oracle's init_params / the ParamStore layout: kernels HWIO / [in+H, 4H]).
+    bf16_storage=True rounds every conv-tower op's output and gradient to bf16
+    (conv, BN, ReLU, max-pool), as the product stores them."""
 
-    def __init__(self, params, rnn_sizes=(512, 512), dtype=torch.float32, cell="lstm"):
+    def __init__(self, params, rnn_sizes=(512, 512), dtype=torch.float32, cell="lstm", bf16_storage=False):
+        self.q = _RoundBF16.apply if bf16_storage else (lambda t: t)
         self.rnn_sizes = tuple(rnn_sizes)
         self.cell = cell
         self.dtype = dtype
@@ -53,16 +70,17 @@ class TorchRef:
         p = self.p
         x = img_u8.permute(0, 3, 1, 2).float() * (1.0 / 255.0) - 0.5          # NCHW, float32 as TF
         x = x.to(self.dtype)
+        q = self.q
         for name, cin, cout, pad, bn in LAYERS:
             w = p[f"convnet/{name}/kernel"].permute(3, 2, 0, 1)                   # HWIO -> OIHW
-            x = F.conv2d(x, w, p[f"convnet/{name}/bias"], padding=1 if pad == "same" else 0)
+            x = q(F.conv2d(x, w, p[f"convnet/{name}/bias"], padding=1 if pad == "same" else 0))
             if bn:
                 pre = f"convnet/{name}/batch_norm"
-                x = F.batch_norm(x, p[pre + "/moving_mean"], p[pre + "/moving_variance"], p[pre + "/gamma"],
-                                 p[pre + "/beta"], training=training, momentum=0.01, eps=1e-3)
-                x = F.max_pool2d(F.relu(x), *POOLS[name])
+                x = q(F.batch_norm(x, p[pre + "/moving_mean"], p[pre + "/moving_variance"], p[pre + "/gamma"],
+                                   p[pre + "/beta"], training=training, momentum=0.01, eps=1e-3))
+                x = q(F.max_pool2d(q(F.relu(x)), *POOLS[name]))
             else:
-                x = F.relu(x)
+                x = q(F.relu(x))
         h = x[:, :, 0, :].permute(2, 0, 1)                                        # [T, B, 256]
         for li, H in enumerate(self.rnn_sizes, start=1):
             outs = []
@@ -78,8 +96,9 @@ class TorchRef:
                 hs = h.new_zeros(h.shape[1], H)
                 cs = h.new_zeros(h.shape[1], H)
                 seq = []
+                gxt = gx.unbind(0)                      # one UnbindBackward, not T x SelectBackward zero-fills
                 for t in (range(h.shape[0] - 1, -1, -1) if rev else range(h.shape[0])):
-                    z = gx[t] + hs @ wh
+                    z = gxt[t] + hs @ wh
                     i, j, f, o = z.chunk(4, dim=1)
                     cs = torch.sigmoid(f + 1.0) * cs + torch.sigmoid(i) * torch.tanh(j)
                     hs = torch.sigmoid(o) * torch.tanh(cs)
@@ -100,21 +119,37 @@ class TorchRef:
         cx = h @ ck[:n_in] + cb                                                  # [T, B, H]
         hs = h.new_zeros(h.shape[1], H)
         seq = []
+        gxt, cxt = gx.unbind(0), cx.unbind(0)
         for t in (range(h.shape[0] - 1, -1, -1) if rev else range(h.shape[0])):
-            r, u = torch.sigmoid(gx[t] + hs @ gk[n_in:]).chunk(2, dim=1)
-            c = torch.tanh(cx[t] + (r * hs) @ ck[n_in:])
+            r, u = torch.sigmoid(gxt[t] + hs @ gk[n_in:]).chunk(2, dim=1)
+            c = torch.tanh(cxt[t] + (r * hs) @ ck[n_in:])
             hs = u * hs + (1 - u) * c
             seq.append(hs)
         if rev:
             seq.reverse()
         return torch.stack(seq)
 
-    def loss(self, logits, labels, label_len):
-        """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised)."""
+    def loss(self, logits, labels, label_len, per_sequence=False):
+        """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised);
+        per_sequence=True: the [B] losses."""
         T, B, _ = logits.shape
         lp = F.log_softmax(logits, dim=2)
         seq = torch.full((B,), T, dtype=torch.long)
+        if per_sequence:
+            return F.ctc_loss(lp, labels, seq, label_len, blank=logits.shape[2] - 1, reduction="none")
         return F.ctc_loss(lp, labels, seq, label_len, blank=logits.shape[2] - 1, reduction="sum") / B
+
+    def loss_and_grads(self, img_u8, labels, label_len):
+        """TRAIN-mode forward + backward without an update: (mean loss, {name: grad},
+        per-sequence losses [B], logits [T, B, C]) as numpy float64 / self.dtype."""
+        for k in self.train_names:
+            self.p[k].grad = None
+        logits = self.forward(img_u8, True)
+        losses = self.loss(logits, labels, label_len, per_sequence=True)
+        loss = losses.sum() / logits.shape[1]
+        loss.backward()
+        grads = {k: self.p[k].grad.detach().numpy() for k in self.train_names}
+        return float(loss.detach()), grads, losses.detach().numpy(), logits.detach().numpy()
 
     def train_step(self, img_u8, labels, label_len, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8):
         """Forward, backward and one TF1 Adam update; returns the loss."""

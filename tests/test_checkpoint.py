@@ -102,10 +102,12 @@ def test_store_save_restore_with_adam_slots(tmp_path, cell, sizes):
     cfg = ModelConfig(cell=cell, rnn_sizes=sizes, dtype=torch.float32)
     a = ParamStore(cfg, device="cpu", seed=1)
     a.stats["convnet/conv2/batch_norm/moving_mean"].fill_(0.25)
-    ta = Trainer(a)
+    ta = Trainer(a, global_step=42)
     ta.m.uniform_()
     ta.v.uniform_()
-    prefix = C.save(a, str(tmp_path), global_step=42, trainer=ta)
+    with pytest.raises(ValueError, match="trainer is at step 42"):
+        C.save(a, str(tmp_path), global_step=41, trainer=ta)      # one source for the step
+    prefix = C.save(a, str(tmp_path), trainer=ta)
     assert os.path.basename(prefix) == "model.ckpt-42"
     b = ParamStore(cfg, device="cpu", seed=2)
     tb = Trainer(b)

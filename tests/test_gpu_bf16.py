@@ -216,3 +216,109 @@ def test_bf16_train_step_bench_routes_vs_float64_oracle(cuda, monkeypatch):
     assert errs["loss_b"] < 1e-2, errs
     bad = {k: (errs[k], bound[k]) for k in bound if errs[k] > bound[k]}
     assert not bad, bad
+
+
+def _bench_batch(B, W, seed):
+    """bench.py's synthetic C3 batch (uint8 crops, labels len U{2..19} fitting T)."""
+    import bench
+    T = (W - 2) // 2 - 2
+    img, _w, (lab, ln) = bench.synthetic_batch(np.random.default_rng(seed), B, W, T, torch.device("cpu"))
+    return img, lab, ln
+
+
+@pytest.mark.parametrize("cell,sizes", [("lstm", (512, 512)), ("gru", (512, 256))])
+def test_bf16_train_step_at_bench_shape_vs_float64(cuda, cell, sizes):
+    """The benched step at the bench's OWN shape: B=256,
+    W=256 (T*B = 32000 rows), the model's recurrent sizes, every default route
+    -- the XCD-grouped persistent role map (B/8 % 16 == 0), the recurrent
+    weight-gradient split-K counts of R = 32000 (model._splits), the batched
+    direction-pair TN launches -- against the reference graph restated in
+    PyTorch float64 on the host (oracle/torch_ref.py, pinned to the NumPy
+    oracle to 1e-9 in tests/test_oracle.py) on the same bf16-rounded weights.
+    cell="gru" is model.py's shipped GRU 512/256 (the bf16 GRU step
+    and its gradients were unpinned).
+    Bounds: mean CTC loss rel < 1e-3 (north_star), per-sequence loss rel < 1e-2,
+    logits rel-L2 < 2e-2, recurrent + logits gradients rel-L2 < 1e-2; each conv
+    variable within 1.5x (+1e-2) of the error that bf16 STORAGE of the conv
+    tower's activations alone causes (the same float64 graph with those
+    outputs and their gradients rounded to bf16)."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, model
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    from oracle.torch_ref import TorchRef
+    B, W = 256, 256
+    vals = M.init_params(seed=11, cell=cell, rnn_sizes=sizes)
+    vals = {k: (_bf(v) if v.ndim >= 1 and "moving" not in k else v) for k, v in vals.items()}
+    img, lab, ln = _bench_batch(B, W, 1234)
+    store = ParamStore(ModelConfig(cell=cell, rnn_sizes=sizes, dtype=torch.bfloat16), device=cuda, values=vals)
+    store.zero_grad()
+    widths = torch.full((B,), W, dtype=torch.int32)
+    feats, seq = model.convnet_layers(img.to(cuda), widths, model.TRAIN, store)
+    logits = model.rnn_layers(feats, seq, 95, store)
+    labd, lnd = lab.to(cuda), ln.to(cuda)
+    loss_b, _, status = Kn.ctc_loss(logits.float().contiguous(), labd, lnd, seq.to(torch.int32), need_grad=False)
+    loss = model.ctc_loss_layer(logits, (labd, lnd), seq)
+    loss.backward()
+    store.join()
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    v64 = {k: v.astype(np.float64) for k, v in vals.items()}
+    lab64, ln64 = lab.long(), ln.long()
+    loss_ref, grads_ref, losses_ref, logits_ref = TorchRef(v64, sizes, torch.float64, cell).loss_and_grads(
+        img, lab64, ln64)
+    _, grads_emu, _, _ = TorchRef(v64, sizes, torch.float64, cell, bf16_storage=True).loss_and_grads(img, lab64, ln64)
+    lg = logits.detach().float().cpu().numpy()
+    errs = {"logits": _rel(lg, logits_ref), "loss": abs(loss.item() - loss_ref) / abs(loss_ref),
+            "loss_b": float(np.max(np.abs(loss_b.cpu().numpy() - losses_ref) / np.abs(losses_ref)))}
+    bound = {}
+    for name, g in grads_ref.items():
+        got = store.grads[name].cpu().numpy()
+        scale = np.linalg.norm(g)
+        if name.endswith("/bias") and name.split("/")[1] in ("conv2", "conv4", "conv6", "conv8"):
+            scale = max(scale, 1e-2 * np.linalg.norm(grads_ref[name.replace("/bias", "/kernel")]))
+        errs[name] = float(np.linalg.norm(got - g) / max(scale, 1e-12))
+        emu = float(np.linalg.norm(grads_emu[name] - g) / max(scale, 1e-12))
+        bound[name] = 1e-2 if name.startswith("rnn/") else 1.5 * emu + 1e-2
+    print(f"{cell} B=256 bf16 errors vs float64:", {k: f"{v:.2e}" for k, v in errs.items()})
+    print("bounds (bf16-storage float64 graph):", {k: f"{v:.2e}" for k, v in bound.items()})
+    assert errs["logits"] < 2e-2, errs
+    assert errs["loss"] < 1e-3, errs
+    assert errs["loss_b"] < 1e-2, errs
+    bad = {k: (errs[k], bound[k]) for k in bound if errs[k] > bound[k]}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("cell,layer", [("lstm", 1), ("lstm", 2), ("gru", 1), ("gru", 2)])
+def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer):
+    """The recurrent weight-gradient launches exactly as model._BiLSTM /
+    _BiGRU.backward issue them at the bench's R = T*B = 32000 rows (batched
+    direction pairs, stride_a / stride_b / stride_c, model._splits' split-K
+    counts), into a non-zero f32 gradient (accumulate) -- against float64."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    from cnn_lstm_ctc_ocr_amd.model import _splits
+    R = 32000
+    H = 512 if (cell == "lstm" or layer == 1) else 256
+    n_in = 256 if layer == 1 else (1024 if cell == "lstm" else 1024)
+    G = 4 * H if cell == "lstm" else 2 * H            # LSTM gates / GRU r|u gates (the candidate block is H)
+    ld = 2 * (4 * H if cell == "lstm" else 3 * H)
+    rng = np.random.default_rng(layer * 10 + len(cell))
+    x = _bf(rng.standard_normal((R, n_in)))
+    hp = _bf(rng.standard_normal((R, 2 * H)))
+    dG = _bf(rng.standard_normal((R, ld)) * 0.1)
+    sk = (n_in + H) * G
+    prev = rng.standard_normal(2 * sk).astype(np.float32)
+    gk = torch.from_numpy(prev).to(cuda)
+    xd, hd, dd = (torch.from_numpy(a).to(cuda).bfloat16() for a in (x, hp, dG))
+    Kn.gemm(xd, dd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G, K=R, lda=n_in, ldb=ld, ldc=G, batch=2,
+            stride_a=0, stride_b=ld // 2, stride_c=sk, splits=_splits(n_in, G, R, batch=2))
+    Kn.gemm(hd, dd, trans_a=True, out=gk[n_in * G:], accumulate=True, M=H, N=G, K=R, lda=2 * H, ldb=ld, ldc=G,
+            batch=2, stride_a=H, stride_b=ld // 2, stride_c=sk, splits=_splits(H, G, R, batch=2))
+    got = gk.cpu().numpy().reshape(2, n_in + H, G)
+    x64, h64, d64 = x.astype(np.float64), hp.astype(np.float64), dG.astype(np.float64)
+    for d in range(2):
+        ref = prev[d * sk:(d + 1) * sk].reshape(n_in + H, G).astype(np.float64)
+        dg = d64[:, d * (ld // 2):d * (ld // 2) + G]
+        ref[:n_in] += x64.T @ dg
+        ref[n_in:] += h64[:, d * H:(d + 1) * H].T @ dg
+        assert _rel(got[d], ref) < 1e-5, (cell, layer, d, _splits(n_in, G, R, batch=2), _splits(H, G, R, batch=2))

@@ -3,7 +3,8 @@ train step: same kernels in the same order, so parameters, BatchNorm moving
 statistics, Adam slots and losses must agree BIT FOR BIT over several steps
 with a different batch loaded into the graph's static buffers each step; and
 the graphed bf16 step at the bench shape (B=256, W=256, LSTM 512/512, the
-hipBLASLt and side-stream paths included) against the eager one."""
+ping-pong GEMM engines, persistent loops and side-stream paths included)
+against the eager one."""
 import numpy as np
 import pytest
 import torch

@@ -236,8 +236,7 @@ def test_adam_matches_oracle(cuda):
 def test_gemm_weight_grad_form_bf16(cuda):
     """dW += x^T . dG as the recurrent backward issues it (bf16 operands, f32
     accumulate into an existing gradient, dG a strided column view, split-K
-    requested): the split-K gemm_tn engine (default) or, with OCRK_BLASLT_TN=1,
-    one hipBLASLt call over all of K must give the float64 product."""
+    requested): the split-K TN engine must give the float64 product."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     rng = np.random.default_rng(5)
     R, n_in, G4 = 1000, 96, 256

@@ -70,12 +70,17 @@ def test_service_end_to_end_on_gpu(cuda):
         assert rec(x, np.array([w], np.int32))[0] == got[i], i
 
 
-def test_replica_pool_on_gpu_matches_single_recognizer(cuda):
-    """Two replica PROCESSES (both on cuda:0 here; one per GPU in production)
-    behind one LocalServer give the single in-process Recognizer's strings."""
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_replica_pool_on_gpu_matches_single_recognizer(cuda, dtype):
+    """Two replica PROCESSES behind one LocalServer give the single in-process
+    Recognizer's strings. One replica per GPU where the box has two (cuda:0,
+    cuda:1: each worker makes its own GPU current before building, ADVICE r2);
+    both on cuda:0 on a one-GPU box. bf16 (allow_bf16) runs the ping-pong GEMM
+    engines, whose LDS limits are set per device."""
     from cnn_lstm_ctc_ocr_amd import ModelConfig
     from cnn_lstm_ctc_ocr_amd.server import LocalServer, Recognizer, ReplicaPool, gpu_recognizer
-    cfg = ModelConfig(rnn_sizes=SIZES, dtype=torch.float32)
+    sizes = SIZES if dtype == torch.float32 else (256, 256)
+    cfg = ModelConfig(rnn_sizes=sizes, dtype=dtype)
     rng = np.random.default_rng(8)
     widths = [int(w) for w in rng.integers(40, 300, 24)]
     crops = [rng.integers(0, 256, (32, w), dtype=np.uint8) for w in widths]
@@ -95,7 +100,18 @@ def test_replica_pool_on_gpu_matches_single_recognizer(cuda):
         return got
 
     from cnn_lstm_ctc_ocr_amd import ParamStore
-    single = serve(Recognizer(ParamStore(cfg, device=cuda, seed=4)))
-    with ReplicaPool(["cuda:0", "cuda:0"], gpu_recognizer(cfg, seed=4)) as pool:
+    bf = dtype == torch.bfloat16
+    single = serve(Recognizer(ParamStore(cfg, device=cuda, seed=4), allow_bf16=bf))
+    devices = ["cuda:0", "cuda:1"] if torch.cuda.device_count() > 1 else ["cuda:0", "cuda:0"]
+    with ReplicaPool(devices, gpu_recognizer(cfg, seed=4, allow_bf16=bf)) as pool:
         multi = serve(pool)
     assert sorted(single) == list(range(len(crops))) and multi == single
+
+
+def test_recognizer_refuses_bf16_store_unless_allowed(cuda):
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.server import Recognizer
+    store = ParamStore(ModelConfig(rnn_sizes=SIZES, dtype=torch.bfloat16), device=cuda, seed=0)
+    with pytest.raises(ValueError, match="allow_bf16"):
+        Recognizer(store)
+    Recognizer(store, allow_bf16=True)

@@ -128,3 +128,55 @@ def test_replica_pool_routes_whole_buckets_and_delivers():
             assert int(tw) == w
             bucket = (w - 1) // 32 - 1                      # buckets (w, w+32] from w = 32
             assert dev == f"dev{pool.replica_of(bucket)}"
+
+
+class _FailingFactory:
+    """make_recognizer that raises on one device (init failure) or returns a
+    recognizer that kills its process / raises on a marked batch."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __call__(self, device):
+        if self.mode == "init" and device == "dev1":
+            raise RuntimeError("no such device")
+
+        def rec(batch, widths):
+            if self.mode == "die":
+                import os
+                os._exit(7)
+            if self.mode == "raise":
+                raise ValueError("bad batch")
+            return [str(int(w)) for w in widths]
+        return rec
+
+
+def test_replica_pool_reports_init_failure_with_rank():
+    import pytest
+
+    from cnn_lstm_ctc_ocr_amd.server import ReplicaError, ReplicaPool
+    with pytest.raises(ReplicaError, match=r"replica 1 \(dev1\) failed to start: RuntimeError: no such device"):
+        ReplicaPool(["dev0", "dev1"], _FailingFactory("init"), timeout=60)
+
+
+def test_replica_pool_notices_a_dead_worker():
+    import numpy as np
+    import pytest
+
+    from cnn_lstm_ctc_ocr_amd.server import ReplicaError, ReplicaPool
+    pool = ReplicaPool(["dev0"], _FailingFactory("die"), timeout=60)
+    pool.submit(0, 0, np.zeros((1, 32, 64, 1), np.uint8), [64])
+    with pytest.raises(ReplicaError, match="replica 0 .* died with exit code 7"):
+        pool.poll(block=True, timeout=60)
+    pool.close()
+
+
+def test_replica_pool_batch_error_names_the_replica():
+    import numpy as np
+    import pytest
+
+    from cnn_lstm_ctc_ocr_amd.server import ReplicaError, ReplicaPool
+    with ReplicaPool(["dev0", "dev1"], _FailingFactory("raise"), timeout=60) as pool:
+        pool.submit(1, 5, np.zeros((1, 32, 64, 1), np.uint8), [64])
+        with pytest.raises(ReplicaError, match="replica 1 failed on batch 5: ValueError: bad batch"):
+            pool.poll(block=True, timeout=60)

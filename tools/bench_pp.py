@@ -77,7 +77,7 @@ def main():
         tot += ms
         print(f"{tag:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s  rel.err {err:.2e}")
     print(f"total {tot:.3f} ms  (OCRK_GEMM_PP={os.environ.get('OCRK_GEMM_PP', '1')}, "
-          f"OCRK_BLASLT={os.environ.get('OCRK_BLASLT', '1')})", flush=True)
+          "no vendor route)", flush=True)
 
 
 if __name__ == "__main__":
