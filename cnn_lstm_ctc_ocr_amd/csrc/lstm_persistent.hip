@@ -49,8 +49,11 @@ extern long long* g_lstm_dbg;
 
 static unsigned lstm_spin_limit() { return recur_spin_limit(); }
 
-// KS = H / 32 k-steps
-template <int KS>
+// KS = H / 32 k-steps. LATE (H = 512): the step's gx loads are issued AFTER the
+// hand-off poll, behind the h_{s-1} LDS-DMA, and written to LDS after the MFMAs:
+// vmcnt is in-order, so gx loads issued before the poll made every poll (and
+// the staging wait) wait for their HBM latency as well.
+template <int KS, bool LATE = false>
 __global__ void __launch_bounds__(256, 1)
 lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
                            const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out,
@@ -90,6 +93,10 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
     }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(bw[j][ks]));   // see the BPTT kernel
 
     // ---- the epilogue item of this thread: row er, units eu..eu+3 (all 4 gates)
     const int er = tid >> 3, eu = 4 * (tid & 7);
@@ -111,18 +118,29 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     // buffer resources for the sc1 hand-off traffic
     const int64_t hx_elems = (int64_t)2 * 2 * B * H;
     auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, (int)(hx_elems * 2), 0x00020000);
+    constexpr bool late = LATE && KS == 16;
+    // gx as one buffer (the late path's loads are single buffer instructions, so the
+    // counted vmcnt wait below can rely on their number)
+    const __amdgpu_buffer_rsrc_t gx_rsrc = uniform_rsrc(gx, (int64_t)T * B * 2 * G4 * 2);
 
     for (int s = 0; s < T; ++s) {
         pstamp(dbg, s, 0);
         // 0. the step's gx tile (independent of h): loads in flight across the wait
+        //    (late: issued behind the staging DMA instead)
         u32x4 gxv[2];
+        auto load_gx = [&]() {
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            const int lr = gx_lr[v];
-            const int t = step_time(dir, s, s_len[lr]);
-            const bf16* gp = gx + (((int64_t)t * B + b0 + lr) * 2 + dir) * G4 + gx_gate[v] * H + u0 + 8 * gx_q[v];
-            gxv[v] = *reinterpret_cast<const u32x4*>(gp);
-        }
+            for (int v = 0; v < 2; ++v) {
+                const int lr = gx_lr[v];
+                const int t = step_time(dir, s, s_len[lr]);
+                const int64_t e = (((int64_t)t * B + b0 + lr) * 2 + dir) * G4 + gx_gate[v] * H + u0 + 8 * gx_q[v];
+                if constexpr (late)
+                    gxv[v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(gx_rsrc, (int)(e * 2), 0, 0));
+                else
+                    gxv[v] = *reinterpret_cast<const u32x4*>(gx + e);
+            }
+        };
+        if constexpr (!late) load_gx();
 
         floatx4 acc[2][2];
 #pragma unroll
@@ -171,7 +189,13 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                             (unsigned)((base + (int64_t)r * H) * 2) + lo, 0, 0, 16);
                     }
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (late) {
+                    asm volatile("" ::: "memory");
+                    load_gx();                                   // 2 loads behind the 8 DMAs
+                    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             } else {
             u32x4 hv[PBR * H / 8 / 256];
 #pragma unroll
@@ -188,10 +212,14 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                 *reinterpret_cast<u32x4*>(&sh[row * LDH + 8 * kq]) = hv[v];
             }
             }
+        } else if constexpr (late) {
+            load_gx();
         }
+        if constexpr (!late) {
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
-            *reinterpret_cast<u32x4*>(&sgx[(gx_lr[v] * 4 + gx_gate[v]) * PHU + 8 * gx_q[v]]) = gxv[v];
+            for (int v = 0; v < 2; ++v)
+                *reinterpret_cast<u32x4*>(&sgx[(gx_lr[v] * 4 + gx_gate[v]) * PHU + 8 * gx_q[v]]) = gxv[v];
+        }
         __syncthreads();
         pstamp(dbg, s, 2);
         if (s > 0) {
@@ -208,6 +236,13 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             }
         }
 
+        if constexpr (late) {
+            // the gx tile, landed during the MFMAs (read after the barrier below; the
+            // previous step's reads of sgx ended before its flag barrier)
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+                *reinterpret_cast<u32x4*>(&sgx[(gx_lr[v] * 4 + gx_gate[v]) * PHU + 8 * gx_q[v]]) = gxv[v];
+        }
         // 4. spill the gate pre-activations: lane (c, g) of wave w holds, for N-tile j,
         //    gate 2j + (c >> 3) of unit 8w + (c & 7), rows 16 mt + 4 g + r
 #pragma unroll
@@ -292,7 +327,10 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
 // in LDS; the cell's gradient (dc kept in registers across steps) gives dz
 // for (row, 4 units, 4 gates) per thread, published (sc1) for step i+1 and
 // stored in time order for the weight-gradient GEMMs.
-template <int KS>
+// LATE (H = 512): the epilogue operands are loaded AFTER the hand-off poll,
+// behind the dz LDS-DMA (single buffer loads; counted vmcnt), so neither the
+// poll nor the staging wait also waits for their HBM latency.
+template <int KS, bool LATE = false>
 __global__ void __launch_bounds__(256, 1)
 lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len,
                            int T, int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
@@ -327,12 +365,24 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
     }
+    // the resident fragments are in before the loop: an empty asm that reads every
+    // fragment makes the waitcnt pass wait for them HERE, after which it knows they
+    // landed -- instead of re-waiting in every step for loads it still counts as
+    // outstanding (which made the tile-0 MFMAs wait for the tile-1 rows' DMA)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(bw[j][ks]));
 
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
     float dcs[4] = {0.f, 0.f, 0.f, 0.f};
     const int64_t zx_elems = (int64_t)2 * 2 * B * G4;
     auto zx_rsrc = __builtin_amdgcn_make_buffer_rsrc(dzx, 0, (int)(zx_elems * 2), 0x00020000);
+    constexpr bool late = LATE && KS == 16;
+    const __amdgpu_buffer_rsrc_t act_rsrc = uniform_rsrc(acts_t, (int64_t)T * B * 2 * G4 * 2);
+    const __amdgpu_buffer_rsrc_t cp_rsrc = uniform_rsrc(cprev_t, (int64_t)T * B * 2 * H * 4);
+    const __amdgpu_buffer_rsrc_t do_rsrc = uniform_rsrc(dout, (int64_t)T * B * 2 * H * 2);
 
     for (int i = 0; i < T; ++i) {
         const int s = T - 1 - i;
@@ -341,11 +391,26 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
         const int t = step_time(dir, s, elen);
         const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
         // 0. epilogue operands (independent of the recurrence) in flight first
+        //    (late: behind the staging DMA, as exactly 6 buffer loads)
         float pa[4][4], pcp[4], pdo[4];
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 la[4], ldo;
+        u32x4 lcp;
+        auto load_late = [&]() {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ld4(pa[k], acts_t + tb * G4 + k * H + u0 + eu);
-        ld4(pcp, cprev_t + tb * H + u0 + eu);
-        ld4(pdo, dout + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu);
+            for (int k = 0; k < 4; ++k)
+                la[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                    act_rsrc, (int)((tb * G4 + k * H + u0 + eu) * 2), 0, 0));
+            lcp = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(cp_rsrc, (int)((tb * H + u0 + eu) * 4), 0, 0));
+            ldo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                do_rsrc, (int)((((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu) * 2), 0, 0));
+        };
+        if constexpr (!late) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ld4(pa[k], acts_t + tb * G4 + k * H + u0 + eu);
+            ld4(pcp, cprev_t + tb * H + u0 + eu);
+            ld4(pdo, dout + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu);
+        }
 
         floatx4 acc[2][2];
 #pragma unroll
@@ -423,10 +488,19 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                             zx_rsrc, (__attribute__((address_space(3))) void*)(sau + r * LDA), 16,
                             (unsigned)((rb + (int64_t)r * G4) * 2) + lo, 0, 0, 16);     // sc1
                 }
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                mma_tile(0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                mma_tile(1);
+                if constexpr (late) {
+                    asm volatile("" ::: "memory");
+                    load_late();                                 // 6 loads behind the 32 DMAs
+                    asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+                    mma_tile(0);
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    mma_tile(1);
+                } else {
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    mma_tile(0);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    mma_tile(1);
+                }
             } else {
                 u32x4 v0[NI], v1[NI];
                 load_rows(v0, 0);
@@ -440,6 +514,19 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                 store_rows(v1, 24);
                 mma_tile(1);
             }
+        } else if constexpr (late) {
+            load_late();
+        }
+        if constexpr (late) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pa[k][0] = __uint_as_float(la[k][0] << 16); pa[k][1] = __uint_as_float(la[k][0] & 0xffff0000u);
+                pa[k][2] = __uint_as_float(la[k][1] << 16); pa[k][3] = __uint_as_float(la[k][1] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pcp[e] = __uint_as_float(lcp[e]);
+            pdo[0] = __uint_as_float(ldo[0] << 16); pdo[1] = __uint_as_float(ldo[0] & 0xffff0000u);
+            pdo[2] = __uint_as_float(ldo[1] << 16); pdo[3] = __uint_as_float(ldo[1] & 0xffff0000u);
         }
         // 3. the four partial products (one per gate's k-range) meet in LDS
 #pragma unroll
@@ -495,6 +582,252 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     }
 }
 
+// ---------------------------------------------------- backward, K-split form
+// The same BPTT with the recurrent product split over the members by K
+// instead of by output unit (default; OCRK_LSTM_BWD_KSPLIT=0 selects the
+// gather form above). Member m computes, from ITS OWN dz (the 4 gates x 32
+// units it just produced, never exchanged), the partial product
+//   P_m[32 rows, H units] = dz_m[32 rows, 128 gate cols] . W_h[H units, own 128 gate cols]^T
+// (K = 128: one 32-deep k-step per gate; wave w: units w H/4 .. +H/4, its W_h
+// slice resident in VGPRs as B fragments), and publishes it as NU f32 blocks
+// of 32 rows x 32 units, block m' for the member that owns those units. A
+// member's dh_rec is then the fixed-order sum of the NU blocks addressed to it
+// (one 16-B load per block per thread, all in flight at once, summed in
+// registers -- deterministic). Per step and member this moves 64 KB in and
+// 64 KB out (f32) instead of gathering every member's dz rows (128 KB bf16 in),
+// keeps no staged rows in LDS (8.5 KB instead of 149 KB), and takes dz out of
+// the exchange, so dh is formed from f32 partial sums of the UNROUNDED-in-
+// exchange products (dz enters the MFMA in bf16 as before).
+// Thread mapping of the cell's gradient = the MFMA output layout: wave w
+// handles M-tile w >> 1 and the 16-unit half w & 1 of the member's units;
+// lane (c, g) holds rows 16 (w >> 1) + 4 g + r (r = 0..3) of unit 16 (w & 1) + c.
+template <int KS, bool PB16>
+__global__ void __launch_bounds__(256, 1)
+lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const int* __restrict__ seq_len, int T,
+                       int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
+                       const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
+                       unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg) {
+    constexpr int H = KS * 32;
+    constexpr int G4 = 4 * H;
+    constexpr int NU = H / PHU;                          // members per group
+    constexpr int NT = H / 64;                           // 16-unit N-tiles per wave (H/4 units)
+    constexpr int LDA = 4 * PHU + 8;                     // padded dz row: 128 gate cols + 8 (bf16)
+    constexpr int BLK = PBR * PHU;                       // elements per (dst, src) block
+    constexpr int EB = PB16 ? 2 : 4;                     // bytes per exchanged element
+    static_assert(NU <= 64 && (H == 256 || H == 512), "one poll lane per member");
+    __shared__ __attribute__((aligned(16))) unsigned short sA[PBR * LDA];
+    // the step's epilogue operands, staged row-wise (vector loads) and read per element
+    __shared__ __attribute__((aligned(16))) unsigned short sAct[PBR * LDA];      // [row][gate][unit] bf16
+    __shared__ __attribute__((aligned(16))) float sCp[PBR * (PHU + 4)];           // [row][unit]
+    __shared__ __attribute__((aligned(16))) float sDo[PBR * (PHU + 4)];
+    __shared__ int s_len[PBR];
+
+    int group, member;
+    const int ngroups = 2 * (B / PBR);
+    persistent_role(ngroups, NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * PHU, b0 = bs * PBR;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    gu32* gflags = (gu32*)(flags) + group * NU;
+    __shared__ int s_local;
+    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;
+
+    // resident B fragments: bw[nt][k] = W_h[unit w H/4 + 16 nt + c][k H + u0 + 8 g .. + 7]
+    bf16x8 bw[NT][4];
+    {
+        const bf16* wdir = wh + (size_t)dir * H * G4;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bw[nt][k] = *reinterpret_cast<const bf16x8*>(
+                    wdir + (size_t)(w * (H / 4) + 16 * nt + c) * G4 + k * H + u0 + 8 * g);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(bw[nt][k]));     // see the gather BPTT
+    }
+    if (tid < PBR) s_len[tid] = seq_len[b0 + tid];
+    __syncthreads();
+
+    const int emt = w >> 1, entl = w & 1;
+    const int ul = 16 * entl + c;                        // the unit (in the slice) of this thread's elements
+    const int rb = 16 * emt + 4 * g;                     // its 4 rows rb .. rb + 3
+    int len[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) len[r] = s_len[rb + r];
+    // row-wise loader item of the epilogue operands: row er, units eu .. eu + 3
+    const int er = tid >> 3, eu = 4 * (tid & 7);
+    const int elen = s_len[er];
+    float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+    // exchange X[parity][group][dst][src][BLK]; a block's element order is the MFMA
+    // output order [mt][n-tile half][lane][r], so producer and consumer lanes move
+    // 4 contiguous elements each
+    const int64_t par_stride = (int64_t)ngroups * NU * NU * BLK;
+    auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc(px, 0, (int)(2 * par_stride * EB), 0x00020000);
+    const int my_off = ((emt * 2 + entl) * 64 + lane) * 4;          // elements, inside a block
+
+    for (int i = 0; i < T; ++i) {
+        const int s = T - 1 - i;
+        pstamp(dbg, i, 0);
+        // 0. epilogue operands (independent of the recurrence): vector loads of row er
+        {
+            const int t = step_time(dir, s, elen);
+            const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 av[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) av[k] = *reinterpret_cast<const u32x2*>(acts_t + tb * G4 + k * H + u0 + eu);
+            const f32x4 cv = *reinterpret_cast<const f32x4*>(cprev_t + tb * H + u0 + eu);
+            const u32x2 dv = *reinterpret_cast<const u32x2*>(dout + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<u32x2*>(&sAct[er * LDA + k * PHU + eu]) = av[k];
+            *reinterpret_cast<f32x4*>(&sCp[er * (PHU + 4) + eu]) = cv;
+            f32x4 dvf;
+            dvf[0] = __uint_as_float(dv[0] << 16); dvf[1] = __uint_as_float(dv[0] & 0xffff0000u);
+            dvf[2] = __uint_as_float(dv[1] << 16); dvf[3] = __uint_as_float(dv[1] & 0xffff0000u);
+            *reinterpret_cast<f32x4*>(&sDo[er * (PHU + 4) + eu]) = dvf;
+        }
+        float dh[4] = {0.f, 0.f, 0.f, 0.f};
+        if (i > 0) {
+            // 1. every member published its partial products of step i-1 (flag >= i)
+            if (w == 0) {
+                unsigned spins = 0;
+                while (true) {
+                    unsigned f = (unsigned)i;
+                    if (lane < NU) f = poll_word(gflags + lane, local);
+                    if (__all(f >= (unsigned)i)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            pstamp(dbg, i, 1);
+            // 2. dh_rec = sum over the NU source members of their block for this member (fixed order)
+            const int64_t boff = ((int64_t)((i - 1) & 1) * par_stride +
+                                  ((int64_t)group * NU + member) * NU * BLK + my_off) * EB;
+            if constexpr (PB16) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                u32x2 pv[NU];
+#pragma unroll
+                for (int src = 0; src < NU; ++src)
+                    pv[src] = local ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(x_rsrc, (int)(boff + (int64_t)src * BLK * EB), 0, 2))
+                                    : __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(x_rsrc, (int)(boff + (int64_t)src * BLK * EB), 0, 16));
+#pragma unroll
+                for (int src = 0; src < NU; ++src) {
+                    dh[0] += __uint_as_float(pv[src][0] << 16); dh[1] += __uint_as_float(pv[src][0] & 0xffff0000u);
+                    dh[2] += __uint_as_float(pv[src][1] << 16); dh[3] += __uint_as_float(pv[src][1] & 0xffff0000u);
+                }
+            } else {
+                u32x4 pv[NU];
+#pragma unroll
+                for (int src = 0; src < NU; ++src) pv[src] = get16(x_rsrc, (int)(boff + (int64_t)src * BLK * EB), local);
+#pragma unroll
+                for (int src = 0; src < NU; ++src)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dh[r] += __uint_as_float(pv[src][r]);
+            }
+        } else {
+            __syncthreads();                                 // the staged epilogue operands
+        }
+        // 3. the cell's gradient for (rows rb..rb+3, unit ul); dz to LDS as the MFMA A operand
+        float dz[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = rb + r;
+            const bool valid = s < len[r];
+            const float dhr = dh[r] + sDo[row * (PHU + 4) + ul];
+            const float ai = bits_f(sAct[row * LDA + 0 * PHU + ul]), aj = bits_f(sAct[row * LDA + 1 * PHU + ul]);
+            const float af = bits_f(sAct[row * LDA + 2 * PHU + ul]), ao = bits_f(sAct[row * LDA + 3 * PHU + ul]);
+            const float cp = sCp[row * (PHU + 4) + ul];
+            const float cc = af * cp + ai * aj;
+            const float tc = tanh_fast(cc);
+            const float dc = dcs[r] + dhr * ao * (1.f - tc * tc);
+            dz[3][r] = valid ? dhr * tc * ao * (1.f - ao) : 0.f;
+            dz[0][r] = valid ? dc * aj * ai * (1.f - ai) : 0.f;
+            dz[1][r] = valid ? dc * ai * (1.f - aj * aj) : 0.f;
+            dz[2][r] = valid ? dc * cp * af * (1.f - af) : 0.f;
+            dcs[r] = valid ? dc * af : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sA[(rb + r) * LDA + k * PHU + ul] = bf16_bits(dz[k][r]);
+        __syncthreads();
+        pstamp(dbg, i, 2);
+        if (i + 1 < T) {
+            // 4. P = dz_own . W_h(own gate cols)^T over this wave's H/4 units
+            floatx4 acc[2][NT];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sA[c * LDA + k * PHU + 8 * g]);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sA[(16 + c) * LDA + k * PHU + 8 * g]);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[nt][k], acc[0][nt], 0, 0, 0);
+                    acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw[nt][k], acc[1][nt], 0, 0, 0);
+                }
+            }
+            // 5. publish the blocks (plain stores stay in the XCD's L2 when the group is
+            //    on one XCD, else write-through), drain, barrier, flag
+            const int64_t pbase = (int64_t)(i & 1) * par_stride + (int64_t)group * NU * NU * BLK;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int dst = (w * (H / 4) + 16 * nt) / PHU;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int64_t off = (pbase + ((int64_t)dst * NU + member) * BLK +
+                                         ((mt * 2 + (nt & 1)) * 64 + lane) * 4) * EB;
+                    if constexpr (PB16) {
+                        const float (&v)[4] = *reinterpret_cast<const float(*)[4]>(&acc[mt][nt]);
+                        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                        const unsigned long long q = pack4(v);
+                        const u32x2 qq = __builtin_bit_cast(u32x2, q);
+                        if (local) __builtin_amdgcn_raw_buffer_store_b64(qq, x_rsrc, (int)off, 0, 0);
+                        else __builtin_amdgcn_raw_buffer_store_b64(qq, x_rsrc, (int)off, 0, 16);
+                    } else {
+                        const u32x4 v = __builtin_bit_cast(u32x4, acc[mt][nt]);
+                        if (local) __builtin_amdgcn_raw_buffer_store_b128(v, x_rsrc, (int)off, 0, 0);
+                        else __builtin_amdgcn_raw_buffer_store_b128(v, x_rsrc, (int)off, 0, 16);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) raise_flag(gflags + member, (unsigned)(i + 1), local);
+        }
+        pstamp(dbg, i, 3);
+        // 6. time-order copy of dz for the weight-gradient GEMMs, 16 B per piece from
+        //    the LDS tile (drains behind the next step; sA is rewritten only after
+        //    the next step's wait barrier)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const int p = tid + 256 * v;
+            const int row = p >> 4, k = (p >> 2) & 3, q = p & 3;
+            const int t = step_time(dir, s, s_len[row]);
+            const u32x4 val = *reinterpret_cast<const u32x4*>(&sA[row * LDA + k * PHU + 8 * q]);
+            *reinterpret_cast<u32x4*>(dG_t + (((int64_t)t * B + b0 + row) * 2 + dir) * G4 + k * H + u0 + 8 * q) = val;
+        }
+        pstamp(dbg, i, 4);
+    }
+}
+
+// The late-load forms (OCRK_PERSIST_LATE=0 disables them, read per launch); their
+// buffer loads address the largest operand (`bytes`) with 32-bit offsets.
+static bool persist_late(int64_t bytes) {
+    const char* e = getenv("OCRK_PERSIST_LATE");
+    return !(e && e[0] == '0') && bytes < 0x7fffffffll;
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H) {
     // flag word + XCC word per workgroup (128-B aligned block), then the h exchange buffer
@@ -527,7 +860,10 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     bf16* hx = (bf16*)((char*)ws + counters);
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
-    if (H == 512)
+    if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
+        lstm_fwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
+                                                                   (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
+    else if (H == 512)
         lstm_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                              (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     else
@@ -537,10 +873,23 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
 }
 
 // ---------------------------------------------------------- backward C ABI
+// OCRK_LSTM_BWD_KSPLIT=1: the K-split form (read per launch). Off by default:
+// measured 5.2 (bf16 partials) / 7.0 (f32) against 4.2 us per step for the
+// gather form at B=256, H=512 -- its exchange buffer (NU x NU blocks per group,
+// 2-4 MB per XCD) does not stay in the XCD's L2 between steps.
+static bool lstm_bwd_ksplit() {
+    const char* e = getenv("OCRK_LSTM_BWD_KSPLIT");
+    return e && e[0] == '1';
+}
+
 extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
-    // flag word + XCC word per workgroup (128-B aligned block), then the dz exchange buffer
+    // flag word + XCC word per workgroup (128-B aligned block), then the exchange buffer:
+    // K-split: [2 parities][groups][NU dst][NU src][32 x 32] f32; gather: [2][2][B][4H] bf16
     size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
-    return counters + (size_t)2 * 2 * B * 4 * H * sizeof(bf16);
+    const size_t nu = (size_t)(H / PHU);
+    const size_t ksplit = (size_t)2 * 2 * (B / PBR) * nu * nu * PBR * PHU * sizeof(float);
+    const size_t gather = (size_t)2 * 2 * B * 4 * H * sizeof(bf16);
+    return counters + (ksplit > gather ? ksplit : gather);
 }
 
 extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
@@ -548,9 +897,11 @@ extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    hipError_t e = H == 512
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<16>, 256, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<8>, 256, 0);
+    hipError_t e = lstm_bwd_ksplit()
+        ? (H == 512 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_ksplit_kernel<16, false>, 256, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_ksplit_kernel<8, false>, 256, 0))
+        : (H == 512 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<16>, 256, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<8>, 256, 0));
     if (e != hipSuccess) return 0;
     const long grid = 2L * (B / PBR) * (H / PHU);
     return grid <= (long)cus * per_cu ? 1 : 0;
@@ -567,7 +918,22 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     bf16* zx = (bf16*)((char*)ws + counters);
     if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
-    if (H == 512)
+    if (lstm_bwd_ksplit()) {
+        const char* pe = getenv("OCRK_LSTM_BWD_PB16");            // partial products exchanged in bf16
+        const bool pb16 = pe && pe[0] == '1';
+#define KSPLIT_LAUNCH(KSV, PB)                                                                                   \
+        lstm_bwd_ksplit_kernel<KSV, PB><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout,  \
+                                                             cprev_t, (const bf16*)acts_t, (bf16*)dG_t, cnt, err,     \
+                                                             lstm_spin_limit(), g_lstm_dbg)
+        if (H == 512) { if (pb16) KSPLIT_LAUNCH(16, true); else KSPLIT_LAUNCH(16, false); }
+        else { if (pb16) KSPLIT_LAUNCH(8, true); else KSPLIT_LAUNCH(8, false); }
+#undef KSPLIT_LAUNCH
+        return ocrk::launch_status("ocrk_lstm_bwd_persistent");
+    }
+    if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
+        lstm_bwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
+                                                                   (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
+    else if (H == 512)
         lstm_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
                                                              (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     else

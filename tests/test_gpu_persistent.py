@@ -82,6 +82,18 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
             dc = np.where(v, dct * sf, dc)
     got = dpers.float().cpu().numpy()
     assert np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
+    # the K-split form of the persistent BPTT (OCRK_LSTM_BWD_KSPLIT=1, opt-in) against
+    # the gather default: same bounds against the oracle and the per-step kernels
+    monkeypatch.setenv("OCRK_LSTM_BWD_KSPLIT", "1")
+    dgat = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("OCRK_LSTM_BWD_KSPLIT")
+    assert K.lstm_error_word(cuda).item() == 0
+    assert (dstep.float() - dgat.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
+    gg = dgat.float().cpu().numpy()
+    assert np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
+    print(f"dz rel err vs oracle: gather {np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref):.3e} "
+          f"K-split {np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref):.3e}")
 
 
 def test_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
