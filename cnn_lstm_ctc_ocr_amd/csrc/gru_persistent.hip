@@ -41,10 +41,17 @@ namespace {
 // its 16 rows have landed (counted vmcnt: nothing else is issued in between).
 __device__ __forceinline__ int stage_swz(int r, int lpr) { return lpr >= 8 ? (r & 7) : ((r >> 2) & 3); }
 
-template <int KR, int NT>
+struct NoExtra {
+    __device__ void operator()() const {}
+};
+
+// `extra` issues exactly NX vector-memory loads BEHIND the DMAs (operands of a
+// later phase): the counted waits below then leave them in flight, so they
+// never delay a hand-off poll or this staging (vmcnt completes in order).
+template <int KR, int NT, int NX = 0, typename F = NoExtra>
 __device__ __forceinline__ void stage_mma(__amdgpu_buffer_rsrc_t rs, int64_t rbase, int ld, bool local,
                                           unsigned short* sA, int wstride, const bf16x8 (&bw)[NT][KR / 32],
-                                          floatx4 (&acc)[2][NT]) {
+                                          floatx4 (&acc)[2][NT], F extra = F()) {
     constexpr int LPR = KR / 8, RPI = 64 / LPR, NI = PBR / RPI;     // NI 1-KB DMA instructions per wave
     static_assert(LPR >= 4 && 64 % LPR == 0 && NI % 2 == 0 && NI / 2 < 16, "row staging");
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -78,10 +85,23 @@ __device__ __forceinline__ void stage_mma(__amdgpu_buffer_rsrc_t rs, int64_t rba
                 acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kk], acc[mt][j], 0, 0, 0);
         }
     };
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI / 2) : "memory");
+    if constexpr (NX > 0) {
+        asm volatile("" ::: "memory");
+        extra();
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI / 2 + NX) : "memory");
     mma_tile(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NX) : "memory");
     mma_tile(1);
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 ld8(__amdgpu_buffer_rsrc_t r, int64_t byte_off) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)byte_off, 0, 0));
+}
+__device__ __forceinline__ void unpack4(u32x2 q, float (&v)[4]) {
+    v[0] = __uint_as_float(q[0] << 16); v[1] = __uint_as_float(q[0] & 0xffff0000u);
+    v[2] = __uint_as_float(q[1] << 16); v[3] = __uint_as_float(q[1] & 0xffff0000u);
 }
 
 // wave w's accumulators -> its partial block sP[w][32 rows][ld]
@@ -168,19 +188,27 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
     const auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, xbytes, 0x00020000);
     const auto rhx_rsrc = __builtin_amdgcn_make_buffer_rsrc(rhx, 0, xbytes, 0x00020000);
 
+    // gx as one buffer: its loads are issued behind the first staging DMA as
+    // exactly 3 buffer instructions (stage_mma's counted waits rely on that)
+    const __amdgpu_buffer_rsrc_t gx_rsrc = uniform_rsrc(gx, (int64_t)T * B * 2 * G3 * 2);
+
     for (int s = 0; s < T; ++s) {
         const bool valid = s < elen;
         const int t = step_time(dir, s, elen);
         const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
-        // 0. this step's input projections (independent of h): in flight across the wait
+        // 0. this step's input projections (independent of h), issued behind the
+        //    h_{s-1} staging DMA so that neither the hand-off poll nor the staging
+        //    waits for their HBM latency (vmcnt completes in order)
         float pr[4], pu[4], pc[4];
-        {
-            const bf16* gp = gx + tb * G3 + u0 + eu;
-            ld4(pr, gp);
-            ld4(pu, gp + H);
-            ld4(pc, gp + 2 * H);
-        }
+        u32x2 gq[3];
+        auto load_gx = [&]() {
+            const int64_t e = (tb * G3 + u0 + eu) * 2;
+            gq[0] = ld8(gx_rsrc, e);
+            gq[1] = ld8(gx_rsrc, e + 2 * H);
+            gq[2] = ld8(gx_rsrc, e + 4 * H);
+        };
         float zr[4] = {0.f, 0.f, 0.f, 0.f}, zu[4] = {0.f, 0.f, 0.f, 0.f}, zc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (s == 0) load_gx();
         if (s > 0) {
             // 1. gates: h_{s-1} . Wg_h over this wave's k-range (h_{-1} = 0: nothing at s = 0)
             group_wait(gflags, NU, 2u * s, local, err, OCRK_STATUS_LSTM_FWD_TIMEOUT, spin_limit, dead);
@@ -189,13 +217,16 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KR, 4>(hx_rsrc, ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sA, PBR * LDA,
-                             bg, acc);
+            stage_mma<KR, 4, 3>(hx_rsrc, ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H + w * KR, H, local, sA,
+                                PBR * LDA, bg, acc, load_gx);
             spill_partial<4>(acc, sPg, LDG);
             __syncthreads();
             sum_partials(sPg, LDG, er, eu, zr);
             sum_partials(sPg, LDG, er, PHU + eu, zu);
         }
+        unpack4(gq[0], pr);
+        unpack4(gq[1], pu);
+        unpack4(gq[2], pc);
         float ar[4], au[4], rh[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -304,20 +335,36 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
     const auto zxc_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxc, 0, 2 * 2 * B * H * 2, 0x00020000);
     const auto zxg_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxg, 0, 2 * 2 * B * 2 * H * 2, 0x00020000);
 
+    // the step's epilogue operands are prefetched one step ahead, issued behind
+    // the previous step's second staging DMA as exactly 5 buffer loads: loaded at
+    // the top of the step they sat in front of its first hand-off drain and poll
+    const __amdgpu_buffer_rsrc_t act_rsrc = uniform_rsrc(acts_t, (int64_t)T * B * 2 * G3 * 2);
+    const __amdgpu_buffer_rsrc_t hp_rsrc = uniform_rsrc(hprev_t, (int64_t)T * B * 2 * H * 2);
+    const __amdgpu_buffer_rsrc_t do_rsrc = uniform_rsrc(dout, (int64_t)T * B * 2 * H * 2);
+    u32x2 pq[5];
+    auto load_step = [&](int ii) {
+        const int ts = step_time(dir, T - 1 - ii, elen);
+        const int64_t tbb = ((int64_t)ts * B + b0 + er) * 2 + dir;
+        const int64_t a = (tbb * G3 + u0 + eu) * 2;
+        pq[0] = ld8(act_rsrc, a);
+        pq[1] = ld8(act_rsrc, a + 2 * H);
+        pq[2] = ld8(act_rsrc, a + 4 * H);
+        pq[3] = ld8(hp_rsrc, (tbb * H + u0 + eu) * 2);
+        pq[4] = ld8(do_rsrc, (((int64_t)ts * B + b0 + er) * 2 * H + dir * H + u0 + eu) * 2);
+    };
+    load_step(0);
+
     for (int i = 0; i < T; ++i) {
         const int s = T - 1 - i;
         const bool valid = s < elen;
         const int t = step_time(dir, s, elen);
         const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
         float ar[4], au[4], ac[4], hp[4], go[4];
-        {
-            const bf16* ap = acts_t + tb * G3 + u0 + eu;
-            ld4(ar, ap);
-            ld4(au, ap + H);
-            ld4(ac, ap + 2 * H);
-            ld4(hp, hprev_t + tb * H + u0 + eu);
-            ld4(go, dout + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu);
-        }
+        unpack4(pq[0], ar);
+        unpack4(pq[1], au);
+        unpack4(pq[2], ac);
+        unpack4(pq[3], hp);
+        unpack4(pq[4], go);
         // 1. dh_tot and dz_c of own units; publish dz_c
         float dt[4], dzc[4];
 #pragma unroll
@@ -361,8 +408,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            stage_mma<KRG, 2>(zxg_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * 2 * H + w * KRG, 2 * H, local, sA,
-                              PBR * LDA, bg, acc);
+            stage_mma<KRG, 2, 5>(zxg_rsrc, ((int64_t)((i & 1) * 2 + dir) * B + b0) * 2 * H + w * KRG, 2 * H, local, sA,
+                                 PBR * LDA, bg, acc, [&]() { load_step(i + 1); });
             spill_partial<2>(acc, sP2, LDP);
             __syncthreads();
             float rec[4];
