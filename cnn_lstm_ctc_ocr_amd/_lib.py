@@ -68,16 +68,17 @@ SIGNATURES = {
     "ocrk_copy_batch": [_p, _i32, _i64, _p],
     "ocrk_gru_fwd_persistent_supported": [_i32, _i32],
     "ocrk_gru_fwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_gru_fwd_persistent": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_gru_fwd_persistent": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_gru_bwd_persistent_supported": [_i32, _i32],
     "ocrk_gru_bwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_gru_bwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_gru_bwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_persistent_flags_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_bwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_bwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_debug_stamps": [_p],
     "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
@@ -102,6 +103,7 @@ SIGNATURES = {
 _RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
 _RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspace_size")})
 _RESTYPE["ocrk_conv_stats_tiles"] = ctypes.c_size_t
+_RESTYPE["ocrk_persistent_flags_size"] = ctypes.c_size_t
 _RESTYPE["ocrk_crc32c"] = ctypes.c_uint32
 
 
@@ -142,6 +144,11 @@ _STATUS_TEXT = {
 }
 
 
+# called before a DeviceError is raised for a recurrent-loop status bit
+# (kernels.reset_persistent_flags re-zeroes the loops' counting hand-off words)
+ON_DEVICE_ERROR = []
+
+
 def raise_for_status(word):
     """Raise the error a non-zero device status word stands for (CTC bits as
     InvalidArgumentError, like tf.nn.ctc_loss; recurrent timeouts as DeviceError)."""
@@ -150,6 +157,8 @@ def raise_for_status(word):
         return
     text = "; ".join(t for b, t in _STATUS_TEXT.items() if word & b)
     if word & STATUS_LSTM:
+        for fn in ON_DEVICE_ERROR:
+            fn()
         raise DeviceError(OCRK_ERR_HIP, f"device status 0x{word:x}: {text}")
     raise InvalidArgumentError(OCRK_ERR_INFEASIBLE, f"device status 0x{word:x}: {text}")
 

@@ -155,8 +155,8 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
-    __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
     bool dead = false;
 
     // resident B fragments, k = w KR + 32 kk + 8 g: gate N-tile j col c is
@@ -211,7 +211,7 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
         if (s == 0) load_gx();
         if (s > 0) {
             // 1. gates: h_{s-1} . Wg_h over this wave's k-range (h_{-1} = 0: nothing at s = 0)
-            group_wait(gflags, NU, 2u * s, local, err, OCRK_STATUS_LSTM_FWD_TIMEOUT, spin_limit, dead);
+            group_wait(gflags, NU, base + 2u * s, local, err, OCRK_STATUS_LSTM_FWD_TIMEOUT, spin_limit, dead);
             floatx4 acc[2][4];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
@@ -237,8 +237,8 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
         if (s > 0) {
             // 2. publish r*h of own units, then the candidate: (r*h) . Wc_h
             put8((gu64*)(rhx + ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu), pack4(rh), local);
-            group_post(gflags + member, 2u * s + 1u, local);
-            group_wait(gflags, NU, 2u * s + 1u, local, err, OCRK_STATUS_LSTM_FWD_TIMEOUT, spin_limit, dead);
+            group_post(gflags + member, base + 2u * s + 1u, local);
+            group_wait(gflags, NU, base + 2u * s + 1u, local, err, OCRK_STATUS_LSTM_FWD_TIMEOUT, spin_limit, dead);
             floatx4 acc[2][2];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
@@ -261,7 +261,7 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
             if (!valid) { ar[e] = 0.f; au[e] = 0.f; ac[e] = 0.f; }
         }
         put8((gu64*)(hx + ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu), pack4(hst), local);
-        group_post(gflags + member, 2u * s + 2u, local);
+        group_post(gflags + member, base + 2u * s + 2u, local);
         // 4. layer output and the tensors saved for the backward pass (drain behind the next step)
         {
             // padded positions (t = s >= len) get this direction's zeros: the caller need not clear out
@@ -309,8 +309,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
-    __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
     bool dead = false;
 
     // resident B fragments: N-tile j col c = unit u0 + 16 j + c; k = w KR + 32 kk + 8 g
@@ -373,8 +373,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
             dzc[e] = bf16r(dt[e] * (1.f - au[e]) * (1.f - ac[e] * ac[e]));
         }
         put8((gu64*)(zxc + ((int64_t)((i & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu), pack4(dzc), local);
-        group_post(gflags + member, 2u * i + 1u, local);
-        group_wait(gflags, NU, 2u * i + 1u, local, err, OCRK_STATUS_LSTM_BWD_TIMEOUT, spin_limit, dead);
+        group_post(gflags + member, base + 2u * i + 1u, local);
+        group_wait(gflags, NU, base + 2u * i + 1u, local, err, OCRK_STATUS_LSTM_BWD_TIMEOUT, spin_limit, dead);
         // 2. d(r*h) of own units = dz_c . Wc_h^T
         float drh[4];
         {
@@ -401,8 +401,8 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
             gu64* zg = (gu64*)(zxg + ((int64_t)((i & 1) * 2 + dir) * B + b0 + er) * 2 * H + u0 + eu);
             put8(zg, pack4(dzr), local);
             put8(zg + H / 4, pack4(dzu), local);
-            group_post(gflags + member, 2u * i + 2u, local);
-            group_wait(gflags, NU, 2u * i + 2u, local, err, OCRK_STATUS_LSTM_BWD_TIMEOUT, spin_limit, dead);
+            group_post(gflags + member, base + 2u * i + 2u, local);
+            group_wait(gflags, NU, base + 2u * i + 2u, local, err, OCRK_STATUS_LSTM_BWD_TIMEOUT, spin_limit, dead);
             floatx4 acc[2][2];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
@@ -447,7 +447,7 @@ extern "C" int ocrk_gru_fwd_persistent_supported(int B, int H) {
 
 extern "C" int ocrk_gru_fwd_persistent(const void* gx, const void* whgT, const void* whcT, const int* seq_len, int T,
                                        int B, int H, void* out, void* hprev_t, void* rh_t, void* acts_t,
-                                       unsigned* err, void* ws, size_t ws_bytes, void* stream) {
+                                       unsigned* err, unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_gru_fwd_persistent_supported(B, H), "ocrk_gru_fwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_gru_fwd_persistent_workspace_size(B, H), "ocrk_gru_fwd_persistent: workspace too small");
     OCRK_REQUIRE(err != nullptr, "ocrk_gru_fwd_persistent: status word required");
@@ -456,16 +456,18 @@ extern "C" int ocrk_gru_fwd_persistent(const void* gx, const void* whgT, const v
     const size_t counters = persistent_counter_bytes(B, H);
     bf16* hx = (bf16*)((char*)ws + counters);
     bf16* rhx = hx + (size_t)2 * 2 * B * H;
-    if (hipMemsetAsync(ws, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_gru_fwd_persistent memset");
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
+    if (!flags && hipMemsetAsync(ws, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_gru_fwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512)
         gru_fwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whgT, (const bf16*)whcT, hx, rhx,
                                                             seq_len, T, B, (bf16*)out, (bf16*)hprev_t, (bf16*)rh_t,
-                                                            (bf16*)acts_t, (unsigned*)ws, err, recur_spin_limit());
+                                                            (bf16*)acts_t, cnt, err, recur_spin_limit());
     else
         gru_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whgT, (const bf16*)whcT, hx, rhx,
                                                            seq_len, T, B, (bf16*)out, (bf16*)hprev_t, (bf16*)rh_t,
-                                                           (bf16*)acts_t, (unsigned*)ws, err, recur_spin_limit());
+                                                           (bf16*)acts_t, cnt, err, recur_spin_limit());
     return ocrk::launch_status("ocrk_gru_fwd_persistent");
 }
 
@@ -480,7 +482,7 @@ extern "C" int ocrk_gru_bwd_persistent_supported(int B, int H) {
 
 extern "C" int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
                                        const void* dout, const void* hprev_t, const void* acts_t, void* dG_t,
-                                       unsigned* err, void* ws, size_t ws_bytes, void* stream) {
+                                       unsigned* err, unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_gru_bwd_persistent_supported(B, H), "ocrk_gru_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_gru_bwd_persistent_workspace_size(B, H), "ocrk_gru_bwd_persistent: workspace too small");
     OCRK_REQUIRE(err != nullptr, "ocrk_gru_bwd_persistent: status word required");
@@ -489,15 +491,17 @@ extern "C" int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const i
     const size_t counters = persistent_counter_bytes(B, H);
     bf16* zxc = (bf16*)((char*)ws + counters);
     bf16* zxg = zxc + (size_t)2 * 2 * B * H;
-    if (hipMemsetAsync(ws, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_gru_bwd_persistent memset");
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
+    if (!flags && hipMemsetAsync(ws, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_gru_bwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512)
         gru_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)whg, (const bf16*)whc, zxc, zxg, seq_len, T, B,
                                                             (const bf16*)dout, (const bf16*)hprev_t, (const bf16*)acts_t,
-                                                            (bf16*)dG_t, (unsigned*)ws, err, recur_spin_limit());
+                                                            (bf16*)dG_t, cnt, err, recur_spin_limit());
     else
         gru_bwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)whg, (const bf16*)whc, zxc, zxg, seq_len, T, B,
                                                            (const bf16*)dout, (const bf16*)hprev_t, (const bf16*)acts_t,
-                                                           (bf16*)dG_t, (unsigned*)ws, err, recur_spin_limit());
+                                                           (bf16*)dG_t, cnt, err, recur_spin_limit());
     return ocrk::launch_status("ocrk_gru_bwd_persistent");
 }

@@ -80,8 +80,8 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     const int lu = 8 * w + (c & 7);                     // the unit (within the slice) this lane finishes
     const int my_unit = u0 + lu;
     gu32* gflags = (gu32*)(flags) + group * NU;
-    __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
     if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // ---- resident B fragments: N-tile j holds gates 2j + (c >> 3) of unit my_unit
@@ -153,9 +153,9 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             if (w == 0) {
                 unsigned spins = 0;
                 while (true) {
-                    unsigned f = (unsigned)s;
+                    unsigned f = base + (unsigned)s;
                     if (lane < NU) f = poll_word(gflags + lane, local);
-                    if (__all(f >= (unsigned)s)) break;
+                    if (__all(reached(f, base + (unsigned)s))) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_FWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -294,7 +294,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) raise_flag(gflags + member, (unsigned)(s + 1), local);
+        if (tid == 0) raise_flag(gflags + member, base + (unsigned)(s + 1), local);
         pstamp(dbg, s, 4);
 
         // 7. the layer output and the tensors saved for the backward pass
@@ -352,8 +352,8 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
-    __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
     if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;     // diagnostics: hand-off form
 
     // resident B fragments: N-tile j = units u0 + 16 j + c; k = w H + 32 ks + 8 g
@@ -422,9 +422,9 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
             if (w == 0) {
                 unsigned spins = 0;
                 while (true) {
-                    unsigned f = (unsigned)i;
+                    unsigned f = base + (unsigned)i;
                     if (lane < NU) f = poll_word(gflags + lane, local);
-                    if (__all(f >= (unsigned)i)) break;
+                    if (__all(reached(f, base + (unsigned)i))) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -573,7 +573,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) raise_flag(gflags + member, (unsigned)(i + 1), local);
+        if (tid == 0) raise_flag(gflags + member, base + (unsigned)(i + 1), local);
         pstamp(dbg, i, 3);
         // 6. time-order copy for the weight-gradient GEMMs (drains behind the next step)
 #pragma unroll
@@ -630,8 +630,8 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
-    __shared__ int s_local;
-    const bool local = group_on_one_xcd((gu32*)(flags) + gridDim.x + group * NU, NU, member, err, spin_limit, &s_local);
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
     if (dbg && threadIdx.x == 0) dbg[(int64_t)blockIdx.x * 8 + 7] = local ? 1 : 0;
 
     // resident B fragments: bw[nt][k] = W_h[unit w H/4 + 16 nt + c][k H + u0 + 8 g .. + 7]
@@ -696,9 +696,9 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
             if (w == 0) {
                 unsigned spins = 0;
                 while (true) {
-                    unsigned f = (unsigned)i;
+                    unsigned f = base + (unsigned)i;
                     if (lane < NU) f = poll_word(gflags + lane, local);
-                    if (__all(f >= (unsigned)i)) break;
+                    if (__all(reached(f, base + (unsigned)i))) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -803,7 +803,7 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) raise_flag(gflags + member, (unsigned)(i + 1), local);
+            if (tid == 0) raise_flag(gflags + member, base + (unsigned)(i + 1), local);
         }
         pstamp(dbg, i, 3);
         // 6. time-order copy of dz for the weight-gradient GEMMs, 16 B per piece from
@@ -849,16 +849,21 @@ extern "C" int ocrk_lstm_fwd_persistent_supported(int B, int H) {
     return grid <= (long)cus * per_cu ? 1 : 0;
 }
 
+extern "C" size_t ocrk_persistent_flags_size(int B, int H) {
+    return (B > 0 && B % PBR == 0 && H > 0 && H % PHU == 0) ? persistent_counter_bytes(B, H) : 0;
+}
+
 extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                                         void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
-                                        void* ws, size_t ws_bytes, void* stream) {
+                                        unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_lstm_fwd_persistent_supported(B, H), "ocrk_lstm_fwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_fwd_persistent_workspace_size(B, H), "ocrk_lstm_fwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
     size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
-    unsigned* cnt = (unsigned*)ws;
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
     bf16* hx = (bf16*)((char*)ws + counters);
-    if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
+    if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
         lstm_fwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
@@ -909,14 +914,15 @@ extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
 
 extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
                                         const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
-                                        void* ws, size_t ws_bytes, void* stream) {
+                                        unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_lstm_bwd_persistent_supported(B, H), "ocrk_lstm_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_bwd_persistent_workspace_size(B, H), "ocrk_lstm_bwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
     size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
-    unsigned* cnt = (unsigned*)ws;
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
     bf16* zx = (bf16*)((char*)ws + counters);
-    if (hipMemsetAsync(cnt, 0, counters, st) != hipSuccess) return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");
+    if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (lstm_bwd_ksplit()) {
         const char* pe = getenv("OCRK_LSTM_BWD_PB16");            // partial products exchanged in bf16

@@ -48,38 +48,59 @@ __device__ __forceinline__ void persistent_role(int ngroups, int nu, int& group,
     }
 }
 
+// Launch setup of a persistent recurrent kernel: the hand-off words count ON
+// across launches, so the caller never clears them (no memset launch in front
+// of every loop). flags[0, grid) are the members' flag words, flags[grid,
+// 2 grid) their XCC census words (`grid` = gridDim.x). Every member of every
+// group ends a launch at the same flag count, so a member's OWN flag, read at
+// launch start, is this launch's base: the waits are for base + n. Census
+// words carry a generation in bits 31:4 (the member's previous word + 1) and
+// the XCC id + 1 in bits 3:0, so last launch's words never pass for this
+// one's. A zeroed buffer is a valid start (base 0, generation 1).
+//
 // Are all members of this workgroup's group on ONE XCD? Each workgroup posts
 // its HW_REG_XCC_ID (+1) once per launch (sc1), wave 0 waits for the group's
 // posts and compares. Placement is the dispatcher's choice: it is measured
 // here, never assumed. On one XCD the group's hand-offs stay in that XCD's L2
 // (plain stores keep the lines in L2; nt loads bypass only the reader's L1);
 // otherwise they use the placement-independent sc1 form.
-__device__ __forceinline__ bool group_on_one_xcd(gu32* xtab, int nu, int member, unsigned* err, unsigned spin_limit,
-                                                 int* s_flag) {
+__device__ __forceinline__ bool persistent_setup(gu32* flags, int group, int nu, int member, unsigned* err,
+                                                 unsigned spin_limit, unsigned& base) {
+    __shared__ unsigned s_setup[3];
     const int tid = threadIdx.x, lane = tid & 63;
+    gu32* xtab = flags + gridDim.x + group * nu;
     if (tid == 0) {
         unsigned x;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-        __hip_atomic_store(xtab + member, (x & 15u) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_setup[0] = __hip_atomic_load(flags + group * nu + member, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned gen = (__hip_atomic_load(xtab + member, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 4) + 1u;
+        s_setup[1] = gen;
+        __hip_atomic_store(xtab + member, (gen << 4) | ((x & 15u) + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();
     if (tid < 64) {
-        unsigned v = 1u, spins = 0;
+        const unsigned gen = s_setup[1];
+        unsigned v = (gen << 4) | 1u, spins = 0;
         while (true) {
             if (lane < nu) v = __hip_atomic_load(xtab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__all(v != 0u)) break;
+            if (__all((v >> 4) == gen)) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > spin_limit) {
                 if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_CENSUS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }
-        const unsigned first = __shfl(v, 0, 64);
-        const bool same = __all(lane >= nu || v == first);
-        if (lane == 0) *s_flag = same ? 1 : 0;
+        const unsigned first = __shfl(v & 15u, 0, 64);
+        const bool same = __all(lane >= nu || ((v >> 4) == gen && (v & 15u) == first));
+        if (lane == 0) s_setup[2] = same ? 1u : 0u;
     }
     __syncthreads();
-    return *s_flag != 0;
+    base = s_setup[0];
+    return s_setup[2] != 0;
 }
+
+// wrap-safe "count has reached target" for the counting flag words
+__device__ __forceinline__ bool reached(unsigned count, unsigned target) { return (int)(count - target) >= 0; }
 
 // The two hand-off forms (see group_on_one_xcd): flag poll, flag raise,
 // 8-B payload store, 16-B payload load.
@@ -116,7 +137,7 @@ __device__ __forceinline__ void group_wait(gu32* gflags, int nu, unsigned target
         while (true) {
             unsigned f = target;
             if (lane < nu) f = poll_word(gflags + lane, local);
-            if (__all(f >= target)) break;
+            if (__all(reached(f, target))) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > spin_limit) {
                 if (lane == 0) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -143,7 +164,8 @@ inline unsigned recur_spin_limit() {
     return v > 0 ? (unsigned)v : (1u << 22);
 }
 
-// flag word + XCC word per workgroup, rounded to a 128-B block
+// flag word + XCC word per workgroup, rounded to a 128-B block (the size of a
+// caller-kept counting buffer as well: ocrk_persistent_flags_size)
 inline size_t persistent_counter_bytes(int B, int H) {
     return ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
 }

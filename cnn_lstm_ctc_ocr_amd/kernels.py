@@ -225,6 +225,34 @@ def lstm_persistent_ok(B, H, dtype):
 
 
 _STATUS = {}
+_FLAGS = {}
+
+
+def persistent_flags(kind, B, H, device):
+    """The counting hand-off words of one persistent entry point (include/ocrk.h,
+    ocrk_persistent_flags_size): zeroed once per (entry point, B, H, device,
+    stream) and kept, so the loops need no clearing launch in front of them.
+    Launches on one stream never overlap, so they may share it; a hipGraph
+    replay keeps counting in the buffer it captured."""
+    device = torch.device(device)
+    key = (kind, B, H, device, torch.cuda.current_stream(device).cuda_stream)
+    t = _FLAGS.get(key)
+    if t is None:
+        nb = _lib.lib().ocrk_persistent_flags_size(B, H)
+        t = _FLAGS[key] = torch.zeros(max(int(nb), 16) // 4, dtype=torch.int32, device=device)
+    return t
+
+
+def reset_persistent_flags():
+    """Re-zero every kept hand-off buffer (after a device error: a loop that gave
+    up leaves its members' counts unequal). In place, so captured graphs stay valid."""
+    for t in _FLAGS.values():
+        t.zero_()
+    if _FLAGS:
+        torch.cuda.synchronize()
+
+
+_lib.ON_DEVICE_ERROR.append(reset_persistent_flags)
 
 
 def status_word(device):
@@ -276,7 +304,8 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
         nb = _lib.lib().ocrk_lstm_fwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
         call("ocrk_lstm_fwd_persistent", ptr(gx), ptr(whT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
-             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(ws), nb, _stream(gx))
+             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_fwd", B, H, dev)), ptr(ws),
+             nb, _stream(gx))
         return out, hprev, cprev, acts
     h_state = torch.zeros(2, 2, B, H, dtype=dtype, device=dev)
     c_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
@@ -298,7 +327,7 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
         nb = _lib.lib().ocrk_lstm_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
         call("ocrk_lstm_bwd_persistent", ptr(wh), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev), ptr(acts), ptr(dG),
-             ptr(lstm_error_word(dev)), ptr(ws), nb, _stream(dout))
+             ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd", B, H, dev)), ptr(ws), nb, _stream(dout))
         return dG
     dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
     dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
@@ -340,7 +369,8 @@ def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
         nb = _lib.lib().ocrk_gru_fwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
         call("ocrk_gru_fwd_persistent", ptr(gx), ptr(whgT), ptr(whcT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
-             ptr(rh_t), ptr(acts), ptr(status_word(dev)), ptr(ws), nb, _stream(gx))
+             ptr(rh_t), ptr(acts), ptr(status_word(dev)), ptr(persistent_flags("gru_fwd", B, H, dev)), ptr(ws), nb,
+             _stream(gx))
         return out, hprev, rh_t, acts
     h = torch.zeros(2, B, H, dtype=dtype, device=dev)
     rh = torch.empty(2, B, H, dtype=dtype, device=dev)
@@ -363,7 +393,7 @@ def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H):
         nb = _lib.lib().ocrk_gru_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
         call("ocrk_gru_bwd_persistent", ptr(whg), ptr(whc), ptr(seq_len), T, B, H, ptr(dout), ptr(hprev), ptr(acts),
-             ptr(dG), ptr(status_word(dev)), ptr(ws), nb, _stream(dout))
+             ptr(dG), ptr(status_word(dev)), ptr(persistent_flags("gru_bwd", B, H, dev)), ptr(ws), nb, _stream(dout))
         return dG
     dzg = torch.empty(2, B, 2 * H, dtype=dtype, device=dev)
     dzc = torch.empty(2, B, H, dtype=dtype, device=dev)

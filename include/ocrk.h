@@ -202,8 +202,8 @@ int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_out, float* d
 int ocrk_lstm_fwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
-                             void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err, void* ws,
-                             size_t ws_bytes, void* stream);
+                             void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
+                             unsigned* flags, void* ws, size_t ws_bytes, void* stream);
 /* Persistent backward time loop (BPTT of the same layer, bf16): ONE launch runs
  * all T reverse steps of both directions with W_h slices in registers, the
  * gate gradients dz exchanged between the co-resident workgroups of a
@@ -213,8 +213,8 @@ int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len
 int ocrk_lstm_bwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
-                             const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err, void* ws,
-                             size_t ws_bytes, void* stream);
+                             const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
+                             unsigned* flags, void* ws, size_t ws_bytes, void* stream);
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
  * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
 int ocrk_lstm_debug_stamps(long long* buf);
@@ -248,13 +248,20 @@ int ocrk_gru_bwd(const void* whg, const void* whc, void* dzg, void* dzc, float* 
 int ocrk_gru_fwd_persistent_supported(int B, int H);
 size_t ocrk_gru_fwd_persistent_workspace_size(int B, int H);
 int ocrk_gru_fwd_persistent(const void* gx, const void* whgT, const void* whcT, const int* seq_len, int T, int B,
-                            int H, void* out, void* hprev_t, void* rh_t, void* acts_t, unsigned* err, void* ws,
-                            size_t ws_bytes, void* stream);
+                            int H, void* out, void* hprev_t, void* rh_t, void* acts_t, unsigned* err,
+                            unsigned* flags, void* ws, size_t ws_bytes, void* stream);
 int ocrk_gru_bwd_persistent_supported(int B, int H);
 size_t ocrk_gru_bwd_persistent_workspace_size(int B, int H);
 int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
                             const void* dout, const void* hprev_t, const void* acts_t, void* dG_t, unsigned* err,
-                            void* ws, size_t ws_bytes, void* stream);
+                            unsigned* flags, void* ws, size_t ws_bytes, void* stream);
+/* Hand-off words of the persistent loops (the `flags` argument of the four
+ * *_persistent entry points above): NULL = they live in the workspace and are
+ * cleared by a memset before every launch; else a caller-kept buffer of
+ * ocrk_persistent_flags_size(B, H) bytes, zeroed ONCE, that the loops count on
+ * from (no clearing launch in front of every loop). Keep one buffer per
+ * (entry point, B, H, stream): launches sharing a buffer must not overlap. */
+size_t ocrk_persistent_flags_size(int B, int H);
 int ocrk_lstm_fwd(const void* gx, const void* whT, void* h_state, float* c_state, const int* seq_len,
                   int T, int B, int H, void* out, void* hprev_t, float* cprev_t, void* acts_t, int dtype,
                   void* stream);
