@@ -71,14 +71,14 @@ SIGNATURES = {
     "ocrk_gru_fwd_persistent": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_gru_bwd_persistent_supported": [_i32, _i32],
     "ocrk_gru_bwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_gru_bwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_gru_bwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_persistent_flags_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_workspace_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_bwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_bwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_debug_stamps": [_p],
     "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],

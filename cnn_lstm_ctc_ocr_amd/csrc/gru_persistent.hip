@@ -293,7 +293,7 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
                           bf16* __restrict__ zxg, const int* __restrict__ seq_len, int T, int B,
                           const bf16* __restrict__ dout, const bf16* __restrict__ hprev_t,
                           const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
-                          unsigned* __restrict__ err, unsigned spin_limit) {
+                          unsigned* __restrict__ err, unsigned spin_limit, float* __restrict__ bpart) {
     constexpr int H = KS * 32, G3 = 3 * H, NU = H / PHU;
     constexpr int KRC = H / 4, KWC = KRC / 32, KRG = H / 2, KWG = KRG / 32;
     constexpr int LDA = KRG + 8, LDP = PHU + 4;
@@ -332,6 +332,7 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
     float dh[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsum[3][4] = {};                              // the bias gradients: (dz_r, dz_u, dz_c) summed over steps
     const auto zxc_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxc, 0, 2 * 2 * B * H * 2, 0x00020000);
     const auto zxg_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxg, 0, 2 * 2 * B * 2 * H * 2, 0x00020000);
 
@@ -422,6 +423,30 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
         st4(gt, dzr);
         st4(gt + H, dzu);
         st4(gt + 2 * H, dzc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            bsum[0][e] += valid ? dzr[e] : 0.f;
+            bsum[1][e] += valid ? dzu[e] : 0.f;
+            bsum[2][e] += valid ? dzc[e] : 0.f;
+        }
+    }
+    if (bpart) {
+        // the layer's bias gradients (model.py:170-180 gates / candidate biases),
+        // fused: the member's 32 rows meet in LDS, one thread per gate column
+        // writes the member's partial; the caller sums the B/32 slices
+        constexpr int LDR = 3 * PHU + 4;
+        float* red = reinterpret_cast<float*>(sA);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[er * LDR + k * PHU + eu + e] = bsum[k][e];
+        __syncthreads();
+        if (tid < 3 * PHU) {
+            float sum = 0.f;
+            for (int r = 0; r < PBR; ++r) sum += red[r * LDR + tid];
+            bpart[(int64_t)(bs * 2 + dir) * G3 + (tid / PHU) * H + u0 + (tid % PHU)] = sum;
+        }
     }
 }
 
@@ -482,7 +507,8 @@ extern "C" int ocrk_gru_bwd_persistent_supported(int B, int H) {
 
 extern "C" int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
                                        const void* dout, const void* hprev_t, const void* acts_t, void* dG_t,
-                                       unsigned* err, unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
+                                       unsigned* err, unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes,
+                                       void* stream) {
     OCRK_REQUIRE(ocrk_gru_bwd_persistent_supported(B, H), "ocrk_gru_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_gru_bwd_persistent_workspace_size(B, H), "ocrk_gru_bwd_persistent: workspace too small");
     OCRK_REQUIRE(err != nullptr, "ocrk_gru_bwd_persistent: status word required");
@@ -498,10 +524,10 @@ extern "C" int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const i
     if (H == 512)
         gru_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)whg, (const bf16*)whc, zxc, zxg, seq_len, T, B,
                                                             (const bf16*)dout, (const bf16*)hprev_t, (const bf16*)acts_t,
-                                                            (bf16*)dG_t, cnt, err, recur_spin_limit());
+                                                            (bf16*)dG_t, cnt, err, recur_spin_limit(), dbias_part);
     else
         gru_bwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)whg, (const bf16*)whc, zxc, zxg, seq_len, T, B,
                                                            (const bf16*)dout, (const bf16*)hprev_t, (const bf16*)acts_t,
-                                                           (bf16*)dG_t, cnt, err, recur_spin_limit());
+                                                           (bf16*)dG_t, cnt, err, recur_spin_limit(), dbias_part);
     return ocrk::launch_status("ocrk_gru_bwd_persistent");
 }

@@ -43,6 +43,31 @@ __device__ __forceinline__ void pstamp(long long* dbg, int s, int i) {
         dbg[(int64_t)blockIdx.x * 8 + (s == 65 ? 6 : i)] = __builtin_amdgcn_s_memrealtime();
 }
 
+// The layer's bias gradient, fused into the BPTT: each thread summed dz of its
+// (row, 4 units, NG gates) over every step in f32 registers; the 32 rows of the
+// member meet in LDS (`red`, >= 32 x (32 NG + 4) floats, free after the loop)
+// and one thread per gate column writes the member's partial
+// part[slice_off + gate H + u0 + unit]; the caller sums the B/32 slices
+// (ocrk_colsum). Fixed order throughout: deterministic. part == NULL: skipped.
+template <int NG>
+__device__ __forceinline__ void bias_partials(float* part, const float (&bsum)[NG][4], float* red, int64_t slice_off,
+                                              int H, int u0) {
+    if (!part) return;
+    constexpr int LDR = NG * PHU + 4;
+    const int tid = threadIdx.x, er = tid >> 3, eu = 4 * (tid & 7);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NG; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[er * LDR + k * PHU + eu + e] = bsum[k][e];
+    __syncthreads();
+    if (tid < NG * PHU) {
+        float sum = 0.f;
+        for (int r = 0; r < PBR; ++r) sum += red[r * LDR + tid];
+        part[slice_off + (tid / PHU) * H + u0 + (tid % PHU)] = sum;
+    }
+}
+
 }  // namespace
 
 extern long long* g_lstm_dbg;
@@ -335,7 +360,8 @@ __global__ void __launch_bounds__(256, 1)
 lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len,
                            int T, int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
                            const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
-                           unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg) {
+                           unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg,
+                           float* __restrict__ bpart) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;
@@ -377,6 +403,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
     float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsum[4][4] = {};                              // the bias gradient: sum of dz over this row's steps
     const int64_t zx_elems = (int64_t)2 * 2 * B * G4;
     auto zx_rsrc = __builtin_amdgcn_make_buffer_rsrc(dzx, 0, (int)(zx_elems * 2), 0x00020000);
     constexpr bool late = LATE && KS == 16;
@@ -559,6 +586,10 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                 dz[2][e] = valid ? dc * cp * af * (1.f - af) : 0.f;
                 dcs[e] = valid ? dc * af : 0.f;
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bsum[k][e] += dz[k][e];
         }
         // 5. publish dz (8-B sc1 stores, one per gate), drain, barrier, one lane raises the flag
         {
@@ -580,6 +611,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
         for (int k = 0; k < 4; ++k) st4(dG_t + tb * G4 + k * H + u0 + eu, dz[k]);
         pstamp(dbg, i, 4);
     }
+    bias_partials<4>(bpart, bsum, reinterpret_cast<float*>(sA), (bs * 2 + dir) * G4, H, u0);
 }
 
 // ---------------------------------------------------- backward, K-split form
@@ -606,7 +638,8 @@ __global__ void __launch_bounds__(256, 1)
 lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const int* __restrict__ seq_len, int T,
                        int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
                        const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
-                       unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg) {
+                       unsigned* __restrict__ err, unsigned spin_limit, long long* __restrict__ dbg,
+                       float* __restrict__ bpart) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;                          // members per group
@@ -662,6 +695,7 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = s_len[er];
     float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};               // the bias gradient: dz of (this unit, gate k), own rows
     // exchange X[parity][group][dst][src][BLK]; a block's element order is the MFMA
     // output order [mt][n-tile half][lane][r], so producer and consumer lanes move
     // 4 contiguous elements each
@@ -756,6 +790,9 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
+            bsum[k] += (dz[k][0] + dz[k][1]) + (dz[k][2] + dz[k][3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int r = 0; r < 4; ++r) sA[(rb + r) * LDA + k * PHU + ul] = bf16_bits(dz[k][r]);
         __syncthreads();
@@ -818,6 +855,20 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
             *reinterpret_cast<u32x4*>(dG_t + (((int64_t)t * B + b0 + row) * 2 + dir) * G4 + k * H + u0 + 8 * q) = val;
         }
         pstamp(dbg, i, 4);
+    }
+    if (bpart) {
+        // the bias partial of (unit ul, gate k) over the member's 32 rows: the
+        // 8 threads holding that unit (4 g x 2 M tiles) meet in LDS, fixed order
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(sAct);                    // [8 row groups][128 gate cols]
+#pragma unroll
+        for (int k = 0; k < 4; ++k) red[(emt * 4 + g) * (4 * PHU) + k * PHU + ul] = bsum[k];
+        __syncthreads();
+        if (tid < 4 * PHU) {
+            float sum = 0.f;
+            for (int q = 0; q < 8; ++q) sum += red[q * (4 * PHU) + tid];
+            bpart[(int64_t)(bs * 2 + dir) * G4 + (tid / PHU) * H + u0 + (tid % PHU)] = sum;
+        }
     }
 }
 
@@ -914,7 +965,7 @@ extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
 
 extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
                                         const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
-                                        unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
+                                        unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream) {
     OCRK_REQUIRE(ocrk_lstm_bwd_persistent_supported(B, H), "ocrk_lstm_bwd_persistent: B=%d H=%d unsupported or not co-resident", B, H);
     OCRK_REQUIRE(ws_bytes >= ocrk_lstm_bwd_persistent_workspace_size(B, H), "ocrk_lstm_bwd_persistent: workspace too small");
     hipStream_t st = ocrk::as_stream(stream);
@@ -930,7 +981,7 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
 #define KSPLIT_LAUNCH(KSV, PB)                                                                                   \
         lstm_bwd_ksplit_kernel<KSV, PB><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout,  \
                                                              cprev_t, (const bf16*)acts_t, (bf16*)dG_t, cnt, err,     \
-                                                             lstm_spin_limit(), g_lstm_dbg)
+                                                             lstm_spin_limit(), g_lstm_dbg, dbias_part)
         if (H == 512) { if (pb16) KSPLIT_LAUNCH(16, true); else KSPLIT_LAUNCH(16, false); }
         else { if (pb16) KSPLIT_LAUNCH(8, true); else KSPLIT_LAUNCH(8, false); }
 #undef KSPLIT_LAUNCH
@@ -938,12 +989,15 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     }
     if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
         lstm_bwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
-                                                                   (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
+                                                                   (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg,
+                                                             dbias_part);
     else if (H == 512)
         lstm_bwd_persistent_kernel<16><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
-                                                             (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
+                                                             (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg,
+                                                             dbias_part);
     else
         lstm_bwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
-                                                            (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
+                                                            (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg,
+                                                             dbias_part);
     return ocrk::launch_status("ocrk_lstm_bwd_persistent");
 }

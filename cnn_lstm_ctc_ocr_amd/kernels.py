@@ -318,21 +318,30 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
     return out, hprev, cprev, acts
 
 
-def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H):
-    _chk(wh, seq_len, dout, cprev, acts)
+def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None):
+    """dG [T,B,2,4H]. dbias (f32 [2*4H], accumulated): the layer's bias gradient
+    (both directions); the persistent loop forms it in-kernel, the per-step
+    path by a column sum of dG."""
+    _chk(wh, seq_len, dout, cprev, acts, dbias)
     dtype = dout.dtype
     dev = dout.device
     dG = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
     if lstm_persistent_ok(B, H, dtype):
         nb = _lib.lib().ocrk_lstm_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
+        part = torch.empty(B // 32, 2 * 4 * H, dtype=torch.float32, device=dev) if dbias is not None else None
         call("ocrk_lstm_bwd_persistent", ptr(wh), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev), ptr(acts), ptr(dG),
-             ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd", B, H, dev)), ptr(ws), nb, _stream(dout))
+             ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd", B, H, dev)), ptr(part), ptr(ws), nb,
+             _stream(dout))
+        if dbias is not None:
+            colsum(part, B // 32, 2 * 4 * H, dbias)
         return dG
     dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
     dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
     call("ocrk_lstm_bwd", ptr(wh), ptr(dg_state), ptr(dc_state), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev),
          ptr(acts), ptr(dG), dtype_code(dtype), _stream(dout))
+    if dbias is not None:
+        colsum(dG, T * B, 2 * 4 * H, dbias)
     return dG
 
 
@@ -383,17 +392,23 @@ def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
     return out, hprev, rh_t, acts
 
 
-def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H):
-    """Returns dG_t [T,B,2,3H] = (dz_r, dz_u, dz_c) per direction."""
-    _chk(whg, whc, seq_len, dout, hprev, acts)
+def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=None):
+    """Returns dG_t [T,B,2,3H] = (dz_r, dz_u, dz_c) per direction. dbias (f32
+    [2*3H], accumulated): the layer's [gates | candidate] bias gradients, formed
+    in the persistent loop (else a column sum of dG)."""
+    _chk(whg, whc, seq_len, dout, hprev, acts, dbias)
     dtype = dout.dtype
     dev = dout.device
     if gru_persistent_ok(B, H, dtype):
         dG = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
         nb = _lib.lib().ocrk_gru_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
+        part = torch.empty(B // 32, 2 * 3 * H, dtype=torch.float32, device=dev) if dbias is not None else None
         call("ocrk_gru_bwd_persistent", ptr(whg), ptr(whc), ptr(seq_len), T, B, H, ptr(dout), ptr(hprev), ptr(acts),
-             ptr(dG), ptr(status_word(dev)), ptr(persistent_flags("gru_bwd", B, H, dev)), ptr(ws), nb, _stream(dout))
+             ptr(dG), ptr(status_word(dev)), ptr(persistent_flags("gru_bwd", B, H, dev)), ptr(part), ptr(ws), nb,
+             _stream(dout))
+        if dbias is not None:
+            colsum(part, B // 32, 2 * 3 * H, dbias)
         return dG
     dzg = torch.empty(2, B, 2 * H, dtype=dtype, device=dev)
     dzc = torch.empty(2, B, H, dtype=dtype, device=dev)
@@ -402,6 +417,8 @@ def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H):
     dG = torch.empty(T, B, 2, 3 * H, dtype=dtype, device=dev)
     call("ocrk_gru_bwd", ptr(whg), ptr(whc), ptr(dzg), ptr(dzc), ptr(dh_tot), ptr(direct), ptr(seq_len), T, B, H,
          ptr(dout), ptr(hprev), ptr(acts), ptr(dG), dtype_code(dtype), _stream(dout))
+    if dbias is not None:
+        colsum(dG, T * B, 2 * 3 * H, dbias)
     return dG
 
 

@@ -247,7 +247,8 @@ class _BiLSTM(torch.autograd.Function):
         if dout.dtype != dt:
             dout = K.cast(dout, dt)
         _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
-        dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H)               # [T,B,2,4H]
+        # [T,B,2,4H]; the bias gradient (both directions) formed in the BPTT loop
+        dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer))
         pre = f"rnn/bdrnn{layer}"
         R = T * B
         with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
@@ -271,7 +272,6 @@ class _BiLSTM(torch.autograd.Function):
                            ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R))
                     K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
                            M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R))
-            K.colsum(dG, R, 2 * G4, store.flat_bias_pair_grad(layer))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
@@ -304,7 +304,8 @@ class _BiGRU(torch.autograd.Function):
         if dout.dtype != dt:
             dout = K.cast(dout, dt)
         _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt)
-        dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H)            # [T,B,2,3H]
+        # [T,B,2,3H]; the [gates | candidate] bias gradients formed in the BPTT loop
+        dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=store.gru_bias_cat_grad(layer))
         pre = f"rnn/bdrnn{layer}"
         R = T * B
         side = side_work(store, x, hprev, rh, dG)
@@ -342,7 +343,6 @@ class _BiGRU(torch.autograd.Function):
                    ldb=2 * G3, ldc=H, splits=_splits(n_in, H, R))
             K.gemm(rhd, dgc, trans_a=True, out=ck[n_in:], accumulate=True, M=H, N=H, K=R, lda=2 * H,
                    ldb=2 * G3, ldc=H, splits=_splits(H, H, R))
-        K.colsum(dG, R, 2 * G3, store.gru_bias_cat_grad(layer))
         side.__exit__(None, None, None)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -214,7 +214,7 @@ int ocrk_lstm_bwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
                              const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
-                             unsigned* flags, void* ws, size_t ws_bytes, void* stream);
+                             unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream);
 /* Diagnostics: when buf != NULL every forward step kernel's workgroups write
  * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
 int ocrk_lstm_debug_stamps(long long* buf);
@@ -254,7 +254,13 @@ int ocrk_gru_bwd_persistent_supported(int B, int H);
 size_t ocrk_gru_bwd_persistent_workspace_size(int B, int H);
 int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
                             const void* dout, const void* hprev_t, const void* acts_t, void* dG_t, unsigned* err,
-                            unsigned* flags, void* ws, size_t ws_bytes, void* stream);
+                            unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream);
+/* dbias_part (the two BPTT entry points; NULL = skipped): f32 [B/32][2][G] with
+ * G = 4H (LSTM) / 3H (GRU): per 32-row batch slice and direction, the sum of the
+ * gate gradients dG_t over its rows and steps -- the layer's bias gradient
+ * (model_bu.py:173-180 / model.py:170-180, tf.gradients of the [x,h].W + b
+ * sums) fused into the loop; the caller sums the B/32 rows (ocrk_colsum)
+ * instead of reading dG_t again. */
 /* Hand-off words of the persistent loops (the `flags` argument of the four
  * *_persistent entry points above): NULL = they live in the workspace and are
  * cleared by a memset before every launch; else a caller-kept buffer of
