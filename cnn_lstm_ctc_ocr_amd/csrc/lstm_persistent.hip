@@ -78,22 +78,37 @@ static unsigned lstm_spin_limit() { return recur_spin_limit(); }
 // hand-off poll, behind the h_{s-1} LDS-DMA, and written to LDS after the MFMAs:
 // vmcnt is in-order, so gx loads issued before the poll made every poll (and
 // the staging wait) wait for their HBM latency as well.
-template <int KS, bool LATE = false>
+// NIN > 0 (H = 512, LATE; the first layer, In = NIN = 256): the input projection
+// x_t . W_x + b is FUSED into the loop instead of read as gx. The member's
+// W_x^T slice (its 128 gate columns x NIN) stays in registers like W_h's; the
+// 32 rows x_t of the step (each row's own t: reverse direction, ragged lengths)
+// are staged by LDS-DMA one step ahead into a 2-deep ring (16-B pieces
+// XOR-swizzled by row, so a fragment read of 16 rows hits 16 bank groups) --
+// issued right behind the h_{s-1} staging DMA, landed by that step's publish
+// drain; the x . W_x MFMAs of step s run at its top, before the hand-off poll
+// (they do not depend on h), the bias is added in the cell. No gx tensor: the
+// [T*B, 8H] projection GEMM and its 2 x 262 MB of HBM traffic (B = 256) go away.
+template <int KS, bool LATE = false, int NIN = 0>
 __global__ void __launch_bounds__(256, 1)
 lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
                            const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out,
                            bf16* __restrict__ hprev_t, float* __restrict__ cprev_t, bf16* __restrict__ acts_t,
                            unsigned* __restrict__ flags, unsigned* __restrict__ err, unsigned spin_limit,
-                           long long* __restrict__ dbg) {
+                           long long* __restrict__ dbg, const bf16* __restrict__ xin = nullptr,
+                           const bf16* __restrict__ wxT = nullptr, const float* __restrict__ bias = nullptr) {
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;                         // members per group
     constexpr int LDH = H + 8;                          // padded LDS row (bf16 elements)
     static_assert(NU <= 64, "one poll lane per member");
     constexpr int LDG = 4 * PHU + 4;                    // padded gate row (floats)
+    constexpr bool fx = NIN > 0;
+    static_assert(!fx || (LATE && KS == 16 && NIN == 256), "fused input projection: H = 512, In = 256, late loads");
+    constexpr int KX = fx ? NIN / 32 : 1;               // k-steps of the input projection
     __shared__ __attribute__((aligned(16))) unsigned short sh[PBR * LDH];
-    __shared__ __attribute__((aligned(16))) unsigned short sgx[PBR * 4 * PHU];   // [row][gate][unit] bf16
+    __shared__ __attribute__((aligned(16))) unsigned short sgx[fx ? 8 : PBR * 4 * PHU];   // [row][gate][unit] bf16
     __shared__ __attribute__((aligned(16))) float sG[PBR * LDG];                 // [row][gate][unit] f32
+    __shared__ __attribute__((aligned(16))) unsigned short sx[fx ? 2 * PBR * NIN : 8];    // x ring [2][row][NIN]
     __shared__ int s_len[PBR];
 
     int group, member;
@@ -123,12 +138,69 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(bw[j][ks]));   // see the BPTT kernel
 
+    // ---- fused input projection: resident W_x^T fragments (same N-tile / lane map as W_h)
+    bf16x8 bx[fx ? 2 : 1][KX];
+    if constexpr (fx) {
+        const bf16* xdir = wxT + (size_t)dir * G4 * NIN;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bf16* row = xdir + (size_t)((2 * j + (c >> 3)) * H + my_unit) * NIN + 8 * g;
+#pragma unroll
+            for (int kx = 0; kx < KX; ++kx) bx[j][kx] = *reinterpret_cast<const bf16x8*>(row + kx * 32);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kx = 0; kx < KX; ++kx) asm volatile("" ::"v"(bx[j][kx]));
+    }
+
     // ---- the epilogue item of this thread: row er, units eu..eu+3 (all 4 gates)
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
     float cst[4] = {0.f, 0.f, 0.f, 0.f}, hst[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsr[fx ? 4 : 1][4];                           // fused: the projection bias of the thread's 16 gate columns
+    if constexpr (fx) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bsr[k][e] = bias[dir * G4 + k * H + u0 + eu + e];
+    }
     if (tid < PBR) s_len[tid] = seq_len[b0 + tid];
     __syncthreads();
+
+    // fused: x_t rows of step `step` into ring slot `buf` -- 4 LDS-DMA wave instructions
+    // of 2 rows x 512 B; lane l fetches logical piece (l & 31) ^ (row & 15) into slot l & 31
+    const __amdgpu_buffer_rsrc_t x_rsrc = uniform_rsrc(fx ? (const void*)xin : (const void*)whT,
+                                                       fx ? (int64_t)T * B * NIN * 2 : 16);
+    // the x rows this lane fetches (fixed over the steps): their lengths and fixed byte parts
+    int xlen[fx ? 4 : 1], xfix[fx ? 4 : 1];
+    if constexpr (fx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = 2 * (w * 4 + q) + (lane >> 5);
+            xlen[q] = s_len[r];
+            xfix[q] = (b0 + r) * NIN * 2 + 16 * ((lane & 31) ^ (r & 15));
+        }
+    }
+    auto issue_x = [&](int step, int buf) {
+        if constexpr (fx) {
+            const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned off = step < T
+                    ? (unsigned)step_time(dir, step, xlen[q]) * (unsigned)(B * NIN * 2) + (unsigned)xfix[q]
+                    : 0x80000000u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    x_rsrc, (__attribute__((address_space(3))) void*)(sx + (buf * PBR + 2 * (wu * 4 + q)) * NIN), 16,
+                    off, 0, 0, 0);
+            }
+        }
+    };
+    if constexpr (fx) {
+        issue_x(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
 
     // gx tile loader: 32 rows x 4 gates x 4 chunks of 8 units = 512 16-B pieces, 2 per thread
     int gx_lr[2], gx_gate[2], gx_q[2];
@@ -172,6 +244,24 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // fused: gates = x_t . W_x (independent of h) -- run in the shadow of the
+        // h_{s-1} staging DMA (at s = 0 there is none)
+        auto x_mma = [&]() {
+            if constexpr (fx) {
+                const unsigned short* xs = sx + (s & 1) * PBR * NIN;
+#pragma unroll
+                for (int kx = 0; kx < KX; ++kx) {
+                    const int sl = (4 * kx + g) ^ c;             // rows c and 16 + c share the swizzle
+                    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&xs[c * NIN + 8 * sl]);
+                    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&xs[(16 + c) * NIN + 8 * sl]);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bx[j][kx], acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bx[j][kx], acc[1][j], 0, 0, 0);
+                    }
+                }
+            }
+        };
 
         if (s > 0) {
             // 1. wait until every member of the group published h_{s-1} (flag >= s)
@@ -191,7 +281,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             __syncthreads();
             pstamp(dbg, s, 1);
             // 2. stage h_{s-1} rows (sc1 loads: the bytes were written through by other CUs)
-            const int64_t base = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
+            const int64_t hbase = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
             if constexpr (KS == 16) {
                 // H = 512: one 1-KB row per LDS-DMA wave instruction, 8 rows per wave,
                 // straight into the padded LDS rows (drained before the barrier below)
@@ -203,7 +293,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                         const int r = wu * (PBR / 4) + q;
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(
                             hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
-                            (unsigned)((base + (int64_t)r * H) * 2) + lo, 0, 0, 2);
+                            (unsigned)((hbase + (int64_t)r * H) * 2) + lo, 0, 0, 2);
                     }
                 } else {
 #pragma unroll
@@ -211,10 +301,15 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                         const int r = wu * (PBR / 4) + q;
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(
                             hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
-                            (unsigned)((base + (int64_t)r * H) * 2) + lo, 0, 0, 16);
+                            (unsigned)((hbase + (int64_t)r * H) * 2) + lo, 0, 0, 16);
                     }
                 }
-                if constexpr (late) {
+                if constexpr (fx) {
+                    asm volatile("" ::: "memory");
+                    issue_x(s + 1, (s + 1) & 1);                 // next step's x rows behind the 8 DMAs
+                    x_mma();                                     // while the h rows land
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                } else if constexpr (late) {
                     asm volatile("" ::: "memory");
                     load_gx();                                   // 2 loads behind the 8 DMAs
                     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -227,7 +322,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             for (int v = 0; v < PBR * H / 8 / 256; ++v) {
                 const int idx = tid + 256 * v;
                 const int row = idx / (H / 8), kq = idx % (H / 8);
-                const int off = (int)((base + (int64_t)row * H + 8 * kq) * 2);
+                const int off = (int)((hbase + (int64_t)row * H + 8 * kq) * 2);
                 hv[v] = get16(hx_rsrc, off, local);
             }
 #pragma unroll
@@ -237,6 +332,9 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                 *reinterpret_cast<u32x4*>(&sh[row * LDH + 8 * kq]) = hv[v];
             }
             }
+        } else if constexpr (fx) {
+            issue_x(1, 1);
+            x_mma();
         } else if constexpr (late) {
             load_gx();
         }
@@ -261,7 +359,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
             }
         }
 
-        if constexpr (late) {
+        if constexpr (late && !fx) {
             // the gx tile, landed during the MFMAs (read after the barrier below; the
             // previous step's reads of sgx ended before its flag barrier)
 #pragma unroll
@@ -287,10 +385,15 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const f32x4 z = *reinterpret_cast<const f32x4*>(&sG[er * LDG + k * PHU + eu]);
-            typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
-            const u16x4 xg = *reinterpret_cast<const u16x4*>(&sgx[(er * 4 + k) * PHU + eu]);
+            if constexpr (fx) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a4[k][e] = z[e] + bits_f(xg[e]);
+                for (int e = 0; e < 4; ++e) a4[k][e] = z[e] + bsr[k][e];
+            } else {
+                typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+                const u16x4 xg = *reinterpret_cast<const u16x4*>(&sgx[(er * 4 + k) * PHU + eu]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a4[k][e] = z[e] + bits_f(xg[e]);
+            }
         }
         float hn[4], cp[4], hp[4];
 #pragma unroll
@@ -926,6 +1029,42 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
         lstm_fwd_persistent_kernel<8><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,
                                                             (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err, lstm_spin_limit(), g_lstm_dbg);
     return ocrk::launch_status("ocrk_lstm_fwd_persistent");
+}
+
+// Fused first layer: x [T][B][n_in] (time-major features), wxT [2][4H][n_in] (per
+// direction W_x^T, gate-major rows), bias f32 [2][4H]; everything else as above.
+extern "C" int ocrk_lstm_fwd_persistent_x_supported(int B, int H, int n_in) {
+    if (H != 512 || n_in != 256 || B % PBR) return 0;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_fwd_persistent_kernel<16, true, 256>, 256, 0) != hipSuccess)
+        return 0;
+    const long grid = 2L * (B / PBR) * (H / PHU);
+    return grid <= (long)cus * per_cu ? 1 : 0;
+}
+
+extern "C" int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* wxT, const float* bias, const void* whT,
+                                          const int* seq_len, int T, int B, int H, void* out, void* hprev_t,
+                                          float* cprev_t, void* acts_t, unsigned* err, unsigned* flags, void* ws,
+                                          size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(ocrk_lstm_fwd_persistent_x_supported(B, H, n_in),
+                 "ocrk_lstm_fwd_persistent_x: B=%d H=%d n_in=%d unsupported or not co-resident", B, H, n_in);
+    OCRK_REQUIRE(ws_bytes >= ocrk_lstm_fwd_persistent_workspace_size(B, H), "ocrk_lstm_fwd_persistent_x: workspace too small");
+    OCRK_REQUIRE(x && wxT && bias && err, "ocrk_lstm_fwd_persistent_x: null operand");
+    OCRK_REQUIRE((int64_t)T * B * n_in * 2 < 0x7fffffffll, "ocrk_lstm_fwd_persistent_x: x exceeds 2 GB");
+    if (T <= 0) return OCRK_OK;
+    hipStream_t st = ocrk::as_stream(stream);
+    size_t counters = ((size_t)2 * 2 * (B / PBR) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
+    bf16* hx = (bf16*)((char*)ws + counters);
+    if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_lstm_fwd_persistent_x memset");
+    const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
+    lstm_fwd_persistent_kernel<16, true, 256><<<grid, 256, 0, st>>>(
+        nullptr, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t, (bf16*)acts_t, cnt, err,
+        lstm_spin_limit(), g_lstm_dbg, (const bf16*)x, (const bf16*)wxT, bias);
+    return ocrk::launch_status("ocrk_lstm_fwd_persistent_x");
 }
 
 // ---------------------------------------------------------- backward C ABI

@@ -318,6 +318,39 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
     return out, hprev, cprev, acts
 
 
+def lstm_fused_x_ok(B, H, n_in, dtype, force=False):
+    """Run the first layer's input projection fused into the persistent forward
+    (ocrk_lstm_fwd_persistent_x)? Opt-in (OCRK_LSTM_FUSE_X=1, or force): measured
+    at B=256 it removes the 109 us projection GEMM but makes every step 0.7 us
+    longer (3.40 vs 2.68 us: the x.W_x MFMAs and the x-row DMA land on the
+    step's critical path), 480 vs 490 us for GEMM + loop alone and 5.865 vs
+    5.847 ms for the train step (profiles/r3_fused_projection.txt)."""
+    import os
+    if not force and os.environ.get("OCRK_LSTM_FUSE_X", "0") != "1":
+        return False
+    if not lstm_persistent_ok(B, H, dtype):
+        return False
+    return bool(_lib.lib().ocrk_lstm_fwd_persistent_x_supported(B, H, n_in))
+
+
+def lstm_fwd_fused_x(x, wxT, bias, whT, seq_len, T, B, H):
+    """The persistent forward with x . W_x + b fused (no gx): x [T,B,In] bf16,
+    wxT [8H, In] (fw | bw W_x^T), bias f32 [8H]. Same outputs as lstm_fwd."""
+    _chk(x, wxT, bias, whT, seq_len)
+    dev = x.device
+    n_in = x.shape[-1]
+    out = torch.empty(T, B, 2 * H, dtype=x.dtype, device=dev)
+    hprev = torch.empty(T, B, 2, H, dtype=x.dtype, device=dev)
+    cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
+    acts = torch.empty(T, B, 2, 4 * H, dtype=x.dtype, device=dev)
+    nb = _lib.lib().ocrk_lstm_fwd_persistent_workspace_size(B, H)
+    ws = _ws(nb, dev)
+    call("ocrk_lstm_fwd_persistent_x", ptr(x), n_in, ptr(wxT), ptr(bias), ptr(whT), ptr(seq_len), T, B, H, ptr(out),
+         ptr(hprev), ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_fwd_x", B, H, dev)),
+         ptr(ws), nb, _stream(x))
+    return out, hprev, cprev, acts
+
+
 def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None):
     """dG [T,B,2,4H]. dbias (f32 [2*4H], accumulated): the layer's bias gradient
     (both directions); the persistent loop forms it in-kernel, the per-step

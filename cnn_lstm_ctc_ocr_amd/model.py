@@ -213,6 +213,19 @@ class side_work:
         return False
 
 
+_DEFER_DWX = os.environ.get("OCRK_DEFER_DWX", "0") == "1"
+
+
+def _run_deferred(store):
+    """Issue weight-gradient work an upper layer deferred (on the side stream,
+    behind everything issued so far on the main stream)."""
+    pending = getattr(store, "deferred", None)
+    while pending:
+        fn, tensors = pending.pop(0)
+        with side_work(store, *tensors):
+            fn()
+
+
 def _conv_side(store, *tensors):
     """Conv weight gradients on the side stream, overlapping the main stream's
     data-gradient GEMMs and BN backward (OCRK_CONV_SIDE=0: issue them inline)."""
@@ -230,8 +243,12 @@ class _BiLSTM(torch.autograd.Function):
         T, B, n_in = x.shape
         H = store.cfg.rnn_sizes[layer - 1]
         wxT, _wx, whT, _wh, bias = store.lstm_images(layer, dt)
-        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
-        out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt)
+        if K.lstm_fused_x_ok(B, H, n_in, dt):
+            # the input projection inside the persistent loop (first layer: In = 256)
+            out, hprev, cprev, acts = K.lstm_fwd_fused_x(x, wxT, bias, whT, seq_len, T, B, H)
+        else:
+            gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
+            out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt)
         ctx.store, ctx.layer, ctx.H = store, layer, H
         ctx.save_for_backward(x, seq_len, hprev, cprev, acts)
         return out
@@ -249,6 +266,7 @@ class _BiLSTM(torch.autograd.Function):
         _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
         # [T,B,2,4H]; the bias gradient (both directions) formed in the BPTT loop
         dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer))
+        _run_deferred(store)                                 # an upper layer's dW_x, now behind this BPTT
         pre = f"rnn/bdrnn{layer}"
         R = T * B
         with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
@@ -259,12 +277,17 @@ class _BiLSTM(torch.autograd.Function):
                 # both directions as one batched GEMM each (batch = direction: dG column
                 # block d * 4H, h_prev column block d * H, gradient d * (In+H) * 4H):
                 # dW_x = x^T . dG_d ; dW_h = h_prev_d^T . dG_d  (split-K over T*B)
-                K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
-                       ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
-                       splits=_splits(n_in, G4, R, batch=2))
+                def dw_x():
+                    K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
+                           ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
+                           splits=_splits(n_in, G4, R, batch=2))
                 K.gemm(hprev.view(R, 2 * H), dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G4, K=R,
                        lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4, stride_c=sk,
                        splits=_splits(H, G4, R, batch=2))
+                if layer > 1 and _DEFER_DWX and ctx.needs_input_grad[0]:
+                    store.deferred.append((dw_x, (x, dG)))   # issued behind the next BPTT (fewer CUs held)
+                else:
+                    dw_x()
             else:
                 for d, gk in enumerate((gf, gb)):
                     dgd = dg[:, d * G4:]                                         # view, ldb = 8H

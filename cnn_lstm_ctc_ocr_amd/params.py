@@ -139,6 +139,7 @@ class ParamStore:
         self.version = 0
         self._images = {}
         self.pending = []          # events of side-stream gradient work not yet joined
+        self.deferred = []         # (launch fn, tensors) of gradient work an upper layer deferred
         self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
 
     # ------------------------------------------------------------ state
@@ -173,6 +174,9 @@ class ParamStore:
     def join(self):
         """Make the current stream wait for side-stream gradient work
         (model.side_work) so flat_grad is complete in stream order."""
+        while self.deferred:        # never issued (no lower layer ran): issue it here, in order
+            fn, _tensors = self.deferred.pop(0)
+            fn()
         if self.pending:
             cur = torch.cuda.current_stream(self.device)
             for ev in self.pending:

@@ -204,6 +204,15 @@ size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                              void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
                              unsigned* flags, void* ws, size_t ws_bytes, void* stream);
+/* The first layer's forward loop with its input projection FUSED (model_bu.py:186-192's
+ * [x, h] . W for the x half): x dtype=bf16 [T][B][n_in] time-major features, wxT
+ * [2][4H][n_in] (per-direction W_x^T, gate-major rows), bias f32 [2][4H]; no gx
+ * tensor and no projection GEMM. H = 512, n_in = 256 (the conv features). */
+int ocrk_lstm_fwd_persistent_x_supported(int B, int H, int n_in);
+int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* wxT, const float* bias, const void* whT,
+                               const int* seq_len, int T, int B, int H, void* out, void* hprev_t, float* cprev_t,
+                               void* acts_t, unsigned* err, unsigned* flags, void* ws, size_t ws_bytes,
+                               void* stream);
 /* Persistent backward time loop (BPTT of the same layer, bf16): ONE launch runs
  * all T reverse steps of both directions with W_h slices in registers, the
  * gate gradients dz exchanged between the co-resident workgroups of a

@@ -121,3 +121,41 @@ def test_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
     # the default limit on the same launch: no bit
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
     assert K.read_status(cuda) == 0
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_fused_input_projection_forward(cuda, B):
+    """The first layer's forward with x . W_x + b fused into the persistent loop
+    (ocrk_lstm_fwd_persistent_x, In = 256, H = 512) against the projection GEMM +
+    persistent loop, and both against the float oracle; ragged lengths. The
+    fused form skips gx's bf16 rounding, so the two differ by a few bf16 ulps."""
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    T, n_in, H = 23, 256, 512
+    rng = np.random.default_rng(31 + B)
+    bf = lambda a: torch.from_numpy(a.astype(np.float32)).bfloat16().float().numpy()   # noqa: E731
+    x = bf(rng.standard_normal((T, B, n_in)))
+    ks = [bf(rng.standard_normal((n_in + H, 4 * H)) * 0.1) for _ in range(2)]
+    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
+    seq = rng.integers(1, T + 1, B).astype(np.int32)
+    seq[:3] = [T, 1, T - 1]
+    outs, _ = zip(*[G.lstm_dir_fwd(x, seq, ks[d], bs[d], d == 1) for d in range(2)])
+    ref = np.concatenate(outs, axis=2)
+    wxT = torch.from_numpy(np.ascontiguousarray(np.concatenate([k[:n_in].T for k in ks], 0))).to(cuda).bfloat16()
+    whT = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))).to(cuda).bfloat16()
+    bias = torch.from_numpy(np.concatenate(bs)).to(cuda)
+    xd = torch.from_numpy(x).to(cuda).bfloat16().contiguous()
+    seq_d = torch.from_numpy(seq).to(cuda)
+    assert K.lstm_fused_x_ok(B, H, n_in, torch.bfloat16, force=True)
+    K.status_word(cuda).zero_()
+    gx = K.gemm(xd.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=torch.bfloat16)
+    unf = K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.bfloat16)
+    fus = K.lstm_fwd_fused_x(xd, wxT, bias, whT, seq_d, T, B, H)
+    torch.cuda.synchronize()
+    assert K.read_status(cuda) == 0
+    for a, b in zip(unf, fus):
+        assert (a.float() - b.float()).abs().max().item() < 6e-2 * max(1.0, a.float().abs().max().item())
+    out = fus[0].float().cpu().numpy()
+    assert np.linalg.norm(out - ref) / np.linalg.norm(ref) < 3e-2
+    assert np.all(out[seq[1]:, 1] == 0)
+    # the saved tensors the BPTT reads: activations of the unfused path within bf16 noise
+    np.testing.assert_allclose(fus[2].cpu().numpy(), unf[2].cpu().numpy(), atol=5e-2)
