@@ -719,7 +719,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 
 // ---------------------------------------------------- backward, K-split form
 // The same BPTT with the recurrent product split over the members by K
-// instead of by output unit (default; OCRK_LSTM_BWD_KSPLIT=0 selects the
+// instead of by output unit (opt-in, OCRK_LSTM_BWD_KSPLIT=1; the default is the
 // gather form above). Member m computes, from ITS OWN dz (the 4 gates x 32
 // units it just produced, never exchanged), the partial product
 //   P_m[32 rows, H units] = dz_m[32 rows, 128 gate cols] . W_h[H units, own 128 gate cols]^T
