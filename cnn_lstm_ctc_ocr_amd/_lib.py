@@ -53,6 +53,7 @@ SIGNATURES = {
     "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],
     "ocrk_conv3x3_bwd_data_workspace_size": [_i32, _i32, _i32, _i32],
     "ocrk_conv3x3_bwd_data": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_conv3x3_bwd_data_slab": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p],
     "ocrk_conv3x3_wgrad_workspace_size": [_i32, _i32, _i32, _i32, _i32],
     "ocrk_conv3x3_bwd_weight": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_bn_finalize_workspace_size": [_i32, _i32],
@@ -63,6 +64,9 @@ SIGNATURES = {
     "ocrk_bn_bwd_workspace_size": [_i32, _i32, _i32, _i32],
     "ocrk_bn_relu_pool_bwd": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
                               _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_bn_bwd_bias_slab_rows": [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32],
+    "ocrk_bn_relu_pool_bwd_slab": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                                   _i32, _p, _p, _p, _i32, _p, _p, _sz, _i32, _p],
     "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_copy_batch": [_p, _i32, _i64, _p],
@@ -93,6 +97,8 @@ SIGNATURES = {
     "ocrk_strided_copy": [_p, _i64, _i64, _i64, _i64, _p, _i32, _i64, _i64, _p],
     "ocrk_colsum_workspace_size": [_i64, _i32],
     "ocrk_colsum": [_p, _i64, _i32, _i32, _p, _i32, _p, _sz, _p],
+    "ocrk_slab_sum_workspace_size": [_i32],
+    "ocrk_slab_sum": [_p, _i32, _i32, _i32, _p, _i32, _p, _sz, _p],
     "ocrk_relu_mask": [_p, _p, _i64, _f32, _p, _i32, _p],
     "ocrk_mul_scalar": [_p, _i64, _p, _p],
     "ocrk_mean": [_p, _i32, _p, _p],
@@ -106,6 +112,7 @@ _RESTYPE = {"ocrk_last_error": ctypes.c_char_p}
 _RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspace_size")})
 _RESTYPE["ocrk_conv_stats_tiles"] = ctypes.c_size_t
 _RESTYPE["ocrk_persistent_flags_size"] = ctypes.c_size_t
+_RESTYPE["ocrk_bn_bwd_bias_slab_rows"] = ctypes.c_size_t
 _RESTYPE["ocrk_crc32c"] = ctypes.c_uint32
 
 

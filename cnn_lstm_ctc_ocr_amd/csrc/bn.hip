@@ -584,11 +584,30 @@ extern "C" size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C) {
     return bn_ws_floats(nb, C) * sizeof(float) + (size_t)B * H * W * C * sizeof(float);
 }
 
-extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C,
-                                     const float* mean, const float* invstd, const float* gamma,
-                                     const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
-                                     void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
-                                     void* ws, size_t ws_bytes, int dtype, void* stream) {
+// Rows of the conv-bias partial-sum slab the apply pass writes (one per block).
+static int64_t bn_bwd_bias_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw) {
+    const int64_t items = (int64_t)B * H * W * (C / 8);
+    int64_t nb = bn_bwd_blocks(items);
+    nb = ocrk::cdiv(items, bn_bwd_ipb(items, nb));
+    if (bn_route_variant(kh, kw, sh, sw, H, W) % 2 == 1) {             // window-walk apply (variants 1, 3)
+        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
+        const int64_t tasks = (int64_t)B * Ho * ocrk::cdiv(Wo, BN_ROUTE_SEG) * (C / 8);
+        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
+        const int64_t tpb = ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256;
+        return ocrk::cdiv(tasks, tpb);
+    }
+    return nb;
+}
+
+extern "C" size_t ocrk_bn_bwd_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw) {
+    if (C < 8 || C % 8 != 0 || (int64_t)B * H * W == 0) return 1;
+    return (size_t)bn_bwd_bias_rows(B, H, W, C, kh, kw, sh, sw);
+}
+
+static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
+                       const float* invstd, const float* gamma, const float* beta, int kh, int kw, int sh, int sw,
+                       int dp_time_major, void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                       float* bias_slab_out, void* ws, size_t ws_bytes, int dtype, void* stream) {
     OCRK_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "ocrk_bn_relu_pool_bwd: C=%d unsupported", C);
     OCRK_REQUIRE(ws_bytes >= ocrk_bn_bwd_workspace_size(B, H, W, C), "ocrk_bn_relu_pool_bwd: workspace too small");
     const int64_t items = (int64_t)B * H * W * (C / 8);
@@ -600,7 +619,7 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
     double* part = (double*)ws;
     float* slab = (float*)(part + (size_t)SLAB_P * 2 * C);
     float* dsum = slab + nb * 2 * C;
-    float* bslab = dsum + 2 * C;
+    float* bslab = bias_slab_out ? bias_slab_out : dsum + 2 * C;
     void* da = (float*)ws + bn_ws_floats(nb, C);
     const int npix = B * H * W;
     hipStream_t s = ocrk::as_stream(stream);
@@ -660,15 +679,38 @@ extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H
         }
 #undef APPLY_ARGS
         st = ocrk::launch_status("ocrk_bn_relu_pool_bwd apply (window walk)");
-        if (st || !dbias) return st;
+        if (st || !dbias || bias_slab_out) return st;
         return slab_sum(bslab, nr, C, part, nullptr, dbias, nullptr, C, accumulate, s);
     }
-    float* bs = dbias ? bslab : nullptr;
+    float* bs = (dbias || bias_slab_out) ? bslab : nullptr;
     if (dtype == OCRK_BF16)
         bn_bwd_apply_kernel<bf16><<<nb, 256, 0, s>>>((const bf16*)z, (const bf16*)da, npix, C, mean, invstd, gamma, dsum, (int)ipb, (bf16*)dz, bs);
     else
         bn_bwd_apply_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)da, npix, C, mean, invstd, gamma, dsum, (int)ipb, (float*)dz, bs);
     st = ocrk::launch_status("ocrk_bn_relu_pool_bwd apply");
-    if (st || !dbias) return st;
+    if (st || !dbias || bias_slab_out) return st;
     return slab_sum(bslab, (int)nb, C, part, nullptr, dbias, nullptr, C, accumulate, s);
+}
+
+extern "C" int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, int C,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                     void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                                     void* ws, size_t ws_bytes, int dtype, void* stream) {
+    return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
+                       dbeta, dbias, accumulate, nullptr, ws, ws_bytes, dtype, stream);
+}
+
+// The same with the conv-bias partials left to the caller: bias_slab gets
+// ocrk_bn_bwd_bias_slab_rows(...) rows of C floats; ocrk_slab_sum(bias_slab,
+// rows, C, C, dbias, ...) on any stream ordered after this call gives the dbias
+// of ocrk_bn_relu_pool_bwd (same bits), off the critical path.
+extern "C" int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, int H, int W, int C,
+                                          const float* mean, const float* invstd, const float* gamma,
+                                          const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                          void* dz, float* dgamma, float* dbeta, int accumulate, float* bias_slab,
+                                          void* ws, size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(bias_slab, "ocrk_bn_relu_pool_bwd_slab: bias_slab is required");
+    return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
+                       dbeta, nullptr, accumulate, bias_slab, ws, ws_bytes, dtype, stream);
 }

@@ -324,6 +324,22 @@ extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, con
 // workspace: stats [tiles][2 cin] f32 | part [SLAB_P][cin] double
 static int64_t bwd_data_tiles(int B, int H, int W) { return ocrk::cdiv((int64_t)B * H * W, 128); }
 
+// dx (and, with stats, the per-tile column statistics of the masked dx)
+static int bwd_data_run(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                        const void* relu_mask, float* stats, int dtype, hipStream_t s) {
+    ocrk::GemmParams p = {};
+    p.M = B * H * W; p.N = cin; p.K = 9 * cout; p.batch = 1;
+    p.A = dy; p.B = w_bwd; p.ldb = 9 * cout;
+    p.C = dx; p.ldc = cin; p.c_bf16 = dtype == OCRK_BF16;
+    p.mask = relu_mask; p.ldmask = cin; p.alpha = 1.f;
+    p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
+    p.convH = H; p.convW = W; p.convC = cout;
+    p.stats = stats;
+    int st = dtype == OCRK_BF16 ? ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s) : -1;
+    if (st < 0) st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
+    return st;
+}
+
 extern "C" size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin) {
     return ((size_t)bwd_data_tiles(B, H, W) * 2 * cin * sizeof(float) + 7) / 8 * 8 +
            (size_t)ocrk::SLAB_P * cin * sizeof(double);
@@ -332,25 +348,27 @@ extern "C" size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int 
 extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd,
                                      int cin, void* dx, const void* relu_mask, float* dbias, int accumulate,
                                      void* ws, size_t ws_bytes, int dtype, void* stream) {
-    ocrk::GemmParams p = {};
-    p.M = B * H * W; p.N = cin; p.K = 9 * cout; p.batch = 1;
-    p.A = dy; p.B = w_bwd; p.ldb = 9 * cout;
-    p.C = dx; p.ldc = cin; p.c_bf16 = dtype == OCRK_BF16;
-    p.mask = relu_mask; p.ldmask = cin; p.alpha = 1.f;
-    p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
-    p.convH = H; p.convW = W; p.convC = cout;
-    if (dbias) {
-        OCRK_REQUIRE(ws && ws_bytes >= ocrk_conv3x3_bwd_data_workspace_size(B, H, W, cin),
-                     "ocrk_conv3x3_bwd_data: workspace too small for the bias gradient");
-        p.stats = (float*)ws;
-    }
     hipStream_t s = ocrk::as_stream(stream);
-    int st = dtype == OCRK_BF16 ? ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, p.stats, s) : -1;
-    if (st < 0) st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
-    if (st || !dbias) return st;
+    if (!dbias) return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, nullptr, dtype, s);
+    OCRK_REQUIRE(ws && ws_bytes >= ocrk_conv3x3_bwd_data_workspace_size(B, H, W, cin),
+                 "ocrk_conv3x3_bwd_data: workspace too small for the bias gradient");
+    int st = bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, (float*)ws, dtype, s);
+    if (st) return st;
     const int tiles = (int)bwd_data_tiles(B, H, W);
     double* part = (double*)((char*)ws + ((size_t)tiles * 2 * cin * sizeof(float) + 7) / 8 * 8);
     return ocrk::slab_sum((const float*)ws, tiles, cin, part, nullptr, dbias, nullptr, cin, accumulate, s, 2 * cin);
+}
+
+// The same with the bias-gradient partials left to the caller: `slab` gets the
+// per-128-row-tile column (sum, M2) of the masked dx, [ocrk_conv_stats_tiles(B*H*W)]
+// rows of 2*cin floats (sums in the first cin); ocrk_slab_sum(slab, tiles, cin,
+// 2*cin, dbias, ...) on any stream ordered after this call gives the dbias of
+// ocrk_conv3x3_bwd_data -- the same bits, off the data-gradient critical path.
+extern "C" int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, int cout, const void* w_bwd,
+                                          int cin, void* dx, const void* relu_mask, float* slab, int dtype,
+                                          void* stream) {
+    OCRK_REQUIRE(slab, "ocrk_conv3x3_bwd_data_slab: slab is required");
+    return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, slab, dtype, ocrk::as_stream(stream));
 }
 
 static int wgrad_splits(int64_t M, int cin, int cout) {

@@ -154,7 +154,13 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     for (int kt = 0; kt < nk; ++kt) {
         // stage kt landed: the stages issued after it (up to S-2 of them) may stay in flight
         const int ahead = min(S - 2, nk - 1 - kt);
-        if constexpr (S >= 4) {
+        if constexpr (S >= 5) {
+            if (ahead >= 4) vm_wait<4 * NPS>();
+            else if (ahead == 3) vm_wait<3 * NPS>();
+            else if (ahead == 2) vm_wait<2 * NPS>();
+            else if (ahead == 1) vm_wait<NPS>();
+            else vm_wait<0>();
+        } else if constexpr (S >= 4) {
             if (ahead >= 2) vm_wait<2 * NPS>();
             else if (ahead == 1) vm_wait<NPS>();
             else vm_wait<0>();
@@ -354,6 +360,8 @@ int launch_nt(const GemmParams& p, hipStream_t stream) {
 //   6: 256 x 256 x 64 / 2, 8 waves -> 128 KB -> 1 (2 waves per SIMD)
 //   7: 256 x 128 x 64 / 2, 8 waves ->  96 KB -> 1   8: 256 x 256 x 32 / 3, 8 waves -> 96 KB
 //   9: 256 x 256 x 32 / 4, 8 waves -> 128 KB       10: 256 x 128 x 32 / 4, 8 waves -> 64 KB -> 2
+//  11: 128 x 128 x 32 / 6 -> 96 KB -> 1           12: 128 x 128 x 32 / 5 -> 80 KB -> 2
+//  13: 128 x 128 x 64 / 4 -> 128 KB -> 1          14: 128 x 64 x 64 / 3 -> 72 KB -> 2
 int nt_cfg() {
     static int c = -2;
     if (c == -2) {
@@ -377,6 +385,10 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
         case 8: return launch_nt<256, 256, 32, 3, 2, AM, 8>(p, s);
         case 9: return launch_nt<256, 256, 32, 4, 2, AM, 8>(p, s);
         case 10: return launch_nt<256, 128, 32, 4, 4, AM, 8>(p, s);
+        case 11: return launch_nt<128, 128, 32, 6, 2, AM>(p, s);
+        case 12: return launch_nt<128, 128, 32, 5, 2, AM>(p, s);
+        case 13: return launch_nt<128, 128, 64, 4, 2, AM>(p, s);
+        case 14: return launch_nt<128, 64, 64, 3, 2, AM>(p, s);
         default: break;
     }
     // measured on MI355X (tools/bench_gemm.py): narrow N -> BK=32, 3 stages;

@@ -224,6 +224,17 @@ extern "C" int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* o
     return ocrk::slab_sum((const float*)ws, (int)nb, N, part, nullptr, out, nullptr, N, accumulate, s);
 }
 
+extern "C" size_t ocrk_slab_sum_workspace_size(int nc) { return (size_t)ocrk::SLAB_P * std::max(nc, 1) * sizeof(double); }
+
+extern "C" int ocrk_slab_sum(const float* slab, int nslab, int nc, int ld, float* out, int accumulate, void* ws,
+                             size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(nslab >= 0 && nc >= 0 && ld >= nc, "ocrk_slab_sum: bad sizes");
+    OCRK_REQUIRE(ws_bytes >= ocrk_slab_sum_workspace_size(nc), "ocrk_slab_sum: workspace too small");
+    if (nc == 0) return OCRK_OK;
+    return ocrk::slab_sum(slab, nslab, nc, (double*)ws, nullptr, out, nullptr, nc, accumulate, ocrk::as_stream(stream),
+                          ld);
+}
+
 extern "C" int ocrk_relu_mask(const float* dy, const float* y, int64_t n, float scale, void* out, int out_dtype,
                               void* stream) {
     if (n == 0) return OCRK_OK;

@@ -97,13 +97,23 @@ def conv3x3_fwd(x, w_nk, bias, relu, stats=None, y_dtype=None):
     return y
 
 
-def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True):
+def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True, defer=None):
     """dx = conv3x3 backward-data (ReLU mask of the producer fused); if dbias
-    is given, dbias (+)= column sums of dx (the producer's bias gradient)."""
+    is given, dbias (+)= column sums of dx (the producer's bias gradient).
+    With a `defer` list, that reduction is appended to it as (fn, tensors) for
+    the caller to issue later (e.g. on the side stream): same bits, off the
+    data-gradient path (ocrk_conv3x3_bwd_data_slab + ocrk_slab_sum)."""
     _chk(dy, w_bwd, relu_mask, dbias)
     B, H, W, Cout = dy.shape
     Cin = w_bwd.shape[0]
     dx = torch.empty(B, H, W, Cin, dtype=dy.dtype, device=dy.device)
+    if dbias is not None and defer is not None:
+        tiles = conv_stats_tiles(B * H * W)
+        slab = torch.empty(tiles, 2 * Cin, dtype=torch.float32, device=dy.device)
+        call("ocrk_conv3x3_bwd_data_slab", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_mask),
+             ptr(slab), dtype_code(dy.dtype), _stream(dy))
+        defer.append((lambda: slab_sum(slab, tiles, Cin, 2 * Cin, dbias, accumulate), (slab,)))
+        return dx
     nb, ws = 0, None
     if dbias is not None:
         nb = _lib.lib().ocrk_conv3x3_bwd_data_workspace_size(B, H, W, Cin)
@@ -159,15 +169,25 @@ def bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=False):
 
 
 def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True,
-                     dbias=None):
+                     dbias=None, defer=None):
     """dz of BN + ReLU + max-pool; dgamma, dbeta and (optionally) dbias = column
-    sums of dz (the conv bias in front of the BN) accumulate in f32."""
+    sums of dz (the conv bias in front of the BN) accumulate in f32. With a
+    `defer` list the dbias reduction is appended to it as (fn, tensors)
+    (ocrk_bn_relu_pool_bwd_slab + ocrk_slab_sum, same bits)."""
     _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta, dbias)
     B, H, W, C = z.shape
     kh, kw, sh, sw = pool
     nb = _lib.lib().ocrk_bn_bwd_workspace_size(B, H, W, C)
     ws = _ws(nb, z.device)
     dz = torch.empty_like(z)
+    if dbias is not None and defer is not None:
+        rows = _lib.lib().ocrk_bn_bwd_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
+        slab = torch.empty(rows, C, dtype=torch.float32, device=z.device)
+        call("ocrk_bn_relu_pool_bwd_slab", ptr(z), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma),
+             ptr(beta), kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), int(accumulate),
+             ptr(slab), ptr(ws), nb, dtype_code(z.dtype), _stream(z))
+        defer.append((lambda: slab_sum(slab, rows, C, C, dbias, accumulate), (slab,)))
+        return dz
     call("ocrk_bn_relu_pool_bwd", ptr(z), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
          kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), ptr(dbias), int(accumulate),
          ptr(ws), nb,
@@ -351,10 +371,11 @@ def lstm_fwd_fused_x(x, wxT, bias, whT, seq_len, T, B, H):
     return out, hprev, cprev, acts
 
 
-def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None):
+def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None, defer=None):
     """dG [T,B,2,4H]. dbias (f32 [2*4H], accumulated): the layer's bias gradient
-    (both directions); the persistent loop forms it in-kernel, the per-step
-    path by a column sum of dG."""
+    (both directions); the persistent loop forms it in-kernel (per-slice
+    partials, summed by ocrk_slab_sum -- appended to `defer` as (fn, tensors)
+    when given), the per-step path by a column sum of dG."""
     _chk(wh, seq_len, dout, cprev, acts, dbias)
     dtype = dout.dtype
     dev = dout.device
@@ -367,7 +388,7 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None):
              ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd", B, H, dev)), ptr(part), ptr(ws), nb,
              _stream(dout))
         if dbias is not None:
-            colsum(part, B // 32, 2 * 4 * H, dbias)
+            _bias_parts(part, B // 32, 2 * 4 * H, dbias, defer)
         return dG
     dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
     dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)
@@ -425,7 +446,7 @@ def gru_fwd(gx, whgT, whcT, seq_len, T, B, H, dtype):
     return out, hprev, rh_t, acts
 
 
-def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=None):
+def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=None, defer=None):
     """Returns dG_t [T,B,2,3H] = (dz_r, dz_u, dz_c) per direction. dbias (f32
     [2*3H], accumulated): the layer's [gates | candidate] bias gradients, formed
     in the persistent loop (else a column sum of dG)."""
@@ -441,7 +462,7 @@ def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=None):
              ptr(dG), ptr(status_word(dev)), ptr(persistent_flags("gru_bwd", B, H, dev)), ptr(part), ptr(ws), nb,
              _stream(dout))
         if dbias is not None:
-            colsum(part, B // 32, 2 * 3 * H, dbias)
+            _bias_parts(part, B // 32, 2 * 3 * H, dbias, defer)
         return dG
     dzg = torch.empty(2, B, 2 * H, dtype=dtype, device=dev)
     dzc = torch.empty(2, B, H, dtype=dtype, device=dev)
@@ -488,6 +509,22 @@ def strided_copy(src, rows, cols, in_rs, in_cs, out, out_rs, out_cs, out_offset=
 def ctypes_offset(t, elems):
     import ctypes
     return ctypes.c_void_p(t.data_ptr() + elems * t.element_size())
+
+
+def slab_sum(slab, nslab, nc, ld, out, accumulate=True):
+    """out[:nc] (+)= the column sums of slab [nslab][ld] f32 (fixed order, double accumulation)."""
+    _chk(slab, out)
+    nb = _lib.lib().ocrk_slab_sum_workspace_size(nc)
+    ws = _ws(nb, slab.device)
+    call("ocrk_slab_sum", ptr(slab), int(nslab), int(nc), int(ld), ptr(out), int(accumulate), ptr(ws), nb,
+         _stream(slab))
+
+
+def _bias_parts(part, rows, nc, dbias, defer):
+    if defer is None:
+        slab_sum(part, rows, nc, nc, dbias)
+    else:
+        defer.append((lambda: slab_sum(part, rows, nc, nc, dbias), (part,)))
 
 
 def colsum(x, M, N, out, accumulate=True):

@@ -145,6 +145,12 @@ size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin);
 int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
                           void* dx, const void* relu_mask, float* dbias, int accumulate, void* ws,
                           size_t ws_bytes, int dtype, void* stream);
+/* The same with the bias-gradient reduction left to the caller (e.g. on a side
+ * stream, off the data-gradient critical path): slab [ocrk_conv_stats_tiles(B*H*W)]
+ * [2*cin] f32 gets the per-tile column (sum, M2) of the masked dx; then
+ * ocrk_slab_sum(slab, tiles, cin, 2*cin, dbias, ...) = ocrk_conv3x3_bwd_data's dbias. */
+int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
+                               void* dx, const void* relu_mask, float* slab, int dtype, void* stream);
 /* dw f32 HWIO [3][3][cin][cout] (+)= im2col(x)^T . dy (split-K). */
 size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin, int cout);
 int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, int cin, int cout,
@@ -174,6 +180,15 @@ int ocrk_bn_relu_pool_bwd(const void* z, const void* dp, int B, int H, int W, in
                           const float* invstd, const float* gamma, const float* beta, int kh, int kw,
                           int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
                           float* dbias, int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
+/* The same with the conv-bias reduction left to the caller: bias_slab f32
+ * [ocrk_bn_bwd_bias_slab_rows(...)][C] gets the apply pass's per-block column sums
+ * of dz; ocrk_slab_sum(bias_slab, rows, C, C, dbias, ...) = the dbias above. */
+size_t ocrk_bn_bwd_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw);
+int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta, int kh, int kw,
+                               int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
+                               int accumulate, float* bias_slab, void* ws, size_t ws_bytes, int dtype,
+                               void* stream);
 
 /* ------------------------------------------------------------- recurrent
  * a7' -- rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199), both
@@ -320,6 +335,12 @@ int ocrk_strided_copy(const float* in, int64_t rows, int64_t cols, int64_t in_rs
 size_t ocrk_colsum_workspace_size(int64_t M, int N);
 int ocrk_colsum(const void* in, int64_t M, int N, int dtype, float* out, int accumulate, void* ws,
                 size_t ws_bytes, void* stream);
+/* out [nc] f32 (+)= the column sums of a [nslab][ld] f32 slab of partial rows, in
+ * a fixed order with double accumulation (deterministic): the reduction step
+ * of the *_slab entry points and of the persistent loops' dbias_part. */
+size_t ocrk_slab_sum_workspace_size(int nc);
+int ocrk_slab_sum(const float* slab, int nslab, int nc, int ld, float* out, int accumulate, void* ws,
+                  size_t ws_bytes, void* stream);
 /* out = (y > 0) ? dy * scale : 0 (ReLU backward of the logits, model.py:216) */
 int ocrk_relu_mask(const float* dy, const float* y, int64_t n, float scale, void* out, int out_dtype,
                    void* stream);

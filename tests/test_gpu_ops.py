@@ -147,6 +147,60 @@ def test_bn_relu_pool(cuda, pool, W):
     np.testing.assert_allclose(db.cpu().numpy(), db_ref, rtol=1e-4, atol=1e-5)
 
 
+# The *_slab entry points (bias reduction left to the caller, e.g. on the side
+# stream) give the same dx / dz and, after ocrk_slab_sum, the same dbias bits
+# as the fused entry points; bf16 at a conv-tower shape (direct and GEMM routes).
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 30, 60), (64, 128, 7, 126), (128, 256, 3, 125)])
+def test_deferred_bias_reductions_match(cuda, cin, cout, H, W):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device=cuda).manual_seed(cin + cout)
+    B = 8
+    dy = torch.randn(B, H, W, cout, device=cuda, generator=g).bfloat16()
+    w_bwd = (torch.randn(cin, 9 * cout, device=cuda, generator=g) / 30).bfloat16()
+    mask = torch.randn(B, H, W, cin, device=cuda, generator=g).bfloat16()
+    d1 = torch.full((cin,), 0.5, device=cuda)
+    d2 = d1.clone()
+    dx1 = Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask, dbias=d1)
+    late = []
+    dx2 = Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask, dbias=d2, defer=late)
+    assert len(late) == 1 and torch.equal(d2, torch.full_like(d2, 0.5))
+    late.pop()[0]()
+    assert torch.equal(dx1, dx2) and torch.equal(d1, d2)
+    for pool in [(2, 2, 2, 2), (2, 2, 2, 1), (3, 1, 3, 1)]:
+        Hz = 3 if pool[0] == 3 else H
+        z = torch.randn(B, Hz, W, cin, device=cuda, generator=g).bfloat16()
+        kh, kw, sh, sw = pool
+        tm = pool == (3, 1, 3, 1)
+        Ho, Wo = (Hz - kh) // sh + 1, (W - kw) // sw + 1
+        dp = torch.randn(*((Wo, B, cin) if tm else (B, Ho, Wo, cin)), device=cuda, generator=g).bfloat16()
+        mean = torch.randn(cin, device=cuda, generator=g) * 0.1
+        inv = torch.rand(cin, device=cuda, generator=g) + 0.5
+        gamma = torch.randn(cin, device=cuda, generator=g)
+        beta = torch.randn(cin, device=cuda, generator=g)
+        outs = []
+        for defer in (None, []):
+            dg, db, dbias = torch.zeros(cin, device=cuda), torch.zeros(cin, device=cuda), torch.ones(cin, device=cuda)
+            dz = Kn.bn_relu_pool_bwd(z, dp, mean, inv, gamma, beta, pool, tm, dg, db, dbias=dbias, defer=defer)
+            if defer is not None:
+                assert len(defer) == 1
+                defer.pop()[0]()
+            outs.append((dz, dg, db, dbias))
+        for u, v in zip(*outs):
+            assert torch.equal(u, v), pool
+
+
+def test_slab_sum_matches_colsum_order(cuda):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    x = torch.randn(8, 4096, device=cuda)
+    out = torch.full((4096,), 2.0, device=cuda)
+    Kn.slab_sum(x, 8, 4096, 4096, out)
+    np.testing.assert_allclose(out.cpu().numpy(), x.double().sum(0).cpu().numpy() + 2.0, rtol=0, atol=1e-5)
+    strided = torch.randn(100, 96, device=cuda)
+    out2 = torch.zeros(40, device=cuda)
+    Kn.slab_sum(strided, 100, 40, 96, out2, accumulate=False)
+    np.testing.assert_allclose(out2.cpu().numpy(), strided[:, :40].double().sum(0).cpu().numpy(), rtol=0, atol=1e-5)
+
+
 # column sums (bias gradients of the odd convs, recurrent and logits layers)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N", [(37, 64), (5000, 24), (3001, 4096), (20000, 256)])
