@@ -299,6 +299,9 @@ int conv_direct_bwd_data(const void* dy, int B, int H, int W, int cout, const vo
 size_t conv_direct_wgrad_ws_bytes(int B, int H, int W, int cin, int cout);
 int conv_direct_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw,
                       int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
+size_t conv_rows_wgrad_ws_bytes(int B);
+int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
+                    void* ws, size_t ws_bytes, hipStream_t s);
 }
 
 extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,
@@ -386,8 +389,10 @@ static int wgrad_splits(int64_t M, int cin, int cout) {
 
 extern "C" size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin, int cout) {
     int64_t M = (int64_t)B * H * W;
-    return std::max(ocrk::gemm_splitk_ws_bytes(9 * cin, cout, 1, wgrad_splits(M, cin, cout)),
-                    ocrk::conv_direct_wgrad_ws_bytes(B, H, W, cin, cout));
+    size_t ws = std::max(ocrk::gemm_splitk_ws_bytes(9 * cin, cout, 1, wgrad_splits(M, cin, cout)),
+                         ocrk::conv_direct_wgrad_ws_bytes(B, H, W, cin, cout));
+    if (cin == 32 && cout == 32) ws = std::max(ws, ocrk::conv_rows_wgrad_ws_bytes(B));
+    return ws;
 }
 
 extern "C" int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, int cin,
@@ -406,8 +411,9 @@ extern "C" int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int
                  "ocrk_conv3x3_bwd_weight: workspace too small");
     p.convH = H; p.convW = W; p.convC = cin;
     if (dtype == OCRK_BF16) {
-        const int st = ocrk::conv_direct_wgrad(x, dy, B, H, W, cin, cout, dw, accumulate, ws, ws_bytes,
-                                               ocrk::as_stream(stream));
+        int st = ocrk::conv_rows_wgrad(x, dy, B, H, W, cin, cout, dw, accumulate, ws, ws_bytes, ocrk::as_stream(stream));
+        if (st >= 0) return st;
+        st = ocrk::conv_direct_wgrad(x, dy, B, H, W, cin, cout, dw, accumulate, ws, ws_bytes, ocrk::as_stream(stream));
         if (st >= 0) return st;
     }
     return ocrk::gemm(p, ocrk::A_IM2COL_T, ocrk::B_KN, dtype, ocrk::as_stream(stream));

@@ -1,0 +1,229 @@
+// a1 backward: the weight gradient of conv2 (3x3 'same', 32 -> 32 channels at
+// 30 x 254, src/weinman/model.py:84-109 backward) by walking image ROWS.
+//
+//   dW[kh][kw][ci][co] = sum_{b,h,w} x[b][h+kh-1][w+kw-1][ci] * dy[b][h][w][co]
+//
+// Why rows: the chunked direct kernel (conv_direct.hip) stages, per 128-pixel
+// chunk of the flat pixel index, three tap rows of x (3 x 130 pixels) plus the
+// chunk's dy by LDS-DMA -- every x byte is staged three times, and the per-chunk
+// DMA issue, wait and barrier dominate (137 us for 36 GFLOP / 250 MB). Here a
+// workgroup owns whole images and walks their rows: output row h needs x rows
+// h-1, h, h+1 (a 4-slot LDS ring, each x row loaded ONCE and used by three
+// output rows) and dy row h (2-slot ring). The next rows are loaded into
+// registers while the current row multiplies and written to the ring after it.
+//
+// MFMA mapping (16x16x32 bf16, f32 accumulate): per output row and tap
+// (kh, kw), C[ci][co] += A[ci][w] . B[w][co] over the row's pixels w (K = 256:
+// the 254 pixels + 2 zero columns), A = x row h+kh-1 shifted by kw-1 pixels.
+// Both ring images are [pixel][channel] (channels contiguous, the NHWC rows
+// as loaded), i.e. k-major, and the fragments come out of them with
+// ds_read_b64_tr_b16 (frag_tr, the TN engine's reads): a kw shift is a shift
+// of the k-row. A zero pixel on each side of every x row is the 'same'
+// padding along w; an x row outside the image skips its three taps.
+// Wave q multiplies the k-steps {2q, 2q+1} (pixels 64q .. 64q+63) for all 9
+// taps: 9 x 2 x 2 accumulator tiles (144 VGPRs) held across all rows; at the
+// end the 4 waves' partials are added in wave order in LDS and the workgroup
+// writes one [9][32][32] f32 slab row; the split-K reduce sums the slab rows
+// in a fixed order (deterministic).
+#include <type_traits>
+
+#include "common.h"
+#include "gemm.h"
+#include "mfma_util.h"
+
+namespace ocrk {
+
+namespace {
+
+constexpr int RW_CI = 32, RW_CO = 32;
+constexpr int RW_ROWB = RW_CI * 2;                 // 64 B per pixel (ci or co)
+constexpr int RW_XROWS = 258;                      // pixels -1 .. 256 of an x row
+constexpr int RW_DROWS = 256;                      // pixels 0 .. 255 of a dy row
+constexpr int RW_XSLOT = RW_XROWS * RW_ROWB;       // 16.1 KB
+constexpr int RW_DSLOT = RW_DROWS * RW_ROWB;       // 16 KB
+constexpr int RW_XOFF = 0, RW_DOFF = 4 * RW_XSLOT;
+constexpr int RW_RING = RW_DOFF + 2 * RW_DSLOT;    // 96.5 KB
+constexpr int RW_PART = 9 * RW_CI * RW_CO;         // floats per partial
+constexpr int RW_LDS = 4 * RW_PART * 4 > RW_RING ? 4 * RW_PART * 4 : RW_RING;   // 144 KB (end: wave partials)
+constexpr int RW_MAXW = 254;
+
+// LDS byte offset of 16-B chunk c of image row r (4 chunks per row, XOR-swizzled
+// by (r >> 2) & 3 as the TN engine's 64-B rows, so a transposed read's 16 k-rows spread)
+__device__ __forceinline__ int rw_off(int r, int c) { return r * RW_ROWB + ((c ^ ((r >> 2) & 3)) << 4); }
+
+__global__ void __launch_bounds__(256, 1)
+conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
+                          int B, int H, int W) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int kr0 = 4 * g + (i16 >> 2);            // k-row of this lane's transposed read
+    const int mq = 4 * (i16 & 3);                   // channel offset within a 16-wide tile
+
+    // zero both rings once: the pad pixels (x rows 0 and W+1.., dy rows W..255) stay zero
+    for (int i = tid; i < RW_RING / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    floatx4 acc[9][2][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[t][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // a row = W pixels x 4 chunks <= 1016 chunks: 4 per thread. Two register
+    // sets: the rows written to the ring at the end of step h were loaded during
+    // step h-1, so a whole step of MFMAs covers their latency.
+    constexpr int PER = 4;
+    u32x4 sx[2][PER], sd[2][PER];
+    // every lane loads (lanes past the row re-read its last chunk, never stored):
+    // branch-free loads keep a fixed count in flight, so the compiler's waits
+    // before the ring stores are counted (vmcnt(N)) instead of vmcnt(0)
+    const int qmax = W * 4 - 1;
+    auto load_row = [&](const bf16* base, u32x4 (&v)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = min(tid + 256 * i, qmax);
+            v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)q * 8);
+        }
+    };
+    auto store_row = [&](int slot_off, int rshift, const u32x4 (&v)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = tid + 256 * i;
+            if (q < W * 4) {
+                const int px = q >> 2, c = q & 3;
+                *reinterpret_cast<u32x4*>(smem + slot_off + rw_off(px + rshift, c)) = v[i];
+            }
+        }
+    };
+    auto xslot = [&](int row) { return RW_XOFF + (row & 3) * RW_XSLOT; };
+    auto dslot = [&](int row) { return RW_DOFF + (row & 1) * RW_DSLOT; };
+
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+        const bf16* xb = x + (size_t)b * H * W * RW_CI;
+        const bf16* db = dy + (size_t)b * H * W * RW_CO;
+        auto xrow = [&](int r) { return xb + (size_t)r * W * RW_CI; };
+        auto drow = [&](int r) { return db + (size_t)r * W * RW_CO; };
+        __syncthreads();                            // the previous image's last reads are done
+        // prologue: x rows 0, 1 and dy row 0 into the ring; x row 2 / dy row 1 into set 0
+        load_row(xrow(0), sx[1]);
+        load_row(drow(0), sd[1]);
+        store_row(xslot(0), 1, sx[1]);
+        store_row(dslot(0), 0, sd[1]);
+        if (H > 1) {
+            load_row(xrow(1), sx[1]);
+            store_row(xslot(1), 1, sx[1]);
+            load_row(drow(1), sd[0]);
+        }
+        if (H > 2) load_row(xrow(2), sx[0]);
+        // step h: rows h-1..h+1 of x and row h of dy are in the ring; set P holds
+        // x row h+2 / dy row h+1 (loaded during step h-1); set 1-P receives x row
+        // h+3 / dy row h+2 now
+        auto step = [&](int h, auto P_) {
+            constexpr int P = decltype(P_)::value;
+            __syncthreads();
+            // unconditional (a clamped row past the image): a fixed count of loads in
+            // flight lets the stores below wait for the older set only
+            load_row(xrow(min(h + 3, H - 1)), sx[1 - P]);
+            load_row(drow(min(h + 2, H - 1)), sd[1 - P]);
+            const char* dsl = smem + dslot(h);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int r = (2 * wave + kk) * 32 + kr0;      // dy k-row (pixel); the second read at r + 16
+                bf16x8 bfr[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int n = 16 * j + mq;
+                    bfr[j] = frag_tr(reinterpret_cast<const unsigned short*>(dsl + rw_off(r, n >> 3) + (n & 7) * 2),
+                                     16 * RW_CO);
+                }
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    const int hr = h + kh - 1;
+                    if (hr < 0 || hr >= H) continue;           // wave-uniform
+                    const char* xsl = smem + xslot(hr);
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const int rx = r + kw;                 // x pixel w + kw - 1 at image row w + kw
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) {
+                            const int m = 16 * i + mq;
+                            const bf16x8 af = frag_tr(
+                                reinterpret_cast<const unsigned short*>(xsl + rw_off(rx, m >> 3) + (m & 7) * 2),
+                                16 * RW_CI);
+#pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                acc[kh * 3 + kw][i][j] =
+                                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[kh * 3 + kw][i][j], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+            // rows h+2 / h+1 into the slots nobody reads this step (x row h-2's, dy row h-1's)
+            if (h + 2 < H) store_row(xslot(h + 2), 1, sx[P]);
+            if (h + 1 < H) store_row(dslot(h + 1), 0, sd[P]);
+        };
+        for (int h = 0; h < H; h += 2) {
+            step(h, std::integral_constant<int, 0>{});
+            if (h + 1 < H) step(h + 1, std::integral_constant<int, 1>{});
+        }
+    }
+
+    // the four waves' partials, added in wave order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem) + wave * RW_PART;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ci = 16 * i + 4 * g + e, co = 16 * j + i16;
+                    red[(t * RW_CI + ci) * RW_CO + co] = acc[t][i][j][e];
+                }
+    __syncthreads();
+    const float* r0 = reinterpret_cast<const float*>(smem);
+    float* out = part + (size_t)blockIdx.x * RW_PART;
+    for (int o = tid * 4; o < RW_PART; o += 256 * 4) {
+        f32x4 s = *reinterpret_cast<const f32x4*>(r0 + o);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) s += *reinterpret_cast<const f32x4*>(r0 + q * RW_PART + o);
+        *reinterpret_cast<f32x4*>(out + o) = s;
+    }
+}
+
+}  // namespace
+
+// OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
+static bool rows_enabled() {
+    const char* e = getenv("OCRK_CONV_ROWS");
+    return !(e && e[0] == '0');
+}
+
+size_t conv_rows_wgrad_ws_bytes(int B) {
+    return (size_t)std::min(B, std::max(cu_count(), 1)) * RW_PART * sizeof(float);
+}
+
+// -1 when the shape is not conv2's (Cin = Cout = 32, W <= 254) or the path is off
+int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
+                    void* ws, size_t ws_bytes, hipStream_t s) {
+    if (!rows_enabled() || cin != RW_CI || cout != RW_CO || W > RW_MAXW || W < 1 || H < 1 || B < 1) return -1;
+    if (ws_bytes < conv_rows_wgrad_ws_bytes(B) || (uintptr_t)ws % 16 != 0) return -1;
+    const int grid = std::min(B, std::max(cu_count(), 1));
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel), RW_LDS);
+    conv3x3_wgrad_rows_kernel<<<grid, 256, RW_LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);
+    int st = launch_status("conv3x3_wgrad_rows");
+    if (st) return st;
+    GemmParams p = {};
+    p.M = 9 * cin; p.N = cout; p.K = B * H * W; p.batch = 1;
+    p.C = dw; p.ldc = cout; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+    p.splits = grid; p.splitk_ws = (float*)ws;
+    return splitk_finish(p, s);
+}
+
+}  // namespace ocrk

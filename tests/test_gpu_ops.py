@@ -303,3 +303,25 @@ def test_gemm_weight_grad_form_bf16(cuda):
             ldc=G4, splits=4)
     ref = C0 + x.float().numpy().astype(np.float64).T @ dG.float().numpy()[:, G4:].astype(np.float64)
     assert _rel(out.cpu().numpy(), ref) < 1e-5
+
+
+# conv2's weight gradient by image rows (conv_rows.hip) against the chunked
+# direct kernel and a float64 reference, at the bench's 30 x 254 rows
+def test_conv2_wgrad_rows_matches(cuda, monkeypatch):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device=cuda).manual_seed(5)
+    B, H, W, C = 6, 30, 254, 32
+    x = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+    dy = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2).transpose(0, 1),
+                                     dy.double().permute(0, 3, 1, 2).transpose(0, 1), padding=1)  # [ci][co][3][3]
+    ref = ref.permute(2, 3, 0, 1).contiguous()                                                # HWIO
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+        dw = torch.full((3, 3, C, C), 0.5, device=cuda)
+        Kn.conv3x3_bwd_weight(x, dy, dw, accumulate=True)
+        outs.append(dw.double() - 0.5)
+    for o in outs:
+        torch.testing.assert_close(o, ref, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-3)
