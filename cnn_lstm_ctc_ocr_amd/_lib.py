@@ -58,6 +58,9 @@ SIGNATURES = {
     "ocrk_conv3x3_bwd_weight": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_bn_finalize_workspace_size": [_i32, _i32],
     "ocrk_bn_finalize": [_p, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_bn_finalize_tiles": [_p, _i32, _i32, _i64, _i32, _f32, _f32, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_conv3x3_fwd_rowstats_supported": [_i32, _i32, _i32, _i32, _i32],
+    "ocrk_conv3x3_fwd_rowstats": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _p, _p],
     "ocrk_bn_infer_params": [_p, _p, _i32, _f32, _p, _p, _p],
     "ocrk_bn_relu_pool_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
                               _p, _i32, _i32, _p],

@@ -509,16 +509,29 @@ extern "C" size_t ocrk_bn_finalize_workspace_size(int tiles, int C) {
     return (size_t)std::min(BN_PARTS, std::max(1, tiles)) * 3 * C * sizeof(double);
 }
 
+extern "C" int ocrk_bn_finalize_tiles(const float* stats, int tiles, int tile_rows, int64_t M, int C, float eps,
+                                      float momentum, float* mean, float* invstd, float* moving_mean,
+                                      float* moving_var, void* ws, size_t ws_bytes, void* stream);
+
 extern "C" int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
                                 float* mean, float* invstd, float* moving_mean, float* moving_var, void* ws,
                                 size_t ws_bytes, void* stream) {
-    OCRK_REQUIRE(tiles >= 1 && C >= 1 && C <= 256 && M >= 1, "ocrk_bn_finalize: bad sizes");
+    return ocrk_bn_finalize_tiles(stats, tiles, 128, M, C, eps, momentum, mean, invstd, moving_mean, moving_var, ws,
+                                  ws_bytes, stream);
+}
+
+extern "C" int ocrk_bn_finalize_tiles(const float* stats, int tiles, int tile_rows, int64_t M, int C, float eps,
+                                      float momentum, float* mean, float* invstd, float* moving_mean,
+                                      float* moving_var, void* ws, size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(tiles >= 1 && C >= 1 && C <= 256 && M >= 1 && tile_rows >= 1 &&
+                 (int64_t)(tiles - 1) * tile_rows < M && (int64_t)tiles * tile_rows >= M,
+                 "ocrk_bn_finalize: bad sizes");
     OCRK_REQUIRE(ws && ws_bytes >= ocrk_bn_finalize_workspace_size(tiles, C), "ocrk_bn_finalize: workspace too small");
     hipStream_t s = ocrk::as_stream(stream);
     const int np0 = std::min(BN_PARTS, tiles);
     const int rpb = (tiles + np0 - 1) / np0;
     const int np = (tiles + rpb - 1) / rpb;
-    bn_stats_partial_kernel<<<np, 256, 0, s>>>(stats, tiles, M, 128, C, rpb, (double*)ws);
+    bn_stats_partial_kernel<<<np, 256, 0, s>>>(stats, tiles, M, tile_rows, C, rpb, (double*)ws);
     int st = ocrk::launch_status("ocrk_bn_finalize partial sums");
     if (st) return st;
     bn_finalize_kernel<<<C, 256, 0, s>>>((const double*)ws, np, M, C, eps, momentum, mean, invstd, moving_mean,

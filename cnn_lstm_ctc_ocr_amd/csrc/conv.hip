@@ -300,6 +300,11 @@ size_t conv_direct_wgrad_ws_bytes(int B, int H, int W, int cin, int cout);
 int conv_direct_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw,
                       int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
 size_t conv_rows_wgrad_ws_bytes(int B);
+bool conv_rows_fwd_covers(int B, int H, int W, int cin, int cout);
+int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout, void* y,
+                  int relu, float* stats, hipStream_t s);
+int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                    const void* relu_mask, const float* stats, hipStream_t s);
 int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, hipStream_t s);
 }
@@ -315,10 +320,25 @@ extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, con
     p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
     p.convH = H; p.convW = W; p.convC = cin;
     if (dtype == OCRK_BF16 && y_dtype == OCRK_BF16) {
-        const int st = ocrk::conv_direct_fwd(x, B, H, W, cin, w_nk, bias, cout, y, relu, stats, ocrk::as_stream(stream));
+        int st = stats ? -1 : ocrk::conv_rows_fwd(x, B, H, W, cin, w_nk, bias, cout, y, relu, nullptr, ocrk::as_stream(stream));
+        if (st >= 0) return st;
+        st = ocrk::conv_direct_fwd(x, B, H, W, cin, w_nk, bias, cout, y, relu, stats, ocrk::as_stream(stream));
         if (st >= 0) return st;
     }
     return ocrk::gemm(p, ocrk::A_IM2COL, ocrk::B_NK, dtype, ocrk::as_stream(stream));
+}
+
+// The forward with the BatchNorm partials per OUTPUT ROW (conv2's shape on the
+// row-walking kernel): stats [B*H][2][cout], finalized with tile_rows = W.
+extern "C" int ocrk_conv3x3_fwd_rowstats_supported(int B, int H, int W, int cin, int cout) {
+    return ocrk::conv_rows_fwd_covers(B, H, W, cin, cout) ? 1 : 0;
+}
+
+extern "C" int ocrk_conv3x3_fwd_rowstats(const void* x, int B, int H, int W, int cin, const void* w_nk,
+                                         const float* bias, int cout, void* y, int relu, float* stats, void* stream) {
+    OCRK_REQUIRE(stats && ocrk::conv_rows_fwd_covers(B, H, W, cin, cout),
+                 "ocrk_conv3x3_fwd_rowstats: shape B=%d H=%d W=%d %d->%d not covered", B, H, W, cin, cout);
+    return ocrk::conv_rows_fwd(x, B, H, W, cin, w_nk, bias, cout, y, relu, stats, ocrk::as_stream(stream));
 }
 
 // Optional fused bias gradient of the producing (odd) conv: the GEMM's
@@ -338,7 +358,8 @@ static int bwd_data_run(const void* dy, int B, int H, int W, int cout, const voi
     p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
     p.convH = H; p.convW = W; p.convC = cout;
     p.stats = stats;
-    int st = dtype == OCRK_BF16 ? ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s) : -1;
+    int st = dtype == OCRK_BF16 ? ocrk::conv_rows_dgrad(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s) : -1;
+    if (st < 0 && dtype == OCRK_BF16) st = ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s);
     if (st < 0) st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
     return st;
 }

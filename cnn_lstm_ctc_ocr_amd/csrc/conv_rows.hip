@@ -51,6 +51,13 @@ constexpr int RW_MAXW = 254;
 // by (r >> 2) & 3 as the TN engine's 64-B rows, so a transposed read's 16 k-rows spread)
 __device__ __forceinline__ int rw_off(int r, int c) { return r * RW_ROWB + ((c ^ ((r >> 2) & 3)) << 4); }
 
+// workgroup barrier over LDS traffic only (the row prefetch loads stay in flight)
+__device__ __forceinline__ void rw_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __global__ void __launch_bounds__(256, 1)
 conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
                           int B, int H, int W) {
@@ -196,6 +203,345 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
     }
 }
 
+// Backward-data of conv2 by rows: dx[h][w][ci] = (y1[h][w][ci] > 0) *
+//   sum_{kh,kw,co} dy[h+1-kh][w+1-kw][co] . Wb[ci][kh][kw][co]
+// (w_bwd image [cin][3][3][cout], the mirrored taps of ocrk_conv3x3_bwd_data).
+// A workgroup owns a band of output rows of one image and walks it: dy rows
+// h-1 .. h+1 sit in a 4-slot LDS ring ([pixel][co], one zero pixel each side),
+// each loaded once (the next one into registers a step ahead). The weights are
+// the MFMA A operand, resident in VGPRs (9 taps x 2 ci tiles); the dy pixels
+// the B operand (ds_read_b128 of 8 co of one pixel), so a lane ends up with 4
+// consecutive ci of one pixel: the ReLU mask is one 8-B load and dx one 8-B
+// store. Wave q covers pixels 64q .. 64q+63 of each row (4 x 2 tiles x 9 taps).
+constexpr int RD_BANDS = 2;                        // row bands per image: 2 workgroups per CU
+constexpr int RD_LDS = 4 * RW_XSLOT;               // 64.5 KB
+
+__global__ void __launch_bounds__(256, 2)
+conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb, const bf16* __restrict__ mask,
+                          bf16* __restrict__ dx, int B, int H, int W) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x / RD_BANDS, band = blockIdx.x - b * RD_BANDS;
+    const int rows = (H + RD_BANDS - 1) / RD_BANDS;
+    const int h0 = band * rows, h1 = min(H, h0 + rows);
+    if (h0 >= h1) return;
+
+    for (int i = tid; i < RD_LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    // resident A fragments: ci tile i, tap t -> w_bwd[16 i + i16][t][8 g .. 8 g + 7]
+    bf16x8 wa[9][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            wa[t][i] = *reinterpret_cast<const bf16x8*>(wb + ((size_t)(16 * i + i16) * 9 + t) * RW_CO + 8 * g);
+
+    constexpr int PER = 4;
+    const int qmax = W * 4 - 1;
+    u32x4 sd[2][PER];
+    const bf16* dyb = dy + (size_t)b * H * W * RW_CO;
+    auto drow = [&](int r) { return dyb + (size_t)r * W * RW_CO; };
+    auto load_row = [&](const bf16* base, u32x4 (&v)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = min(tid + 256 * i, qmax);
+            v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)q * 8);
+        }
+    };
+    auto store_row = [&](int row, const u32x4 (&v)[PER]) {
+        char* slot = smem + (row & 3) * RW_XSLOT;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = tid + 256 * i;
+            if (q < W * 4) *reinterpret_cast<u32x4*>(slot + rw_off((q >> 2) + 1, q & 3)) = v[i];
+        }
+    };
+    auto zero_row = [&](int row) {                   // a dy row outside the image
+        char* slot = smem + (row & 3) * RW_XSLOT;
+        for (int i = tid; i < RW_XSLOT / 16; i += 256) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+    };
+    __syncthreads();
+    // prologue: dy rows h0-1, h0, h0+1 into the ring (zero rows past the image), h0+2 into set 0
+    for (int r = h0 - 1; r <= h0 + 1; ++r) {
+        if (r < 0 || r >= H) {
+            zero_row(r);
+        } else {
+            load_row(drow(r), sd[1]);
+            store_row(r, sd[1]);
+        }
+    }
+    load_row(drow(min(h0 + 2, H - 1)), sd[0]);
+
+    auto step = [&](int h, auto P_) {
+        constexpr int P = decltype(P_)::value;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        load_row(drow(min(h + 3, H - 1)), sd[1 - P]);
+        // the ReLU mask of this row's outputs, in flight during the MFMAs
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 mk[4][2];
+        const bf16* mrow = mask + ((size_t)b * H + h) * W * RW_CI;
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int px = min(64 * wave + 16 * n + i16, W - 1);
+                mk[n][i] = *reinterpret_cast<const u32x2*>(mrow + (size_t)px * RW_CI + 16 * i + 4 * g);
+            }
+        floatx4 acc[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) acc[n][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const char* slot = smem + ((h + 1 - kh) & 3) * RW_XSLOT;   // zero rows past the image
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    // output pixel w = 64 q + 16 n + i16 reads dy pixel w + 1 - kw = image row w + 2 - kw
+                    const int r = 64 * wave + 16 * n + i16 + 2 - kw;
+                    const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rw_off(r, g));
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        acc[n][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][i], bf, acc[n][i], 0, 0, 0);
+                }
+            }
+        }
+        // lane: ci 16 i + 4 g .. +3 of pixel 64 q + 16 n + i16
+        bf16* orow = dx + ((size_t)b * H + h) * W * RW_CI;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int px = 64 * wave + 16 * n + i16;
+            if (px >= W) continue;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                u32x2 o;
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2) {
+                    const unsigned m = mk[n][i][e2];
+                    const float v0 = __uint_as_float(m << 16) > 0.f ? acc[n][i][2 * e2] : 0.f;
+                    const float v1 = __uint_as_float(m & 0xffff0000u) > 0.f ? acc[n][i][2 * e2 + 1] : 0.f;
+                    o[e2] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v0) |
+                            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v1) << 16);
+                }
+                *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CI + 16 * i + 4 * g) = o;
+            }
+        }
+        // dy row h+2 into the slot of row h-2 (or zeros past the image)
+        if (h + 2 < H) store_row(h + 2, sd[P]);
+        else if (h + 2 == H) zero_row(h + 2);
+    };
+    for (int h = h0; h < h1; h += 2) {
+        step(h, std::integral_constant<int, 0>{});
+        if (h + 1 < h1) step(h + 1, std::integral_constant<int, 1>{});
+    }
+}
+
+// Forward of conv2 by rows: z[h][w][co] = bias[co] + sum_{kh,kw,ci}
+// x[h+kh-1][w+kw-1][ci] . Wn[co][kh][kw][ci] (w_nk image), optional ReLU, and
+// the BatchNorm partial statistics of each OUTPUT ROW (tile = one image row of
+// W pixels: [B*H][2][cout] (sum, M2 about the row mean), finalized with
+// tile_rows = W). Same ring / band walk as the backward-data kernel above,
+// with x rows in the ring and the w_nk fragments resident.
+__global__ void __launch_bounds__(256, 2)
+conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
+                        bf16* __restrict__ y, float* __restrict__ stats, int relu, int B, int H, int W) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float s_red[2][4][RW_CO];           // [sum | M2][wave][channel]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x / RD_BANDS, band = blockIdx.x - b * RD_BANDS;
+    const int rows = (H + RD_BANDS - 1) / RD_BANDS;
+    const int h0 = band * rows, h1 = min(H, h0 + rows);
+    if (h0 >= h1) return;
+
+    for (int i = tid; i < RD_LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    // resident A fragments: co tile j, tap t -> w_nk[16 j + i16][t][8 g .. 8 g + 7]
+    bf16x8 wa[9][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            wa[t][j] = *reinterpret_cast<const bf16x8*>(wn + ((size_t)(16 * j + i16) * 9 + t) * RW_CI + 8 * g);
+    float bco[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bco[j][e] = bias ? bias[16 * j + 4 * g + e] : 0.f;
+
+    constexpr int PER = 4;
+    const int qmax = W * 4 - 1;
+    u32x4 sd[2][PER];
+    const bf16* xb = x + (size_t)b * H * W * RW_CI;
+    auto xrow = [&](int r) { return xb + (size_t)r * W * RW_CI; };
+    auto load_row = [&](const bf16* base, u32x4 (&v)[PER]) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = min(tid + 256 * i, qmax);
+            v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)q * 8);
+        }
+    };
+    auto store_row = [&](int row, const u32x4 (&v)[PER]) {
+        char* slot = smem + (row & 3) * RW_XSLOT;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int q = tid + 256 * i;
+            if (q < W * 4) *reinterpret_cast<u32x4*>(slot + rw_off((q >> 2) + 1, q & 3)) = v[i];
+        }
+    };
+    auto zero_row = [&](int row) {
+        char* slot = smem + (row & 3) * RW_XSLOT;
+        for (int i = tid; i < RW_XSLOT / 16; i += 256) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+    };
+    __syncthreads();
+    for (int r = h0 - 1; r <= h0 + 1; ++r) {
+        if (r < 0 || r >= H) {
+            zero_row(r);
+        } else {
+            load_row(xrow(r), sd[1]);
+            store_row(r, sd[1]);
+        }
+    }
+    load_row(xrow(min(h0 + 2, H - 1)), sd[0]);
+    const float inv_w = 1.f / (float)W;
+
+    auto step = [&](int h, auto P_) {
+        constexpr int P = decltype(P_)::value;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        load_row(xrow(min(h + 3, H - 1)), sd[1 - P]);
+        floatx4 acc[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[n][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const char* slot = smem + ((h + kh - 1) & 3) * RW_XSLOT;   // zero rows past the image
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    // output pixel w = 64 q + 16 n + i16 reads x pixel w + kw - 1 = image row w + kw
+                    const int r = 64 * wave + 16 * n + i16 + kw;
+                    const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rw_off(r, g));
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][j], bf, acc[n][j], 0, 0, 0);
+                }
+            }
+        }
+        // lane: co 16 j + 4 g .. +3 of pixel 64 q + 16 n + i16
+        float sum[2][4] = {};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const bool in = 64 * wave + 16 * n + i16 < W;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = acc[n][j][e] + bco[j][e];
+                    if (relu) v = fmaxf(v, 0.f);
+                    acc[n][j][e] = v;
+                    if (in) sum[j][e] += v;
+                }
+        }
+        bf16* orow = y + ((size_t)b * H + h) * W * RW_CO;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int px = 64 * wave + 16 * n + i16;
+            if (px >= W) continue;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                u32x2 o;
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2)
+                    o[e2] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][j][2 * e2]) |
+                            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][j][2 * e2 + 1]) << 16);
+                *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CO + 16 * j + 4 * g) = o;
+            }
+        }
+        if (stats) {
+            // the row's (sum, M2): lanes of a 16-lane row share channels -> DPP row sums,
+            // waves in wave order through LDS; M2 about the row mean in a second pass
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = sum[j][e];
+                    v += dpp_row<0x128>(v);
+                    v += dpp_row<0x124>(v);
+                    v += dpp_row<0x122>(v);
+                    v += dpp_row<0x121>(v);
+                    sum[j][e] = v;
+                }
+            if (i16 == 0)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s_red[0][wave][16 * j + 4 * g + e] = sum[j][e];
+            rw_barrier();
+            float mean[2][4], q2[2][4];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int c = 16 * j + 4 * g + e;
+                    mean[j][e] = (((s_red[0][0][c] + s_red[0][1][c]) + s_red[0][2][c]) + s_red[0][3][c]) * inv_w;
+                    q2[j][e] = 0.f;
+                }
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const bool in = 64 * wave + 16 * n + i16 < W;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = acc[n][j][e] - mean[j][e];
+                        if (in) q2[j][e] += d * d;
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = q2[j][e];
+                    v += dpp_row<0x128>(v);
+                    v += dpp_row<0x124>(v);
+                    v += dpp_row<0x122>(v);
+                    v += dpp_row<0x121>(v);
+                    q2[j][e] = v;
+                }
+            if (i16 == 0)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s_red[1][wave][16 * j + 4 * g + e] = q2[j][e];
+            rw_barrier();
+            if (tid < 2 * RW_CO) {
+                const int k = tid / RW_CO, c = tid - k * RW_CO;
+                stats[((size_t)b * H + h) * 2 * RW_CO + tid] =
+                    ((s_red[k][0][c] + s_red[k][1][c]) + s_red[k][2][c]) + s_red[k][3][c];
+            }
+        }
+        if (h + 2 < H) store_row(h + 2, sd[P]);
+        else if (h + 2 == H) zero_row(h + 2);
+    };
+    for (int h = h0; h < h1; h += 2) {
+        step(h, std::integral_constant<int, 0>{});
+        if (h + 1 < h1) step(h + 1, std::integral_constant<int, 1>{});
+    }
+}
+
 }  // namespace
 
 // OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
@@ -206,6 +552,33 @@ static bool rows_enabled() {
 
 size_t conv_rows_wgrad_ws_bytes(int B) {
     return (size_t)std::min(B, std::max(cu_count(), 1)) * RW_PART * sizeof(float);
+}
+
+// forward with per-row BatchNorm partials (stats [B*H][2][32], tile_rows = W), conv2's shape only
+bool conv_rows_fwd_covers(int B, int H, int W, int cin, int cout) {
+    return rows_enabled() && cin == RW_CI && cout == RW_CO && W <= RW_MAXW && W >= 1 && H >= 1 && B >= 1;
+}
+
+int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout, void* y,
+                  int relu, float* stats, hipStream_t s) {
+    if (!conv_rows_fwd_covers(B, H, W, cin, cout)) return -1;
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_kernel), RD_LDS);
+    conv3x3_fwd_rows_kernel<<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats,
+                                                              relu, B, H, W);
+    return launch_status("conv3x3_fwd_rows");
+}
+
+// backward-data with the producer's ReLU mask, conv2's shape only (-1 otherwise)
+int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                    const void* relu_mask, const float* stats, hipStream_t s) {
+    if (!rows_enabled() || cin != RW_CI || cout != RW_CO || W > RW_MAXW || W < 1 || H < 1 || B < 1) return -1;
+    if (!relu_mask || stats) return -1;
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel), RD_LDS);
+    conv3x3_dgrad_rows_kernel<<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)dy, (const bf16*)w_bwd,
+                                                                (const bf16*)relu_mask, (bf16*)dx, B, H, W);
+    return launch_status("conv3x3_dgrad_rows");
 }
 
 // -1 when the shape is not conv2's (Cin = Cout = 32, W <= 254) or the path is off

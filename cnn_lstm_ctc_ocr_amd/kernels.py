@@ -134,16 +134,40 @@ def conv3x3_bwd_weight(x, dy, dw, accumulate=True):
 
 
 # -------------------------------------------------------------- batch norm
-def bn_finalize(stats, M, C, eps, momentum, moving_mean=None, moving_var=None):
+def bn_finalize(stats, M, C, eps, momentum, moving_mean=None, moving_var=None, tile_rows=128):
+    """Batch mean / invstd (and the moving averages) from per-tile (sum, M2)
+    partials of `tile_rows` rows each (128: the GEMM epilogues; W: the conv2
+    row kernel, conv3x3_fwd_rowstats)."""
     _chk(stats, moving_mean, moving_var)
     tiles = stats.shape[0]
     mean = torch.empty(C, dtype=torch.float32, device=stats.device)
     invstd = torch.empty_like(mean)
     nb = _lib.lib().ocrk_bn_finalize_workspace_size(tiles, C)
     ws = _ws(nb, stats.device)
-    call("ocrk_bn_finalize", ptr(stats), tiles, M, C, float(eps), float(momentum), ptr(mean), ptr(invstd),
-         ptr(moving_mean), ptr(moving_var), ptr(ws), nb, _stream(stats))
+    call("ocrk_bn_finalize_tiles", ptr(stats), tiles, int(tile_rows), M, C, float(eps), float(momentum), ptr(mean),
+         ptr(invstd), ptr(moving_mean), ptr(moving_var), ptr(ws), nb, _stream(stats))
     return mean, invstd
+
+
+def conv3x3_fwd_rowstats_ok(x, cout):
+    """Does the conv2 row kernel take this forward (bf16, Cin = Cout = 32, W <= 254)?"""
+    if x.dtype != torch.bfloat16 or not x.is_cuda:
+        return False
+    B, H, W, cin = x.shape
+    return bool(_lib.lib().ocrk_conv3x3_fwd_rowstats_supported(B, H, W, cin, cout))
+
+
+def conv3x3_fwd_rowstats(x, w_nk, bias, relu=False):
+    """(y, stats [B*H, 2, Cout]): the forward with BatchNorm partials per output
+    row (finalize with tile_rows = W)."""
+    _chk(x, w_nk, bias)
+    B, H, W, cin = x.shape
+    cout = w_nk.shape[0]
+    y = torch.empty(B, H, W, cout, dtype=x.dtype, device=x.device)
+    stats = torch.empty(B * H, 2, cout, dtype=torch.float32, device=x.device)
+    call("ocrk_conv3x3_fwd_rowstats", ptr(x), B, H, W, cin, ptr(w_nk), ptr(bias), cout, ptr(y), int(relu),
+         ptr(stats), _stream(x))
+    return y, stats
 
 
 def bn_infer_params(moving_mean, moving_var, eps):

@@ -75,11 +75,17 @@ class _ConvBlock(torch.autograd.Function):
         w_nk, _ = store.conv_images(even, dt)
         C = w_nk.shape[0]
         if training:
-            stats = torch.empty(K.conv_stats_tiles(M), 2, C, dtype=torch.float32, device=x.device)
-            z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False, stats=stats)
+            if K.conv3x3_fwd_rowstats_ok(y_odd, C):
+                # conv2 on the row-walking kernel: BN partials per output row
+                z, stats = K.conv3x3_fwd_rowstats(y_odd, w_nk, P[pe + "/bias"])
+                trows = W
+            else:
+                stats = torch.empty(K.conv_stats_tiles(M), 2, C, dtype=torch.float32, device=x.device)
+                z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False, stats=stats)
+                trows = 128
             mean, invstd = K.bn_finalize(stats, M, C, BN_EPS, BN_MOMENTUM,
                                          store.stats[pe + "/batch_norm/moving_mean"],
-                                         store.stats[pe + "/batch_norm/moving_variance"])
+                                         store.stats[pe + "/batch_norm/moving_variance"], tile_rows=trows)
         else:
             z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False)
             mean, invstd = K.bn_infer_params(store.stats[pe + "/batch_norm/moving_mean"],

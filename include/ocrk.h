@@ -133,6 +133,12 @@ int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int
  * [ocrk_conv_stats_tiles(B*H*W)][2][cout] per-tile (sum, M2) of the output,
  * the BatchNorm statistics input of ocrk_bn_finalize. */
 size_t ocrk_conv_stats_tiles(int64_t M);
+/* conv2's forward on the row-walking kernel (conv_rows.hip: Cin = Cout = 32, W <= 254,
+ * bf16): stats [B*H][2][cout] = (sum, M2) of each OUTPUT ROW of W pixels, for
+ * ocrk_bn_finalize_tiles(..., tile_rows = W, ...). The same z bits as ocrk_conv3x3_fwd. */
+int ocrk_conv3x3_fwd_rowstats_supported(int B, int H, int W, int cin, int cout);
+int ocrk_conv3x3_fwd_rowstats(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias,
+                              int cout, void* y, int relu, float* stats, void* stream);
 int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias,
                      int cout, void* y, int y_dtype, int relu, float* stats, int dtype, void* stream);
 /* dx [B,H,W,cin] = conv3x3 backward-data of dy [B,H,W,cout] with w_bwd
@@ -161,6 +167,10 @@ int ocrk_conv3x3_bwd_weight(const void* x, const void* dy, int B, int H, int W, 
  * epilogue partials (mean, 1/sqrt(var+eps)) and the [TF1] moving averages
  * (moving_mean/var may be NULL = no update). bn_infer_params: INFER mode. */
 size_t ocrk_bn_finalize_workspace_size(int tiles, int C);
+/* ocrk_bn_finalize for partials of tile_rows rows per tile (the last may be short) */
+int ocrk_bn_finalize_tiles(const float* stats, int tiles, int tile_rows, int64_t M, int C, float eps,
+                           float momentum, float* mean, float* invstd, float* moving_mean, float* moving_var,
+                           void* ws, size_t ws_bytes, void* stream);
 int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
                      float* mean, float* invstd, float* moving_mean, float* moving_var, void* ws, size_t ws_bytes,
                      void* stream);   /* ws: ocrk_bn_finalize_workspace_size bytes (row-range partial sums) */

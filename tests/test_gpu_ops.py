@@ -325,3 +325,57 @@ def test_conv2_wgrad_rows_matches(cuda, monkeypatch):
     for o in outs:
         torch.testing.assert_close(o, ref, rtol=1e-4, atol=2e-3)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-3)
+
+
+# conv2's data gradient by image rows (conv_rows.hip) against the chunked direct
+# kernel (same bits: same products, same k order per output) and float64
+def test_conv2_dgrad_rows_matches(cuda, monkeypatch):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device=cuda).manual_seed(7)
+    for B, H, W in [(4, 30, 254), (3, 7, 37), (2, 1, 5)]:
+        C = 32
+        dy = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(3, 3, C, C, device=cuda, generator=g) / 17).bfloat16()          # HWIO
+        w_bwd = w.permute(2, 0, 1, 3).contiguous().view(C, 9 * C)                          # [ci][kh][kw][co]
+        mask = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+        ref = torch.nn.functional.conv_transpose2d(dy.double().permute(0, 3, 1, 2),
+                                                   w.double().permute(2, 3, 0, 1).transpose(0, 1), padding=1)
+        ref = ref.permute(0, 2, 3, 1) * (mask.double() > 0)
+        outs = []
+        for mode in ("1", "0"):
+            monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+            outs.append(Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask))
+        torch.testing.assert_close(outs[0].double(), ref, rtol=2e-2, atol=2e-2)
+        assert torch.equal(outs[0], outs[1]), (B, H, W)
+
+
+# conv2's forward by image rows: the same z bits as the chunked direct kernel,
+# BatchNorm mean / invstd from the per-row partials within float tolerance
+def test_conv2_fwd_rowstats_matches(cuda, monkeypatch):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device=cuda).manual_seed(9)
+    for B, H, W in [(4, 30, 254), (3, 7, 37), (2, 1, 5)]:
+        C = 32
+        x = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+        w_nk = (torch.randn(C, 9 * C, device=cuda, generator=g) / 17).bfloat16()
+        bias = torch.randn(C, device=cuda, generator=g)
+        assert Kn.conv3x3_fwd_rowstats_ok(x, C)
+        z, st = Kn.conv3x3_fwd_rowstats(x, w_nk, bias)
+        M = B * H * W
+        monkeypatch.setenv("OCRK_CONV_ROWS", "0")
+        st_ref = torch.empty(Kn.conv_stats_tiles(M), 2, C, device=cuda)
+        z_ref = Kn.conv3x3_fwd(x, w_nk, bias, relu=False, stats=st_ref)
+        monkeypatch.delenv("OCRK_CONV_ROWS")
+        assert torch.equal(z, z_ref), (B, H, W)
+        m1, i1 = Kn.bn_finalize(st, M, C, 1e-3, 0.99, tile_rows=W)
+        m2, i2 = Kn.bn_finalize(st_ref, M, C, 1e-3, 0.99)
+        zf = z.double().view(-1, C)
+        # the partials are of the f32 values before the bf16 rounding of z: against z
+        # only to bf16 rounding (the tight check is the 128-tile path below)
+        tol = 8e-3 * float(zf.abs().max())
+        torch.testing.assert_close(m1.double(), zf.mean(0), rtol=0, atol=tol)
+        torch.testing.assert_close(i1.double(), 1 / torch.sqrt(zf.var(0, unbiased=False) + 1e-3), rtol=2e-2, atol=0)
+        torch.testing.assert_close(m1, m2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(i1, i2, rtol=1e-5, atol=1e-6)
+        # no-statistics forward (serving) takes the row kernel too: same bits
+        assert torch.equal(Kn.conv3x3_fwd(x, w_nk, bias, relu=True), torch.relu(z_ref.float()).bfloat16())
