@@ -299,7 +299,7 @@ int conv_direct_bwd_data(const void* dy, int B, int H, int W, int cout, const vo
 size_t conv_direct_wgrad_ws_bytes(int B, int H, int W, int cin, int cout);
 int conv_direct_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw,
                       int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
-size_t conv_rows_wgrad_ws_bytes(int B);
+size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout);
 bool conv_rows_fwd_covers(int B, int H, int W, int cin, int cout);
 int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout, void* y,
                   int relu, float* stats, hipStream_t s);
@@ -412,7 +412,8 @@ extern "C" size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin
     int64_t M = (int64_t)B * H * W;
     size_t ws = std::max(ocrk::gemm_splitk_ws_bytes(9 * cin, cout, 1, wgrad_splits(M, cin, cout)),
                          ocrk::conv_direct_wgrad_ws_bytes(B, H, W, cin, cout));
-    if (cin == 32 && cout == 32) ws = std::max(ws, ocrk::conv_rows_wgrad_ws_bytes(B));
+    if ((cin == 32 && cout == 32) || (cout == 64 && (cin == 32 || cin == 64)))
+        ws = std::max(ws, ocrk::conv_rows_wgrad_ws_bytes(B, cin, cout));
     return ws;
 }
 

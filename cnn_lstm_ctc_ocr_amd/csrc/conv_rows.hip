@@ -542,6 +542,144 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
     }
 }
 
+// The weight gradient by rows for Cout = 64 (conv3: 32 -> 64, conv4: 64 -> 64 at
+// 15 x 127): the same ring walk, but wave q owns output channels 16q .. 16q+15
+// over the WHOLE row (K = KPX pixels, KPX/32 k-steps), so no cross-wave sum:
+// acc [9 taps][CI/16 tiles] (18 / 36 f32x4). x rows are CI*2 bytes, dy rows 128 B,
+// 16-B chunks XOR-swizzled per row as in the TN engine (rows of >= 8 chunks by
+// r mod 8, of 4 chunks by (r >> 2) mod 4).
+template <int CPR>
+__device__ __forceinline__ int rc_off(int r, int c) {
+    constexpr int SWM = CPR >= 8 ? 7 : 3;
+    const int sw = CPR >= 8 ? (r & SWM) : ((r >> 2) & SWM);
+    return r * CPR * 16 + ((c ^ sw) << 4);
+}
+
+template <int CI, int KPX>
+struct RcCfg {
+    static constexpr int CO = 64;
+    static constexpr int XCPR = CI / 8, DCPR = CO / 8;       // 16-B chunks per pixel
+    static constexpr int XSLOT = (KPX + 2) * CI * 2, DSLOT = KPX * CO * 2;
+    static constexpr int DOFF = 4 * XSLOT;
+    static constexpr int LDS = DOFF + 2 * DSLOT;
+    static constexpr int XPER = (KPX * XCPR + 255) / 256, DPER = (KPX * DCPR + 255) / 256;   // chunks per thread
+    static constexpr int PART = 9 * CI * CO;
+};
+
+template <int CI, int KPX>
+__global__ void __launch_bounds__(256, 1)
+conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
+                             int B, int H, int W) {
+    using C = RcCfg<CI, KPX>;
+    constexpr int CO = C::CO, TI = CI / 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int kr0 = 4 * g + (i16 >> 2);
+    const int mq = 4 * (i16 & 3);
+
+    for (int i = tid; i < C::LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    floatx4 acc[9][TI];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int xq = W * C::XCPR - 1, dq = W * C::DCPR - 1;
+    u32x4 sx[2][C::XPER], sd[2][C::DPER];
+    auto load_x = [&](const bf16* base, u32x4 (&v)[C::XPER]) {
+#pragma unroll
+        for (int i = 0; i < C::XPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + 256 * i, xq) * 8);
+    };
+    auto load_d = [&](const bf16* base, u32x4 (&v)[C::DPER]) {
+#pragma unroll
+        for (int i = 0; i < C::DPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + 256 * i, dq) * 8);
+    };
+    auto store_x = [&](int row, const u32x4 (&v)[C::XPER]) {
+        char* slot = smem + (row & 3) * C::XSLOT;
+#pragma unroll
+        for (int i = 0; i < C::XPER; ++i) {
+            const int q = tid + 256 * i;
+            if (q <= xq) *reinterpret_cast<u32x4*>(slot + rc_off<C::XCPR>(q / C::XCPR + 1, q % C::XCPR)) = v[i];
+        }
+    };
+    auto store_d = [&](int row, const u32x4 (&v)[C::DPER]) {
+        char* slot = smem + C::DOFF + (row & 1) * C::DSLOT;
+#pragma unroll
+        for (int i = 0; i < C::DPER; ++i) {
+            const int q = tid + 256 * i;
+            if (q <= dq) *reinterpret_cast<u32x4*>(slot + rc_off<C::DCPR>(q / C::DCPR, q % C::DCPR)) = v[i];
+        }
+    };
+
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+        const bf16* xb = x + (size_t)b * H * W * CI;
+        const bf16* db = dy + (size_t)b * H * W * CO;
+        auto xrow = [&](int r) { return xb + (size_t)r * W * CI; };
+        auto drow = [&](int r) { return db + (size_t)r * W * CO; };
+        __syncthreads();
+        load_x(xrow(0), sx[1]);
+        load_d(drow(0), sd[1]);
+        store_x(0, sx[1]);
+        store_d(0, sd[1]);
+        if (H > 1) {
+            load_x(xrow(1), sx[1]);
+            store_x(1, sx[1]);
+            load_d(drow(1), sd[0]);
+        }
+        if (H > 2) load_x(xrow(2), sx[0]);
+        auto step = [&](int h, auto P_) {
+            constexpr int P = decltype(P_)::value;
+            rw_barrier();
+            load_x(xrow(min(h + 3, H - 1)), sx[1 - P]);
+            load_d(drow(min(h + 2, H - 1)), sd[1 - P]);
+            const char* dsl = smem + C::DOFF + (h & 1) * C::DSLOT;
+#pragma unroll
+            for (int kk = 0; kk < KPX / 32; ++kk) {
+                const int r = kk * 32 + kr0;
+                const int n = 16 * wave + mq;
+                const bf16x8 bfr = frag_tr(
+                    reinterpret_cast<const unsigned short*>(dsl + rc_off<C::DCPR>(r, n >> 3) + (n & 7) * 2), 16 * CO);
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    const int hr = h + kh - 1;
+                    if (hr < 0 || hr >= H) continue;
+                    const char* xsl = smem + (hr & 3) * C::XSLOT;
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+                        for (int i = 0; i < TI; ++i) {
+                            const int m = 16 * i + mq;
+                            const bf16x8 af = frag_tr(reinterpret_cast<const unsigned short*>(
+                                                          xsl + rc_off<C::XCPR>(r + kw, m >> 3) + (m & 7) * 2),
+                                                      16 * CI);
+                            acc[kh * 3 + kw][i] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[kh * 3 + kw][i], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+            if (h + 2 < H) store_x(h + 2, sx[P]);
+            if (h + 1 < H) store_d(h + 1, sd[P]);
+        };
+        for (int h = 0; h < H; h += 2) {
+            step(h, std::integral_constant<int, 0>{});
+            if (h + 1 < H) step(h + 1, std::integral_constant<int, 1>{});
+        }
+    }
+    // this wave's 16 output channels of the [9][CI][64] partial
+    float* out = part + (size_t)blockIdx.x * C::PART;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                out[(t * CI + 16 * i + 4 * g + e) * CO + 16 * wave + i16] = acc[t][i][e];
+}
+
 }  // namespace
 
 // OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
@@ -550,8 +688,8 @@ static bool rows_enabled() {
     return !(e && e[0] == '0');
 }
 
-size_t conv_rows_wgrad_ws_bytes(int B) {
-    return (size_t)std::min(B, std::max(cu_count(), 1)) * RW_PART * sizeof(float);
+size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
+    return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
 }
 
 // forward with per-row BatchNorm partials (stats [B*H][2][32], tile_rows = W), conv2's shape only
@@ -581,11 +719,34 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
     return launch_status("conv3x3_dgrad_rows");
 }
 
+template <int CI, int KPX>
+static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, float* dw, int accumulate, void* ws,
+                          hipStream_t s) {
+    using C = RcCfg<CI, KPX>;
+    const int grid = std::min(B, std::max(cu_count(), 1));
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX>), C::LDS);
+    conv3x3_wgrad_rows_co_kernel<CI, KPX><<<grid, 256, C::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);
+    int st = launch_status("conv3x3_wgrad_rows_co");
+    if (st) return st;
+    GemmParams p = {};
+    p.M = 9 * CI; p.N = C::CO; p.K = B * H * W; p.batch = 1;
+    p.C = dw; p.ldc = C::CO; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+    p.splits = grid; p.splitk_ws = (float*)ws;
+    return splitk_finish(p, s);
+}
+
 // -1 when the shape is not conv2's (Cin = Cout = 32, W <= 254) or the path is off
 int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, hipStream_t s) {
-    if (!rows_enabled() || cin != RW_CI || cout != RW_CO || W > RW_MAXW || W < 1 || H < 1 || B < 1) return -1;
-    if (ws_bytes < conv_rows_wgrad_ws_bytes(B) || (uintptr_t)ws % 16 != 0) return -1;
+    if (!rows_enabled() || W < 1 || H < 1 || B < 1) return -1;
+    if (ws_bytes < conv_rows_wgrad_ws_bytes(B, cin, cout) || (uintptr_t)ws % 16 != 0) return -1;
+    if (cout == 64 && W <= 128) {                    // conv3 / conv4
+        if (cin == 32) return launch_rows_co<32, 128>(x, dy, B, H, W, dw, accumulate, ws, s);
+        if (cin == 64) return launch_rows_co<64, 128>(x, dy, B, H, W, dw, accumulate, ws, s);
+        return -1;
+    }
+    if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel), RW_LDS);

@@ -307,19 +307,20 @@ def test_gemm_weight_grad_form_bf16(cuda):
 
 # conv2's weight gradient by image rows (conv_rows.hip) against the chunked
 # direct kernel and a float64 reference, at the bench's 30 x 254 rows
-def test_conv2_wgrad_rows_matches(cuda, monkeypatch):
+@pytest.mark.parametrize("B,H,W,C,CO", [(6, 30, 254, 32, 32), (5, 15, 127, 32, 64), (5, 15, 127, 64, 64),
+                                        (3, 4, 9, 64, 64)])
+def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(5)
-    B, H, W, C = 6, 30, 254, 32
     x = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
-    dy = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
+    dy = torch.randn(B, H, W, CO, device=cuda, generator=g).bfloat16()
     ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2).transpose(0, 1),
                                      dy.double().permute(0, 3, 1, 2).transpose(0, 1), padding=1)  # [ci][co][3][3]
     ref = ref.permute(2, 3, 0, 1).contiguous()                                                # HWIO
     outs = []
     for mode in ("1", "0"):
         monkeypatch.setenv("OCRK_CONV_ROWS", mode)
-        dw = torch.full((3, 3, C, C), 0.5, device=cuda)
+        dw = torch.full((3, 3, C, CO), 0.5, device=cuda)
         Kn.conv3x3_bwd_weight(x, dy, dw, accumulate=True)
         outs.append(dw.double() - 0.5)
     for o in outs:
