@@ -680,6 +680,175 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
                 out[(t * CI + 16 * i + 4 * g + e) * CO + 16 * wave + i16] = acc[t][i][e];
 }
 
+// Generic forward by rows for the wider layers (conv3-conv6, W <= KPX):
+// NW waves, wave w owns output channels 16w .. 16w+15 (CO = 16 NW) with its
+// 9 x CI/32 weight fragments resident (the MFMA A operand); every wave runs
+// over all KPX/16 pixel tiles of the row, B fragments from the x ring (one
+// ds_read_b128 = 8 ci of one pixel). Per-row BatchNorm partials are wave-local
+// (a wave owns its channels): DPP row sums over the 16 pixels of a tile, the
+// tiles in order, M2 about the row mean in a second pass.
+template <int CI, int CO, int KPX>
+struct RfCfg {
+    static constexpr int NW = CO / 16, NT = NW * 64, KS = CI / 32, PT = KPX / 16;
+    static constexpr int CPR = CI / 8;
+    static constexpr int XSLOT = (KPX + 2) * CI * 2;
+    static constexpr int LDS = 4 * XSLOT;
+    static constexpr int PER = (KPX * CPR + NT - 1) / NT;
+    static constexpr int PER_CU = LDS <= 80 * 1024 && NW <= 4 ? 2 : 1;
+    static constexpr int BANDS = PER_CU;
+};
+
+template <int CI, int CO, int KPX>
+__global__ void __launch_bounds__((RfCfg<CI, CO, KPX>::NT), (RfCfg<CI, CO, KPX>::PER_CU))
+conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
+                           bf16* __restrict__ y, float* __restrict__ stats, int relu, int B, int H, int W) {
+    using C = RfCfg<CI, CO, KPX>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x / C::BANDS, band = blockIdx.x - b * C::BANDS;
+    const int rows = (H + C::BANDS - 1) / C::BANDS;
+    const int h0 = band * rows, h1 = min(H, h0 + rows);
+    if (h0 >= h1) return;
+    for (int i = tid; i < C::LDS / 16; i += C::NT) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    bf16x8 wa[9][C::KS];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int k = 0; k < C::KS; ++k)
+            wa[t][k] = *reinterpret_cast<const bf16x8*>(wn + ((size_t)(16 * wave + i16) * 9 + t) * CI + 32 * k + 8 * g);
+    float bco[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bco[e] = bias ? bias[16 * wave + 4 * g + e] : 0.f;
+
+    const int qmax = W * C::CPR - 1;
+    u32x4 sx[2][C::PER];
+    const bf16* xb = x + (size_t)b * H * W * CI;
+    auto xrow = [&](int r) { return xb + (size_t)r * W * CI; };
+    auto load_row = [&](const bf16* base, u32x4 (&v)[C::PER]) {
+#pragma unroll
+        for (int i = 0; i < C::PER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + C::NT * i, qmax) * 8);
+    };
+    auto store_row = [&](int row, const u32x4 (&v)[C::PER]) {
+        char* slot = smem + (row & 3) * C::XSLOT;
+#pragma unroll
+        for (int i = 0; i < C::PER; ++i) {
+            const int q = tid + C::NT * i;
+            if (q <= qmax) *reinterpret_cast<u32x4*>(slot + rc_off<C::CPR>(q / C::CPR + 1, q % C::CPR)) = v[i];
+        }
+    };
+    auto zero_row = [&](int row) {
+        char* slot = smem + (row & 3) * C::XSLOT;
+        for (int i = tid; i < C::XSLOT / 16; i += C::NT) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+    };
+    __syncthreads();
+    for (int r = h0 - 1; r <= h0 + 1; ++r) {
+        if (r < 0 || r >= H) {
+            zero_row(r);
+        } else {
+            load_row(xrow(r), sx[1]);
+            store_row(r, sx[1]);
+        }
+    }
+    load_row(xrow(min(h0 + 2, H - 1)), sx[0]);
+    const float inv_w = 1.f / (float)W;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+    auto step = [&](int h, auto P_) {
+        constexpr int P = decltype(P_)::value;
+        rw_barrier();
+        load_row(xrow(min(h + 3, H - 1)), sx[1 - P]);
+        floatx4 acc[C::PT];
+#pragma unroll
+        for (int n = 0; n < C::PT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const char* slot = smem + ((h + kh - 1) & 3) * C::XSLOT;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                for (int k = 0; k < C::KS; ++k)
+#pragma unroll
+                    for (int n = 0; n < C::PT; ++n) {
+                        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rc_off<C::CPR>(16 * n + i16 + kw, 4 * k + g));
+                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][k], bf, acc[n], 0, 0, 0);
+                    }
+        }
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        bf16* orow = y + ((size_t)b * H + h) * W * CO;
+#pragma unroll
+        for (int n = 0; n < C::PT; ++n) {
+            const int px = 16 * n + i16;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[n][e] + bco[e];
+                if (relu) v = fmaxf(v, 0.f);
+                acc[n][e] = v;
+                if (px < W) sum[e] += v;
+            }
+            if (px < W) {
+                u32x2 o;
+                o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][0]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][1]) << 16);
+                o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][2]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][3]) << 16);
+                *reinterpret_cast<u32x2*>(orow + (size_t)px * CO + 16 * wave + 4 * g) = o;
+            }
+        }
+        if (stats) {
+            float q2[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = sum[e];
+                v += dpp_row<0x128>(v);
+                v += dpp_row<0x124>(v);
+                v += dpp_row<0x122>(v);
+                v += dpp_row<0x121>(v);
+                sum[e] = v;
+                const float mean = v * inv_w;
+                float q = 0.f;
+#pragma unroll
+                for (int n = 0; n < C::PT; ++n) {
+                    const float d = acc[n][e] - mean;
+                    if (16 * n + i16 < W) q += d * d;
+                }
+                q += dpp_row<0x128>(q);
+                q += dpp_row<0x124>(q);
+                q += dpp_row<0x122>(q);
+                q += dpp_row<0x121>(q);
+                q2[e] = q;
+            }
+            if (i16 == 0) {
+                float* st = stats + ((size_t)b * H + h) * 2 * CO + 16 * wave + 4 * g;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    st[e] = sum[e];
+                    st[CO + e] = q2[e];
+                }
+            }
+        }
+        if (h + 2 < H) store_row(h + 2, sx[P]);
+        else if (h + 2 == H) zero_row(h + 2);
+    };
+    for (int h = h0; h < h1; h += 2) {
+        step(h, std::integral_constant<int, 0>{});
+        if (h + 1 < h1) step(h + 1, std::integral_constant<int, 1>{});
+    }
+}
+
+template <int CI, int CO, int KPX>
+static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, const float* bias, void* y, int relu,
+                         float* stats, hipStream_t s) {
+    using C = RfCfg<CI, CO, KPX>;
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX>), C::LDS);
+    conv3x3_fwd_rows_co_kernel<CI, CO, KPX><<<B * C::BANDS, C::NT, C::LDS, s>>>(
+        (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, relu, B, H, W);
+    return launch_status("conv3x3_fwd_rows_co");
+}
+
 }  // namespace
 
 // OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
@@ -692,14 +861,31 @@ size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
     return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
 }
 
-// forward with per-row BatchNorm partials (stats [B*H][2][32], tile_rows = W), conv2's shape only
+// OCRK_CONV_ROWS_WIDE=0: the wider layers (conv3-conv6) stay on the GEMM / direct engines
+static bool rows_wide_enabled() {
+    const char* e = getenv("OCRK_CONV_ROWS_WIDE");
+    return !(e && e[0] == '0');
+}
+
+static bool rows_fwd_wide(int cin, int cout) {
+    return (cin == 32 && cout == 64) || (cin == 64 && cout == 64) || (cin == 64 && cout == 128);
+}
+
+// forward with per-row BatchNorm partials (stats [B*H][2][cout], tile_rows = W)
 bool conv_rows_fwd_covers(int B, int H, int W, int cin, int cout) {
-    return rows_enabled() && cin == RW_CI && cout == RW_CO && W <= RW_MAXW && W >= 1 && H >= 1 && B >= 1;
+    if (!rows_enabled() || W < 1 || H < 1 || B < 1) return false;
+    if (cin == RW_CI && cout == RW_CO) return W <= RW_MAXW;
+    return rows_wide_enabled() && rows_fwd_wide(cin, cout) && W <= 128;
 }
 
 int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout, void* y,
                   int relu, float* stats, hipStream_t s) {
     if (!conv_rows_fwd_covers(B, H, W, cin, cout)) return -1;
+    if (cin != RW_CI || cout != RW_CO) {
+        if (cin == 32) return launch_fwd_co<32, 64, 128>(x, B, H, W, w_nk, bias, y, relu, stats, s);
+        if (cout == 64) return launch_fwd_co<64, 64, 128>(x, B, H, W, w_nk, bias, y, relu, stats, s);
+        return launch_fwd_co<64, 128, 128>(x, B, H, W, w_nk, bias, y, relu, stats, s);
+    }
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_kernel), RD_LDS);
     conv3x3_fwd_rows_kernel<<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats,

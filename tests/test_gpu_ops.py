@@ -352,13 +352,17 @@ def test_conv2_dgrad_rows_matches(cuda, monkeypatch):
 
 # conv2's forward by image rows: the same z bits as the chunked direct kernel,
 # BatchNorm mean / invstd from the per-row partials within float tolerance
-def test_conv2_fwd_rowstats_matches(cuda, monkeypatch):
+@pytest.mark.parametrize("CI,CO,shapes", [(32, 32, [(4, 30, 254), (3, 7, 37), (2, 1, 5)]),
+                                          (32, 64, [(4, 15, 127), (2, 3, 20)]),
+                                          (64, 64, [(4, 15, 127), (2, 2, 9)]),
+                                          (64, 128, [(4, 7, 126), (2, 5, 17)])])
+def test_conv2_fwd_rowstats_matches(cuda, monkeypatch, CI, CO, shapes):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(9)
-    for B, H, W in [(4, 30, 254), (3, 7, 37), (2, 1, 5)]:
-        C = 32
-        x = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
-        w_nk = (torch.randn(C, 9 * C, device=cuda, generator=g) / 17).bfloat16()
+    for B, H, W in shapes:
+        C = CO
+        x = torch.randn(B, H, W, CI, device=cuda, generator=g).bfloat16()
+        w_nk = (torch.randn(C, 9 * CI, device=cuda, generator=g) / 17).bfloat16()
         bias = torch.randn(C, device=cuda, generator=g)
         assert Kn.conv3x3_fwd_rowstats_ok(x, C)
         z, st = Kn.conv3x3_fwd_rowstats(x, w_nk, bias)
