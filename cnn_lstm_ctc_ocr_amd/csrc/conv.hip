@@ -304,7 +304,7 @@ bool conv_rows_fwd_covers(int B, int H, int W, int cin, int cout);
 int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout, void* y,
                   int relu, float* stats, hipStream_t s);
 int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
-                    const void* relu_mask, const float* stats, hipStream_t s);
+                    const void* relu_mask, float* stats, hipStream_t s);
 int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, hipStream_t s);
 }

@@ -849,6 +849,179 @@ static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, c
     return launch_status("conv3x3_fwd_rows_co");
 }
 
+// Generic backward-data by rows (routed for conv4's 64 <- 64; conv5's 64 <- 128
+// measured slower here at one workgroup per CU: 78 vs 68 us): dx[h][w][ci] =
+// mask * sum_{kh,kw,co} dy[h+1-kh][w+1-kw][co] . Wb[ci][kh][kw][co]. NW = CI/16
+// waves, wave w owns input channels 16w .. 16w+15 with its 9 x CO/32 w_bwd
+// fragments resident; dy rows in the 4-slot ring. With `stats` (the bias
+// gradient of the producing layer) each workgroup writes the column sums of
+// its masked dx as ONE row of the [tiles][2][CI] table (sums in the first CI)
+// and the rows past the grid are zeroed, so summing every table row gives
+// the same total as the 128-pixel tiles of the GEMM path.
+template <int CI, int CO, int KPX>
+struct RbCfg {
+    static constexpr int NW = CI / 16, NT = NW * 64, KS = CO / 32, PT = KPX / 16;
+    static constexpr int CPR = CO / 8;
+    static constexpr int XSLOT = (KPX + 2) * CO * 2;
+    static constexpr int LDS = 4 * XSLOT;
+    static constexpr int PER = (KPX * CPR + NT - 1) / NT;
+    static constexpr int PER_CU = LDS <= 80 * 1024 && NW <= 4 ? 2 : 1;
+    static constexpr int BANDS = PER_CU;
+};
+
+template <int CI, int CO, int KPX>
+__global__ void __launch_bounds__((RbCfg<CI, CO, KPX>::NT), (RbCfg<CI, CO, KPX>::PER_CU))
+conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb,
+                             const bf16* __restrict__ mask, bf16* __restrict__ dx, float* __restrict__ stats,
+                             int stat_rows, int B, int H, int W) {
+    using C = RbCfg<CI, CO, KPX>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x / C::BANDS, band = blockIdx.x - b * C::BANDS;
+    const int rows = (H + C::BANDS - 1) / C::BANDS;
+    const int h0 = band * rows, h1 = min(H, h0 + rows);
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    if (stats)                                     // table rows past the grid: zero
+        for (int r = gridDim.x + blockIdx.x; r < stat_rows; r += gridDim.x)
+            for (int i = tid; i < 2 * CI; i += C::NT) stats[(size_t)r * 2 * CI + i] = 0.f;
+    if (h0 < h1) {
+        for (int i = tid; i < C::LDS / 16; i += C::NT) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+        bf16x8 wa[9][C::KS];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int k = 0; k < C::KS; ++k)
+                wa[t][k] = *reinterpret_cast<const bf16x8*>(wb + ((size_t)(16 * wave + i16) * 9 + t) * CO + 32 * k + 8 * g);
+        const int qmax = W * C::CPR - 1;
+        u32x4 sx[2][C::PER];
+        const bf16* db = dy + (size_t)b * H * W * CO;
+        auto drow = [&](int r) { return db + (size_t)r * W * CO; };
+        auto load_row = [&](const bf16* base, u32x4 (&v)[C::PER]) {
+#pragma unroll
+            for (int i = 0; i < C::PER; ++i)
+                v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + C::NT * i, qmax) * 8);
+        };
+        auto store_row = [&](int row, const u32x4 (&v)[C::PER]) {
+            char* slot = smem + (row & 3) * C::XSLOT;
+#pragma unroll
+            for (int i = 0; i < C::PER; ++i) {
+                const int q = tid + C::NT * i;
+                if (q <= qmax) *reinterpret_cast<u32x4*>(slot + rc_off<C::CPR>(q / C::CPR + 1, q % C::CPR)) = v[i];
+            }
+        };
+        auto zero_row = [&](int row) {
+            char* slot = smem + (row & 3) * C::XSLOT;
+            for (int i = tid; i < C::XSLOT / 16; i += C::NT) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+        };
+        __syncthreads();
+        for (int r = h0 - 1; r <= h0 + 1; ++r) {
+            if (r < 0 || r >= H) {
+                zero_row(r);
+            } else {
+                load_row(drow(r), sx[1]);
+                store_row(r, sx[1]);
+            }
+        }
+        load_row(drow(min(h0 + 2, H - 1)), sx[0]);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+        auto step = [&](int h, auto P_) {
+            constexpr int P = decltype(P_)::value;
+            rw_barrier();
+            load_row(drow(min(h + 3, H - 1)), sx[1 - P]);
+            u32x2 mk[C::PT];
+            const bf16* mrow = mask ? mask + ((size_t)b * H + h) * W * CI : nullptr;
+            if (mask) {
+#pragma unroll
+                for (int n = 0; n < C::PT; ++n)
+                    mk[n] = *reinterpret_cast<const u32x2*>(mrow + (size_t)min(16 * n + i16, W - 1) * CI + 16 * wave + 4 * g);
+            }
+            floatx4 acc[C::PT];
+#pragma unroll
+            for (int n = 0; n < C::PT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const char* slot = smem + ((h + 1 - kh) & 3) * C::XSLOT;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                    for (int k = 0; k < C::KS; ++k)
+#pragma unroll
+                        for (int n = 0; n < C::PT; ++n) {
+                            const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rc_off<C::CPR>(16 * n + i16 + 2 - kw, 4 * k + g));
+                            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][k], bf, acc[n], 0, 0, 0);
+                        }
+            }
+            bf16* orow = dx + ((size_t)b * H + h) * W * CI;
+#pragma unroll
+            for (int n = 0; n < C::PT; ++n) {
+                const int px = 16 * n + i16;
+                if (px >= W) continue;
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[n][e];
+                if (mask) {
+#pragma unroll
+                    for (int e2 = 0; e2 < 2; ++e2) {
+                        const unsigned m = mk[n][e2];
+                        if (!(__uint_as_float(m << 16) > 0.f)) v[2 * e2] = 0.f;
+                        if (!(__uint_as_float(m & 0xffff0000u) > 0.f)) v[2 * e2 + 1] = 0.f;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bsum[e] += v[e];
+                u32x2 o;
+                o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16);
+                o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16);
+                *reinterpret_cast<u32x2*>(orow + (size_t)px * CI + 16 * wave + 4 * g) = o;
+            }
+            if (h + 2 < H) store_row(h + 2, sx[P]);
+            else if (h + 2 == H) zero_row(h + 2);
+        };
+        for (int h = h0; h < h1; h += 2) {
+            step(h, std::integral_constant<int, 0>{});
+            if (h + 1 < h1) step(h + 1, std::integral_constant<int, 1>{});
+        }
+    }
+    if (stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = bsum[e];
+            v += dpp_row<0x128>(v);
+            v += dpp_row<0x124>(v);
+            v += dpp_row<0x122>(v);
+            v += dpp_row<0x121>(v);
+            bsum[e] = v;
+        }
+        if (i16 == 0) {
+            float* st = stats + (size_t)blockIdx.x * 2 * CI + 16 * wave + 4 * g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                st[e] = bsum[e];
+                st[CI + e] = 0.f;
+            }
+        }
+    }
+}
+
+template <int CI, int CO, int KPX>
+static int launch_dgrad_co(const void* dy, int B, int H, int W, const void* w_bwd, void* dx, const void* mask,
+                           float* stats, hipStream_t s) {
+    using C = RbCfg<CI, CO, KPX>;
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_co_kernel<CI, CO, KPX>), C::LDS);
+    const int grid = B * C::BANDS;
+    const int64_t trows = cdiv((int64_t)B * H * W, 128);
+    if (stats && trows < grid) return -1;          // the table has fewer rows than workgroups
+    conv3x3_dgrad_rows_co_kernel<CI, CO, KPX><<<grid, C::NT, C::LDS, s>>>(
+        (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)mask, (bf16*)dx, stats, (int)trows, B, H, W);
+    return launch_status("conv3x3_dgrad_rows_co");
+}
+
 }  // namespace
 
 // OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
@@ -895,8 +1068,12 @@ int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,
 
 // backward-data with the producer's ReLU mask, conv2's shape only (-1 otherwise)
 int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
-                    const void* relu_mask, const float* stats, hipStream_t s) {
-    if (!rows_enabled() || cin != RW_CI || cout != RW_CO || W > RW_MAXW || W < 1 || H < 1 || B < 1) return -1;
+                    const void* relu_mask, float* stats, hipStream_t s) {
+    if (!rows_enabled() || W < 1 || H < 1 || B < 1) return -1;
+    if (rows_wide_enabled() && W <= 128) {
+        if (cin == 64 && cout == 64) return launch_dgrad_co<64, 64, 128>(dy, B, H, W, w_bwd, dx, relu_mask, stats, s);
+    }
+    if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     if (!relu_mask || stats) return -1;
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel), RD_LDS);

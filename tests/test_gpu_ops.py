@@ -384,3 +384,27 @@ def test_conv2_fwd_rowstats_matches(cuda, monkeypatch, CI, CO, shapes):
         torch.testing.assert_close(i1, i2, rtol=1e-5, atol=1e-6)
         # no-statistics forward (serving) takes the row kernel too: same bits
         assert torch.equal(Kn.conv3x3_fwd(x, w_nk, bias, relu=True), torch.relu(z_ref.float()).bfloat16())
+
+
+# the wider layers' data gradient by rows (conv4: 64 <- 64 with the ReLU mask and
+# the producer's bias sums, conv5: 64 <- 128 plain) against the GEMM path
+@pytest.mark.parametrize("CI,CO,H,W,masked", [(64, 64, 15, 127, True), (64, 64, 15, 127, False),
+                                              (64, 64, 3, 20, True)])
+def test_dgrad_rows_wide_matches(cuda, monkeypatch, CI, CO, H, W, masked):
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device=cuda).manual_seed(CI + CO + W)
+    B = 5
+    dy = torch.randn(B, H, W, CO, device=cuda, generator=g).bfloat16()
+    w_bwd = (torch.randn(CI, 9 * CO, device=cuda, generator=g) / 20).bfloat16()
+    mask = torch.randn(B, H, W, CI, device=cuda, generator=g).bfloat16() if masked else None
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+        db = torch.full((CI,), 0.25, device=cuda) if masked else None
+        dx = Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask, dbias=db)
+        outs.append((dx, db))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if masked:
+        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
+        ref = outs[1][0].double().view(-1, CI).sum(0) + 0.25
+        torch.testing.assert_close(outs[0][1].double(), ref, rtol=1e-4, atol=2e-2)
