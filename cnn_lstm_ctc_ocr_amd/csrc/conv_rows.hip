@@ -696,6 +696,7 @@ struct RfCfg {
     static constexpr int PER = (KPX * CPR + NT - 1) / NT;
     static constexpr int PER_CU = LDS <= 80 * 1024 && NW <= 4 ? 2 : 1;
     static constexpr int BANDS = PER_CU;
+    static constexpr int PH = KS >= 4 ? 2 : 1;              // pixel parts per row (register budget)
 };
 
 template <int CI, int CO, int KPX>
@@ -753,80 +754,99 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
         }
     }
     load_row(xrow(min(h0 + 2, H - 1)), sx[0]);
-    const float inv_w = 1.f / (float)W;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
     auto step = [&](int h, auto P_) {
         constexpr int P = decltype(P_)::value;
         rw_barrier();
         load_row(xrow(min(h + 3, H - 1)), sx[1 - P]);
-        floatx4 acc[C::PT];
-#pragma unroll
-        for (int n = 0; n < C::PT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-            const char* slot = smem + ((h + kh - 1) & 3) * C::XSLOT;
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-                for (int k = 0; k < C::KS; ++k)
-#pragma unroll
-                    for (int n = 0; n < C::PT; ++n) {
-                        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rc_off<C::CPR>(16 * n + i16 + kw, 4 * k + g));
-                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][k], bf, acc[n], 0, 0, 0);
-                    }
-        }
-        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        // the row in PH pixel parts (PT/PH tiles each: fewer live accumulators for
+        // the 8-wave configs); each part's (n, sum, M2 about its mean) merged into the
+        // row's by Chan's formula
+        constexpr int PP = C::PT / C::PH;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f}, rm2[4] = {0.f, 0.f, 0.f, 0.f};
+        float rn = 0.f;
         bf16* orow = y + ((size_t)b * H + h) * W * CO;
 #pragma unroll
-        for (int n = 0; n < C::PT; ++n) {
-            const int px = 16 * n + i16;
+        for (int ph = 0; ph < C::PH; ++ph) {
+            floatx4 acc[PP];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float v = acc[n][e] + bco[e];
-                if (relu) v = fmaxf(v, 0.f);
-                acc[n][e] = v;
-                if (px < W) sum[e] += v;
-            }
-            if (px < W) {
-                u32x2 o;
-                o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][0]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][1]) << 16);
-                o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][2]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][3]) << 16);
-                *reinterpret_cast<u32x2*>(orow + (size_t)px * CO + 16 * wave + 4 * g) = o;
-            }
-        }
-        if (stats) {
-            float q2[4];
+            for (int n = 0; n < PP; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float v = sum[e];
-                v += dpp_row<0x128>(v);
-                v += dpp_row<0x124>(v);
-                v += dpp_row<0x122>(v);
-                v += dpp_row<0x121>(v);
-                sum[e] = v;
-                const float mean = v * inv_w;
-                float q = 0.f;
+            for (int kh = 0; kh < 3; ++kh) {
+                const char* slot = smem + ((h + kh - 1) & 3) * C::XSLOT;
 #pragma unroll
-                for (int n = 0; n < C::PT; ++n) {
-                    const float d = acc[n][e] - mean;
-                    if (16 * n + i16 < W) q += d * d;
-                }
-                q += dpp_row<0x128>(q);
-                q += dpp_row<0x124>(q);
-                q += dpp_row<0x122>(q);
-                q += dpp_row<0x121>(q);
-                q2[e] = q;
+                for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                    for (int k = 0; k < C::KS; ++k)
+#pragma unroll
+                        for (int n = 0; n < PP; ++n) {
+                            const int pt = ph * PP + n;
+                            const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rc_off<C::CPR>(16 * pt + i16 + kw, 4 * k + g));
+                            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][k], bf, acc[n], 0, 0, 0);
+                        }
             }
-            if (i16 == 0) {
-                float* st = stats + ((size_t)b * H + h) * 2 * CO + 16 * wave + 4 * g;
+            float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int n = 0; n < PP; ++n) {
+                const int px = 16 * (ph * PP + n) + i16;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    st[e] = sum[e];
-                    st[CO + e] = q2[e];
+                    float v = acc[n][e] + bco[e];
+                    if (relu) v = fmaxf(v, 0.f);
+                    acc[n][e] = v;
+                    if (px < W) sum[e] += v;
                 }
+                if (px < W) {
+                    u32x2 o;
+                    o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][0]) |
+                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][1]) << 16);
+                    o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][2]) |
+                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][3]) << 16);
+                    *reinterpret_cast<u32x2*>(orow + (size_t)px * CO + 16 * wave + 4 * g) = o;
+                }
+            }
+            if (stats) {
+                const int p0 = 16 * PP * ph;
+                const float np = (float)max(0, min(W - p0, 16 * PP));
+                if (np > 0.f) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float v = sum[e];
+                        v += dpp_row<0x128>(v);
+                        v += dpp_row<0x124>(v);
+                        v += dpp_row<0x122>(v);
+                        v += dpp_row<0x121>(v);
+                        const float mean = v / np;
+                        float q = 0.f;
+#pragma unroll
+                        for (int n = 0; n < PP; ++n) {
+                            const float d = acc[n][e] - mean;
+                            if (16 * (ph * PP + n) + i16 < W) q += d * d;
+                        }
+                        q += dpp_row<0x128>(q);
+                        q += dpp_row<0x124>(q);
+                        q += dpp_row<0x122>(q);
+                        q += dpp_row<0x121>(q);
+                        if (ph == 0) {
+                            rs[e] = v;
+                            rm2[e] = q;
+                        } else {                                   // Chan: merge (rn, rs, rm2) with (np, v, q)
+                            const float dm = v / np - rs[e] / rn;
+                            rm2[e] += q + dm * dm * rn * np / (rn + np);
+                            rs[e] += v;
+                        }
+                    }
+                    rn += np;
+                }
+            }
+        }
+        if (stats && i16 == 0) {
+            float* st = stats + ((size_t)b * H + h) * 2 * CO + 16 * wave + 4 * g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                st[e] = rs[e];
+                st[CO + e] = rm2[e];
             }
         }
         if (h + 2 < H) store_row(h + 2, sx[P]);
@@ -1041,6 +1061,7 @@ static bool rows_wide_enabled() {
 }
 
 static bool rows_fwd_wide(int cin, int cout) {
+    // conv6's 128 -> 128 spills at 8 waves (146 vs 110 us on the GEMM engine): not routed
     return (cin == 32 && cout == 64) || (cin == 64 && cout == 64) || (cin == 64 && cout == 128);
 }
 

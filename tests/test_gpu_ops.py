@@ -406,5 +406,7 @@ def test_dgrad_rows_wide_matches(cuda, monkeypatch, CI, CO, H, W, masked):
     assert torch.equal(outs[0][0], outs[1][0])
     if masked:
         torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-3)
+        # against the bf16-rounded dx only to rounding noise (the sums are of the f32 values)
         ref = outs[1][0].double().view(-1, CI).sum(0) + 0.25
-        torch.testing.assert_close(outs[0][1].double(), ref, rtol=1e-4, atol=2e-2)
+        n = outs[1][0].numel() // CI
+        torch.testing.assert_close(outs[0][1].double(), ref, rtol=0, atol=0.01 * n ** 0.5)
