@@ -555,23 +555,23 @@ __device__ __forceinline__ int rc_off(int r, int c) {
     return r * CPR * 16 + ((c ^ sw) << 4);
 }
 
-template <int CI, int KPX>
+template <int CI, int KPX, int CO_ = 64>
 struct RcCfg {
-    static constexpr int CO = 64;
+    static constexpr int CO = CO_, NW = CO / 16, NT = NW * 64;
     static constexpr int XCPR = CI / 8, DCPR = CO / 8;       // 16-B chunks per pixel
     static constexpr int XSLOT = (KPX + 2) * CI * 2, DSLOT = KPX * CO * 2;
     static constexpr int DOFF = 4 * XSLOT;
     static constexpr int LDS = DOFF + 2 * DSLOT;
-    static constexpr int XPER = (KPX * XCPR + 255) / 256, DPER = (KPX * DCPR + 255) / 256;   // chunks per thread
+    static constexpr int XPER = (KPX * XCPR + NT - 1) / NT, DPER = (KPX * DCPR + NT - 1) / NT;   // chunks per thread
     static constexpr int PART = 9 * CI * CO;
 };
 
-template <int CI, int KPX>
-__global__ void __launch_bounds__(256, 1)
+template <int CI, int KPX, int CO_>
+__global__ void __launch_bounds__((RcCfg<CI, KPX, CO_>::NT), 1)
 conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
                              int B, int H, int W) {
-    using C = RcCfg<CI, KPX>;
-    constexpr int CO = C::CO, TI = CI / 16;
+    using C = RcCfg<CI, KPX, CO_>;
+    constexpr int CO = C::CO, TI = CI / 16, NT = C::NT;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -579,7 +579,7 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
     const int kr0 = 4 * g + (i16 >> 2);
     const int mq = 4 * (i16 & 3);
 
-    for (int i = tid; i < C::LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < C::LDS / 16; i += NT) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
 
     floatx4 acc[9][TI];
 #pragma unroll
@@ -591,17 +591,17 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
     u32x4 sx[2][C::XPER], sd[2][C::DPER];
     auto load_x = [&](const bf16* base, u32x4 (&v)[C::XPER]) {
 #pragma unroll
-        for (int i = 0; i < C::XPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + 256 * i, xq) * 8);
+        for (int i = 0; i < C::XPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + NT * i, xq) * 8);
     };
     auto load_d = [&](const bf16* base, u32x4 (&v)[C::DPER]) {
 #pragma unroll
-        for (int i = 0; i < C::DPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + 256 * i, dq) * 8);
+        for (int i = 0; i < C::DPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + NT * i, dq) * 8);
     };
     auto store_x = [&](int row, const u32x4 (&v)[C::XPER]) {
         char* slot = smem + (row & 3) * C::XSLOT;
 #pragma unroll
         for (int i = 0; i < C::XPER; ++i) {
-            const int q = tid + 256 * i;
+            const int q = tid + NT * i;
             if (q <= xq) *reinterpret_cast<u32x4*>(slot + rc_off<C::XCPR>(q / C::XCPR + 1, q % C::XCPR)) = v[i];
         }
     };
@@ -609,7 +609,7 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
         char* slot = smem + C::DOFF + (row & 1) * C::DSLOT;
 #pragma unroll
         for (int i = 0; i < C::DPER; ++i) {
-            const int q = tid + 256 * i;
+            const int q = tid + NT * i;
             if (q <= dq) *reinterpret_cast<u32x4*>(slot + rc_off<C::DCPR>(q / C::DCPR, q % C::DCPR)) = v[i];
         }
     };
@@ -1103,14 +1103,15 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
     return launch_status("conv3x3_dgrad_rows");
 }
 
-template <int CI, int KPX>
+template <int CI, int KPX, int CO = 64>
 static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, float* dw, int accumulate, void* ws,
                           hipStream_t s) {
-    using C = RcCfg<CI, KPX>;
+    using C = RcCfg<CI, KPX, CO>;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX>), C::LDS);
-    conv3x3_wgrad_rows_co_kernel<CI, KPX><<<grid, 256, C::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX, CO>), C::LDS);
+    conv3x3_wgrad_rows_co_kernel<CI, KPX, CO><<<grid, C::NT, C::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws,
+                                                                           B, H, W);
     int st = launch_status("conv3x3_wgrad_rows_co");
     if (st) return st;
     GemmParams p = {};
@@ -1130,6 +1131,8 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
         if (cin == 64) return launch_rows_co<64, 128>(x, dy, B, H, W, dw, accumulate, ws, s);
         return -1;
     }
+    // conv5 (64 -> 128) would need 8 waves at <= 256 registers: its 144 accumulator
+    // registers spill there, so it stays on the TN engine
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;
