@@ -687,28 +687,31 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
 // ds_read_b128 = 8 ci of one pixel). Per-row BatchNorm partials are wave-local
 // (a wave owns its channels): DPP row sums over the 16 pixels of a tile, the
 // tiles in order, M2 about the row mean in a second pass.
-template <int CI, int CO, int KPX>
+template <int CI, int CO, int KPX, int CS = 1>
 struct RfCfg {
-    static constexpr int NW = CO / 16, NT = NW * 64, KS = CI / 32, PT = KPX / 16;
+    // CS workgroups split the output channels of a row band (CO / CS per workgroup)
+    static constexpr int NW = CO / 16 / CS, NT = NW * 64, KS = CI / 32, PT = KPX / 16;
     static constexpr int CPR = CI / 8;
     static constexpr int XSLOT = (KPX + 2) * CI * 2;
     static constexpr int LDS = 4 * XSLOT;
     static constexpr int PER = (KPX * CPR + NT - 1) / NT;
     static constexpr int PER_CU = LDS <= 80 * 1024 && NW <= 4 ? 2 : 1;
     static constexpr int BANDS = PER_CU;
-    static constexpr int PH = KS >= 4 ? 2 : 1;              // pixel parts per row (register budget)
+    static constexpr int PH = KS >= 4 && NW > 4 ? 2 : 1;    // pixel parts per row (register budget)
 };
 
-template <int CI, int CO, int KPX>
-__global__ void __launch_bounds__((RfCfg<CI, CO, KPX>::NT), (RfCfg<CI, CO, KPX>::PER_CU))
+template <int CI, int CO, int KPX, int CS>
+__global__ void __launch_bounds__((RfCfg<CI, CO, KPX, CS>::NT), (RfCfg<CI, CO, KPX, CS>::PER_CU))
 conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
                            bf16* __restrict__ y, float* __restrict__ stats, int relu, int B, int H, int W) {
-    using C = RfCfg<CI, CO, KPX>;
+    using C = RfCfg<CI, CO, KPX, CS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cs = blockIdx.x % CS;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) + cs * C::NW;     // the wave's output-channel tile
     const int i16 = lane & 15, g = lane >> 4;
-    const int b = blockIdx.x / C::BANDS, band = blockIdx.x - b * C::BANDS;
+    const int bid = blockIdx.x / CS;
+    const int b = bid / C::BANDS, band = bid - b * C::BANDS;
     const int rows = (H + C::BANDS - 1) / C::BANDS;
     const int h0 = band * rows, h1 = min(H, h0 + rows);
     if (h0 >= h1) return;
@@ -858,13 +861,13 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
     }
 }
 
-template <int CI, int CO, int KPX>
+template <int CI, int CO, int KPX, int CS = 1>
 static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, const float* bias, void* y, int relu,
                          float* stats, hipStream_t s) {
-    using C = RfCfg<CI, CO, KPX>;
+    using C = RfCfg<CI, CO, KPX, CS>;
     static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX>), C::LDS);
-    conv3x3_fwd_rows_co_kernel<CI, CO, KPX><<<B * C::BANDS, C::NT, C::LDS, s>>>(
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS>), C::LDS);
+    conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
         (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, relu, B, H, W);
     return launch_status("conv3x3_fwd_rows_co");
 }
@@ -878,9 +881,10 @@ static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, c
 // its masked dx as ONE row of the [tiles][2][CI] table (sums in the first CI)
 // and the rows past the grid are zeroed, so summing every table row gives
 // the same total as the 128-pixel tiles of the GEMM path.
-template <int CI, int CO, int KPX>
+template <int CI, int CO, int KPX, int CS = 1>
 struct RbCfg {
-    static constexpr int NW = CI / 16, NT = NW * 64, KS = CO / 32, PT = KPX / 16;
+    // CS workgroups split the input channels (the outputs here) of a row band
+    static constexpr int NW = CI / 16 / CS, NT = NW * 64, KS = CO / 32, PT = KPX / 16;
     static constexpr int CPR = CO / 8;
     static constexpr int XSLOT = (KPX + 2) * CO * 2;
     static constexpr int LDS = 4 * XSLOT;
@@ -889,22 +893,25 @@ struct RbCfg {
     static constexpr int BANDS = PER_CU;
 };
 
-template <int CI, int CO, int KPX>
-__global__ void __launch_bounds__((RbCfg<CI, CO, KPX>::NT), (RbCfg<CI, CO, KPX>::PER_CU))
+template <int CI, int CO, int KPX, int CS>
+__global__ void __launch_bounds__((RbCfg<CI, CO, KPX, CS>::NT), (RbCfg<CI, CO, KPX, CS>::PER_CU))
 conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb,
                              const bf16* __restrict__ mask, bf16* __restrict__ dx, float* __restrict__ stats,
                              int stat_rows, int B, int H, int W) {
-    using C = RbCfg<CI, CO, KPX>;
+    using C = RbCfg<CI, CO, KPX, CS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cs = blockIdx.x % CS;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6) + cs * C::NW;     // the wave's channel tile
     const int i16 = lane & 15, g = lane >> 4;
-    const int b = blockIdx.x / C::BANDS, band = blockIdx.x - b * C::BANDS;
+    const int bid = blockIdx.x / CS;
+    const int b = bid / C::BANDS, band = bid - b * C::BANDS;
     const int rows = (H + C::BANDS - 1) / C::BANDS;
     const int h0 = band * rows, h1 = min(H, h0 + rows);
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    if (stats)                                     // table rows past the grid: zero
-        for (int r = gridDim.x + blockIdx.x; r < stat_rows; r += gridDim.x)
+    const int nbid = gridDim.x / CS;               // table rows written: one per band workgroup
+    if (stats && cs == 0)                          // table rows past them: zero
+        for (int r = nbid + bid; r < stat_rows; r += nbid)
             for (int i = tid; i < 2 * CI; i += C::NT) stats[(size_t)r * 2 * CI + i] = 0.f;
     if (h0 < h1) {
         for (int i = tid; i < C::LDS / 16; i += C::NT) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
@@ -1018,7 +1025,7 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
             bsum[e] = v;
         }
         if (i16 == 0) {
-            float* st = stats + (size_t)blockIdx.x * 2 * CI + 16 * wave + 4 * g;
+            float* st = stats + (size_t)bid * 2 * CI + 16 * wave + 4 * g;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 st[e] = bsum[e];
@@ -1028,16 +1035,16 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
     }
 }
 
-template <int CI, int CO, int KPX>
+template <int CI, int CO, int KPX, int CS = 1>
 static int launch_dgrad_co(const void* dy, int B, int H, int W, const void* w_bwd, void* dx, const void* mask,
                            float* stats, hipStream_t s) {
-    using C = RbCfg<CI, CO, KPX>;
-    static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_co_kernel<CI, CO, KPX>), C::LDS);
-    const int grid = B * C::BANDS;
+    using C = RbCfg<CI, CO, KPX, CS>;
+    const int grid = B * C::BANDS * CS;
     const int64_t trows = cdiv((int64_t)B * H * W, 128);
-    if (stats && trows < grid) return -1;          // the table has fewer rows than workgroups
-    conv3x3_dgrad_rows_co_kernel<CI, CO, KPX><<<grid, C::NT, C::LDS, s>>>(
+    if (stats && trows < B * C::BANDS) return -1;  // the table has fewer rows than band workgroups
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS>), C::LDS);
+    conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS><<<grid, C::NT, C::LDS, s>>>(
         (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)mask, (bf16*)dx, stats, (int)trows, B, H, W);
     return launch_status("conv3x3_dgrad_rows_co");
 }
@@ -1061,7 +1068,9 @@ static bool rows_wide_enabled() {
 }
 
 static bool rows_fwd_wide(int cin, int cout) {
-    // conv6's 128 -> 128 spills at 8 waves (146 vs 110 us on the GEMM engine): not routed
+    // conv6's 128 -> 128 stays on the GEMM engine: one 8-wave workgroup spills
+    // (146 vs 110 us), two 4-wave workgroups per band (CS = 2, one wave per SIMD at
+    // 133 KB of ring) are latency-bound (158 us forward, 172 us backward-data)
     return (cin == 32 && cout == 64) || (cin == 64 && cout == 64) || (cin == 64 && cout == 128);
 }
 
