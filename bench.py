@@ -64,7 +64,9 @@ def work_gemm(args):
 
 
 ROOFLINE_OPS = {
-    "conv": ("ocrk_conv3x3_fwd", work_conv_fwd, "conv2-conv8 forward implicit-GEMM launches (MFMA bf16)"),
+    # conv2-conv5 run on the row-walking kernels (ocrk_conv3x3_fwd_rowstats for the BN layers)
+    "conv": (("ocrk_conv3x3_fwd", "ocrk_conv3x3_fwd_rowstats"), work_conv_fwd,
+             "conv2-conv8 forward launches (row-walking conv2-conv5, implicit GEMM conv6-conv8; MFMA bf16)"),
     "lstm": ("ocrk_lstm_fwd", work_lstm_fwd, "recurrent h.W_h time loop, both directions (MFMA bf16)"),
     "gemm": ("ocrk_gemm", work_gemm, "dense GEMM launches"),
 }
@@ -491,11 +493,14 @@ def main():
     probe = []
     table = {}
 
+    op_names = op_name if isinstance(op_name, tuple) else (op_name,)
+
     def arm_probes():
-        _lib.PROBES[op_name] = (work_fn, probe)
+        for name in op_names:
+            _lib.PROBES[name] = (work_fn, probe)
         if args.breakdown:
             for name in _lib.SIGNATURES:
-                if name != op_name and not name.endswith(("_size", "version", "last_error", "tiles")) \
+                if name not in op_names and not name.endswith(("_size", "version", "last_error", "tiles")) \
                         and not name.startswith("ocrk_timer"):
                     table[name] = []
                     _lib.PROBES[name] = (None, table[name])
@@ -571,7 +576,7 @@ def main():
 
     if args.breakdown and rank == 0:
         rows = [(n, sum(v) / probed, len(v) // probed) for n, v in rows.items()]
-        rows.append((op_name, sum(ms) / probed, len(ms) // probed))
+        rows.append(("+".join(op_names), sum(ms) / probed, len(ms) // probed))
         tot = sum(r[1] for r in rows)
         print(f"# per-step device time by entry point (sum {tot:.2f} ms, wall {1e3 * elapsed / args.steps:.2f} ms)",
               file=sys.stderr)
