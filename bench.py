@@ -10,6 +10,7 @@ gradient all-reduce (N > 1) and the Adam kernel, on synthetic uint8 crops and
 labels already resident in HBM. Rank 0 prints ONE JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -620,9 +621,16 @@ def main():
     if args.roofline == "conv" and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             pmc = json.load(fh)
-        result["roofline"]["traffic"] = pmc["bytes_per_launch"]
-        result["roofline"]["traffic_unit"] = "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
-        result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
+        # the summary counts only while it was taken of the library this run loaded
+        lib_sha = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+        src = os.path.relpath(args.traffic_json, ROOT)
+        if pmc.get("libocrk_sha256") == lib_sha:
+            result["roofline"]["traffic"] = pmc["bytes_per_launch"]
+            result["roofline"]["traffic_unit"] = "bytes per launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+            result["roofline"]["traffic_source"] = f"{src} (PMC passes of this libocrk.so, sha256 {lib_sha[:12]})"
+        else:
+            result["roofline"]["traffic_note"] = (f"{src} was taken of another libocrk.so build "
+                                                  f"({str(pmc.get('libocrk_sha256'))[:12]} vs {lib_sha[:12]}): not reported")
     if rank == 0 and not args.no_cer and args.cell == "lstm":      # the golden decodes are of the LSTM model
         result["cer_vs_ref"] = cer_vs_ref(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -10,13 +10,16 @@ read side is doubled; WRITE_SIZE is exact for 16-B/lane stores.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import re
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def per_dispatch(root, counter, match):
+
+def per_dispatch(root, counter, match, names=None):
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {root}")
@@ -27,6 +30,8 @@ def per_dispatch(root, counter, match):
                 if row.get("Counter_Name") != counter or not re.search(match, row.get("Kernel_Name", "")):
                     continue
                 vals[(f, row.get("Dispatch_Id"))] += float(row["Counter_Value"])
+                if names is not None:
+                    names.add(row["Kernel_Name"])
     return list(vals.values())
 
 
@@ -38,8 +43,12 @@ def main():
     ap.add_argument("--desc", default="")
     ap.add_argument("--command", default="")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "cnn_lstm_ctc_ocr_amd", "libocrk.so"),
+                    help="the library the profiled run loaded: its sha256 ties the summary to the code "
+                         "(bench.py reports the traffic only while the loaded library matches)")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.match)
+    names = set()
+    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.match, names)
     write = per_dispatch(a.write, "WRITE_SIZE", a.match)
     if not fetch or not write:
         raise SystemExit(f"no dispatches matching {a.match!r}")
@@ -55,6 +64,8 @@ def main():
         "write_bytes_per_launch": round(w_kib * 1024),
         "bytes_per_launch": round((2 * f_kib + w_kib) * 1024),
         "command": a.command,
+        "kernels": sorted(names),
+        "libocrk_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
     }
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)
