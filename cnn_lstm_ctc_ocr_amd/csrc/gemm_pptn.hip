@@ -106,7 +106,6 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
             t_c0[s] = col - tap * p.convC;
         }
     }
-    int pix_h = 0, pix_w = 0;
 
     auto issue = [&](auto U_, int kt, char* buf) {
         constexpr int U = decltype(U_)::value;
@@ -114,10 +113,7 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
         const bool kok = k < kend;
         const unsigned kst = (unsigned)((int64_t)(kt * BK + kbeg) * (U == 0 || U == 3 ? p.lda : p.ldb) * 2);
         if constexpr ((U == 0 || U == 3) && AM == A_IM2COL_T) {
-            if constexpr (U == 0) {                        // U3 of the same K-tile follows: same pixel
-                pix_w = k % p.convW;
-                pix_h = (k / p.convW) % p.convH;
-            }
+            const int pix_w = k % p.convW, pix_h = (k / p.convW) % p.convH;   // this lane's pixel
 #pragma unroll
             for (int i = 0; i < NUA; ++i) {
                 const int s = (U == 0 ? 0 : 2) + i;
@@ -157,18 +153,36 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
 
+    // Staging schedule: every unit is issued as soon as the reads of its slot
+    // (two K-tiles back, same buffer) allow, so it has 4-5 phases to land
+    // before the wait that retires it (a K-tile ahead left it 2, and the waits
+    // stalled on DMA latency). Per K-tile k, in issue order:
+    //   phase 0: U3(k+1)    phase 2: U1(k+2)    phase 3: U0(k+2), U2(k+2)
+    // (U1 and U0 / U2 of K-tile k are read in phases 0 / 0 / 1, U3 in phase 2;
+    // a slot is rewritten >= 2 phases after its last read). B q0 stays in
+    // registers from phase 0 to phase 3, so phase 3 reads nothing. Waits, each
+    // before a phase's first barrier for the next phase's reads, count the DMAs
+    // issued after the retired one: phase 0 (U2(k)) 10, phase 1 (U3(k)) 8,
+    // phase 3 (U0, U1 of k+1) 10 instructions; the last two K-tiles drain to 0.
     issue(I0{}, 0, smem);
     issue(I1{}, 0, smem);
     issue(I2{}, 0, smem);
     issue(I3{}, 0, smem);
-    vm_wait<0>();
+    if (nk > 1) {
+        issue(I1{}, 1, smem + BUF);
+        issue(I0{}, 1, smem + BUF);
+        issue(I2{}, 1, smem + BUF);
+        vm_wait<NUB + NUA + NUB>();                       // K-tile 0 landed
+    } else {
+        vm_wait<0>();
+    }
     tt_barrier();
     if (wm == 1) tt_barrier();                            // stagger: waves 4-7 one barrier behind
 
     // transposed fragment reads (frag_tr): lane reads k-row kr0 (+16) of the
     // 32-deep kk block, 4 consecutive columns at cq within a 16-column group
     const int kr0 = 4 * g + (i16 >> 2), cq = 4 * (i16 & 3);
-    bf16x8 afr[4][2], bfr[2][2];
+    bf16x8 afr[4][2], bq0[2][2], bq1[2][2];
     auto tr_addr = [&](int blk_off, int col, int kk) {   // byte offset of (k-row kk*32 + kr0, col) in a block
         const int r = kk * 32 + kr0;
         return blk_off + r * ROWB + ((((col >> 3) ^ (r & 7))) << 4) + (col & 7) * 2;
@@ -182,7 +196,7 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
                 afr[i][kk] = frag_tr(reinterpret_cast<const unsigned short*>(cur + tr_addr(blk, i * 16 + cq, kk)),
                                      16 * (ROWB / 2));
     };
-    auto read_b = [&](const char* cur, int qb) {
+    auto read_b = [&](const char* cur, int qb, bf16x8 (&bfr)[2][2]) {
         const int blk = A_BYTES + (2 * qb + (wn >> 1)) * BLK;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -192,7 +206,7 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
                                          cur + tr_addr(blk, (wn & 1) * 32 + j * 16 + cq, kk)),
                                      16 * (ROWB / 2));
     };
-    auto mfma_q = [&](auto QA_, auto QB_) {
+    auto mfma_q = [&](auto QA_, auto QB_, const bf16x8 (&bfr)[2][2]) {
         constexpr int QA = decltype(QA_)::value, QB = decltype(QB_)::value;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -207,37 +221,39 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     };
 
     for (int kt = 0; kt < nk; ++kt) {
-        const char* cur = smem + (kt & 1) * BUF;
+        char* cur = smem + (kt & 1) * BUF;
         char* nxt = smem + ((kt + 1) & 1) * BUF;
-        const bool more = kt + 1 < nk;
+        const bool full = kt + 2 < nk;
+        // phase 0: A q0, B q0; U3 of the next K-tile
         read_a(cur, 0);
-        read_b(cur, 0);
-        if (more) {
-            issue(I0{}, kt + 1, nxt);
-            if (kt > 0) vm_wait<NUA + NUA>(); else vm_wait<NUA>();
+        read_b(cur, 0, bq0);
+        if (kt + 1 < nk) issue(I3{}, kt + 1, nxt);
+        if (full) vm_wait<NUA + NUB + NUA + NUB + NUA>(); else vm_wait<0>();
+        tt_barrier();
+        mfma_q(I0{}, I0{}, bq0);
+        tt_barrier();
+        // phase 1: B q1
+        read_b(cur, 1, bq1);
+        if (full) vm_wait<NUB + NUA + NUB + NUA>(); else vm_wait<0>();
+        tt_barrier();
+        mfma_q(I0{}, I1{}, bq1);
+        tt_barrier();
+        // phase 2: A q1; U1 of K-tile kt+2 into this buffer (no wait: phase 3 reads nothing)
+        read_a(cur, 1);
+        if (full) issue(I1{}, kt + 2, cur);
+        tt_barrier();
+        mfma_q(I1{}, I1{}, bq1);
+        tt_barrier();
+        // phase 3: U0, U2 of K-tile kt+2
+        if (full) {
+            issue(I0{}, kt + 2, cur);
+            issue(I2{}, kt + 2, cur);
+            vm_wait<NUB + NUA + NUB + NUA + NUB>();
         } else {
-            if (kt > 0) vm_wait<NUA>(); else vm_wait<0>();
+            vm_wait<0>();
         }
         tt_barrier();
-        mfma_q(I0{}, I0{});
-        tt_barrier();
-        read_b(cur, 1);
-        if (more) { issue(I1{}, kt + 1, nxt); vm_wait<NUB + NUA>(); }
-        else vm_wait<0>();
-        tt_barrier();
-        mfma_q(I0{}, I1{});
-        tt_barrier();
-        read_a(cur, 1);
-        if (more) { issue(I2{}, kt + 1, nxt); vm_wait<NUB + NUB>(); }
-        else vm_wait<0>();
-        tt_barrier();
-        mfma_q(I1{}, I1{});
-        tt_barrier();
-        read_b(cur, 0);
-        if (more) { issue(I3{}, kt + 1, nxt); vm_wait<NUA + NUB>(); }
-        else vm_wait<0>();
-        tt_barrier();
-        mfma_q(I1{}, I0{});
+        mfma_q(I1{}, I0{}, bq0);
         tt_barrier();
     }
     if (wm == 0) tt_barrier();                            // balance the stagger
