@@ -38,8 +38,8 @@ namespace {
 
 constexpr unsigned TT_OOB = 0x80000000u;
 
-__device__ __forceinline__ void tt_dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+__device__ __forceinline__ void tt_dma16(const i32x4_t& r, void* lds, unsigned voff) {
+    lds_dma16_asm(r, lds, voff);
 }
 
 __device__ __forceinline__ void tt_barrier() {
@@ -78,9 +78,8 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
     const int kbeg = zs * p.k_chunk;
     const int kend = min(p.K, kbeg + p.k_chunk);
     const int nk = max(1, (kend - kbeg + BK - 1) / BK);
-    const __amdgpu_buffer_rsrc_t ra =
-        uniform_rsrc(A, (int64_t)p.K * (AM == A_IM2COL_T ? p.convC : p.lda) * 2);
-    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, (int64_t)p.K * p.ldb * 2);
+    const i32x4_t ra = uniform_rsrc_words(A, (int64_t)p.K * (AM == A_IM2COL_T ? p.convC : p.lda) * 2);
+    const i32x4_t rb = uniform_rsrc_words(B, (int64_t)p.K * p.ldb * 2);
 
     // ---- per-lane DMA geometry: instruction idx = i*8 + wave (i = 0, 1) of a
     // unit covers block idx >> 3, k-rows (idx & 7)*8 + lane/8, slot lane & 7

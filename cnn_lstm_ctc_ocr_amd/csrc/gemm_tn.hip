@@ -19,8 +19,8 @@ namespace {
 
 constexpr unsigned TN_OOB = 0x80000000u;
 
-__device__ __forceinline__ void tn_dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+__device__ __forceinline__ void tn_dma16(const i32x4_t& r, void* lds, unsigned voff) {
+    lds_dma16_asm(r, lds, voff);                          // asm: see mfma_util.h
 }
 
 template <int CPR>
@@ -55,8 +55,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_tn_kernel(const GemmParams p) {
     if constexpr (AM == A_COLK) a_elems = (int64_t)p.K * p.lda;
     else a_elems = (int64_t)p.K * p.convC;                        // NHWC source, K = B*H*W pixels
     const int64_t b_elems = (int64_t)p.K * p.ldb;
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, a_elems * 2);
-    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, b_elems * 2);
+    const i32x4_t ra = uniform_rsrc_words(A, a_elems * 2);
+    const i32x4_t rb = uniform_rsrc_words(B, b_elems * 2);
 
     // ---- per-lane geometry of each A instruction (stage-invariant parts)
     const int qa = lane / CPRA, sa_slot = lane % CPRA;

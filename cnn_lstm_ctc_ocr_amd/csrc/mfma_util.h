@@ -79,4 +79,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
 }
 
+// The same descriptor as four SGPR words, for inline-asm buffer operations.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t uniform_rsrc_words(const void* base, int64_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    const int lo = (int)__builtin_amdgcn_readfirstlane((unsigned)b);
+    const int hi = (int)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32) & 0xffffu);   // stride 0
+    const int nb = __builtin_amdgcn_readfirstlane(bytes > 0x7fffffff ? 0x7fffffff : (int)bytes);
+    return i32x4_t{lo, hi, nb, 0x00020000};
+}
+
+// LDS-DMA (buffer_load_dwordx4 ... lds, 16 B per lane, lane-linear at `lds`) as
+// inline asm. The compiler's waitcnt pass cannot tell one LDS buffer of a kernel's
+// single __shared__ array from another, so after the builtin form it drains every
+// pending DMA (s_waitcnt vmcnt(0)) in front of each ds_read -- which defeats a
+// schedule that keeps DMAs in flight across phases. Hidden from it, the caller's
+// counted vm_wait<N> + barriers are the only ordering (RAW and WAR as the
+// schedule states), and the compiler's own vmcnt waits only over-count.
+__device__ __forceinline__ void lds_dma16_asm(const i32x4_t& r, void* lds, unsigned voff) {
+    const unsigned a = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :: "v"(voff), "s"(r), "s"(a) : "memory", "m0");
+}
+
 }  // namespace ocrk
