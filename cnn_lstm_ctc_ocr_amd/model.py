@@ -411,7 +411,7 @@ class _BiGRU(torch.autograd.Function):
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 
-_TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "224"))
+_TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
 
 
 def _splits(M, N, Kdim, batch=1):
@@ -420,9 +420,9 @@ def _splits(M, N, Kdim, batch=1):
     ping-pong TN engine (one item per CU, slices of >= 1024 rows), smaller
     outputs on the 128 x 128 engine (~2 items per CU, >= 2048 rows). `batch`
     problems share the chip. The 256 x 256 launches stop at OCRK_TN_ITEMS
-    (224) items, one round on 7/8 of the CUs: the main stream's BN backward and
-    data-gradient kernels beside them find free CUs instead of waiting for the
-    whole round (6.23 vs 6.29 ms per step with 256)."""
+    (256) items, one round on the chip (round 2 measured 224 faster, 6.23 vs
+    6.29 ms; since the TN engines keep their DMAs in flight (round 3) 256 is:
+    5.374-5.402 vs 5.416-5.426 ms, 320 / 384 / 512 5.45 / 5.44-5.48 / 5.56-5.58)."""
     if M >= 256 and N >= 256:
         tiles = -(-M // 256) * -(-N // 256) * batch
         return int(max(1, min(_TN_ITEMS // tiles, Kdim // 1024)))      # <= 256 items: one round on the chip
