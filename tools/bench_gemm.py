@@ -37,7 +37,7 @@ def main():
     rows = []
     for (M, N, Kd, tag) in [(32000, 4096, 256, "proj L1"), (32000, 4096, 1024, "proj L2"),
                             (32000, 1024, 4096, "dx L2"), (32000, 256, 4096, "dx L1"),
-                            (32000, 1024, 96, "logits dx")]:
+                            (32000, 1024, 96, "logits dx"), (32000, 96, 1024, "logits fwd")]:
         if only and only not in tag:
             continue
         a = torch.randn(M, Kd, device=dev).to(bf)
