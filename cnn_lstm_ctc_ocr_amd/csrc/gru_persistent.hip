@@ -183,6 +183,7 @@ gru_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ 
     // the epilogue item of this thread: row er, units eu..eu+3
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));                       // settled before the loop (lstm_persistent.hip)
     float hst[4] = {0.f, 0.f, 0.f, 0.f};
     const int xbytes = 2 * 2 * B * H * 2;
     const auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, xbytes, 0x00020000);
@@ -331,6 +332,7 @@ gru_bwd_persistent_kernel(const bf16* __restrict__ whg, const bf16* __restrict__
 
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));                       // settled before the loop (lstm_persistent.hip)
     float dh[4] = {0.f, 0.f, 0.f, 0.f};
     float bsum[3][4] = {};                              // the bias gradients: (dz_r, dz_u, dz_c) summed over steps
     const auto zxc_rsrc = __builtin_amdgcn_make_buffer_rsrc(zxc, 0, 2 * 2 * B * H * 2, 0x00020000);

@@ -157,6 +157,10 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     // ---- the epilogue item of this thread: row er, units eu..eu+3 (all 4 gates)
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
+    // settle the load before the loop: its first use inside the loop otherwise made
+    // the waitcnt pass drain every outstanding load there, every step (vmcnt(0));
+    // measured 2.74 -> 2.64 us/step forward, 3.51 -> 3.39 BPTT (the same below)
+    asm volatile("" ::"v"(elen));
     float cst[4] = {0.f, 0.f, 0.f, 0.f}, hst[4] = {0.f, 0.f, 0.f, 0.f};
     float bsr[fx ? 4 : 1][4];                           // fused: the projection bias of the thread's 16 gate columns
     if constexpr (fx) {
@@ -505,6 +509,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 
     const int er = tid >> 3, eu = 4 * (tid & 7);
     const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));                       // settled before the loop (see the forward)
     float dcs[4] = {0.f, 0.f, 0.f, 0.f};
     float bsum[4][4] = {};                              // the bias gradient: sum of dz over this row's steps
     const int64_t zx_elems = (int64_t)2 * 2 * B * G4;

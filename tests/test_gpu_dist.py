@@ -6,8 +6,10 @@ RCCL run is the driver's), each rank a different batch shard: the bucketed
 all-reduce -- recurrent bucket started from the hook on the conv tower's
 output gradient, on a comm stream that waits for the side-stream weight
 gradients -- times 1/world must equal the mean of the two shards' gradients
-computed one process at a time. fp32, per-step recurrent kernels (two
-processes' persistent grids cannot both be co-resident on one GPU)."""
+computed one process at a time; and a whole Trainer.step leaves both ranks
+with the same parameters, the Adam update of the mean gradient. fp32,
+per-step recurrent kernels (two processes' persistent grids cannot both be
+co-resident on one GPU)."""
 import os
 import socket
 
@@ -69,3 +71,47 @@ def test_two_rank_train_step_gradient_equals_mean_of_shards(cuda, tmp_path):
     want = (ref[0] + ref[1]) / 2
     err = np.linalg.norm(g0 - want) / np.linalg.norm(want)
     assert err < 1e-5, err
+
+
+def _step_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OCRK_LSTM_PERSISTENT="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    dev = torch.device("cuda:0")
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=SIZES, dtype=torch.float32), device=dev, seed=5)
+    tr = Trainer(store)
+    img, labels = _shard(rank)
+    tr.step(torch.from_numpy(img).to(dev), np.full(B, W, np.int32), labels)
+    torch.cuda.synchronize()
+    np.save(os.path.join(outdir, f"p{rank}.npy"), store.flat.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_train_step_updates_agree(cuda, tmp_path):
+    import torch.multiprocessing as mp
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_step_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
+    np.testing.assert_array_equal(p0, p1)
+    # reference: the mean of the two shards' gradients, one Adam launch in one process
+    g = []
+    for r in range(2):
+        store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=SIZES, dtype=torch.float32), device=cuda, seed=5)
+        g.append(_grads(store, Trainer(store), r, cuda))
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=SIZES, dtype=torch.float32), device=cuda, seed=5)
+    p_init = store.flat.cpu().numpy()
+    tr = Trainer(store)
+    store.flat_grad.copy_(torch.from_numpy((g[0] + g[1]) / 2).to(cuda))
+    tr.apply_gradients()
+    torch.cuda.synchronize()
+    d_ref = store.flat.cpu().numpy() - p_init
+    d = p0 - p_init
+    assert np.linalg.norm(d - d_ref) <= 1e-3 * np.linalg.norm(d_ref)
