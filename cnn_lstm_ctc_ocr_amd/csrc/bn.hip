@@ -370,20 +370,29 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
                 for (int i = 0; i < 8; ++i) { zr[j][dh][i] = v.v[i]; dr[j][dh][i] = 0.f; }
             }
+        auto dp_off = [&](int wo) {
+            return dp_time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
+                                 : (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+        };
+        // the pooled gradient is prefetched a window ahead like the z columns: the
+        // window's compute then waits only for loads issued a window earlier (in-order
+        // vmcnt), not for the loads just issued (a same-window dp load behind the
+        // prefetch made every window wait vmcnt(0))
+        F8 gp = load8(dp + dp_off(wfirst));
         for (int wo = wfirst; wo < wb; ++wo) {
             const int x0 = wo * SW;
-            // next window's new columns and this window's pooled gradient in flight first
-            F8 nz[SW][KH];
+            // next window's pooled gradient and new columns in flight first, kept raw
+            // (converted when they enter the window, after this window's work)
+            Pend8<T> nz[SW][KH];
+            Pend8<T> gpn;
             const bool more = wo + 1 < wb;
             if (more) {
+                gpn = load_pend8(dp + dp_off(wo + 1));
 #pragma unroll
                 for (int j = 0; j < SW; ++j)
 #pragma unroll
-                    for (int dh = 0; dh < KH; ++dh) nz[j][dh] = load8(zrow + ((int64_t)dh * W + x0 + KW + j) * C);
+                    for (int dh = 0; dh < KH; ++dh) nz[j][dh] = load_pend8(zrow + ((int64_t)dh * W + x0 + KW + j) * C);
             }
-            const int64_t o = dp_time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
-                                            : (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
-            const F8 gp = load8(dp + o);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 float best = -INFINITY;
@@ -405,6 +414,7 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
             for (int j = 0; j < SW; ++j) retire(x0 + j, zr[j], dr[j]);
             if (!more) break;
+            gp = cvt8(gpn);
 #pragma unroll
             for (int j = 0; j + SW < KW; ++j)
 #pragma unroll
@@ -414,12 +424,14 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
             for (int j = 0; j < SW; ++j)
 #pragma unroll
-                for (int dh = 0; dh < KH; ++dh)
+                for (int dh = 0; dh < KH; ++dh) {
+                    const F8 v = cvt8(nz[j][dh]);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        zr[KW - SW + j][dh][i] = nz[j][dh].v[i];
+                        zr[KW - SW + j][dh][i] = v.v[i];
                         dr[KW - SW + j][dh][i] = 0.f;
                     }
+                }
         }
         // columns still in the last window, then the uncovered ones on the right
         const int xl = (wb - 1) * SW;

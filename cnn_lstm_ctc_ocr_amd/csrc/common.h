@@ -94,6 +94,31 @@ template <> __device__ __forceinline__ F8 load8<bf16>(const bf16* p) {
     for (int i = 0; i < 8; ++i) r.v[i] = (float)u.e[i];
     return r;
 }
+// The raw bytes of 8 elements, converted to fp32 only at use (cvt8): a prefetch
+// kept raw does not make the compiler wait for its load where it is issued (a
+// load8 converts at once, so its wait lands right behind the load).
+template <typename T> struct Pend8;
+template <> struct Pend8<float> { float4 a, b; };
+template <> struct Pend8<bf16> { uint4 q; };
+template <typename T> __device__ __forceinline__ Pend8<T> load_pend8(const T* p);
+template <> __device__ __forceinline__ Pend8<float> load_pend8<float>(const float* p) {
+    return Pend8<float>{reinterpret_cast<const float4*>(p)[0], reinterpret_cast<const float4*>(p)[1]};
+}
+template <> __device__ __forceinline__ Pend8<bf16> load_pend8<bf16>(const bf16* p) {
+    return Pend8<bf16>{*reinterpret_cast<const uint4*>(p)};
+}
+__device__ __forceinline__ F8 cvt8(const Pend8<float>& r) {
+    return F8{{r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w}};
+}
+__device__ __forceinline__ F8 cvt8(const Pend8<bf16>& r) {
+    union { uint4 q; bf16 e[8]; } u;
+    u.q = r.q;
+    F8 f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.v[i] = (float)u.e[i];
+    return f;
+}
+
 template <typename T> __device__ __forceinline__ void store8(T* p, const F8& x);
 template <> __device__ __forceinline__ void store8<float>(float* p, const F8& x) {
     reinterpret_cast<float4*>(p)[0] = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
