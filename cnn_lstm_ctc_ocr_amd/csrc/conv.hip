@@ -395,12 +395,24 @@ extern "C" int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, i
     return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, slab, dtype, ocrk::as_stream(stream));
 }
 
+// Item cap of the 256 x 256 weight-gradient launches (OCRK_CONV_TN_ITEMS,
+// default 256 = one round on the chip): they run beside the main stream's BN
+// backward, whose kernels cannot share a CU with an item (VGPRs).
+static int conv_tn_items() {
+    static const int n = [] {
+        const char* e = getenv("OCRK_CONV_TN_ITEMS");
+        const int v = e ? atoi(e) : 256;
+        return v >= 16 ? v : 256;
+    }();
+    return n;
+}
+
 static int wgrad_splits(int64_t M, int cin, int cout) {
     // enough partial tiles to cover the chip ~2x (the 256 x 256 ping-pong
     // engine: ~1x, one item per CU); each split >= 4096 pixels
     if (ocrk::gemm_pptn_covers(ocrk::A_IM2COL_T, 9 * cin, cout, cin)) {
         const int64_t tiles = ocrk::cdiv(9 * cin, 256) * ocrk::cdiv(cout, 256);
-        return (int)std::max<int64_t>(1, std::min<int64_t>(256 / tiles, M / 2048));   // items <= 256: one round
+        return (int)std::max<int64_t>(1, std::min<int64_t>(conv_tn_items() / tiles, M / 2048));
     }
     int64_t tiles = ocrk::cdiv(9 * cin, 128) * ocrk::cdiv(cout, cout <= 32 ? 32 : (cout <= 64 ? 64 : 128));
     int64_t want = ocrk::cdiv(512, tiles);

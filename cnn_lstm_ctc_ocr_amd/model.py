@@ -315,10 +315,10 @@ class _BiLSTM(torch.autograd.Function):
                 def dw_x():
                     K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
                            ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
-                           splits=_splits(n_in, G4, R, batch=2))
+                           splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer)))
                 K.gemm(hprev.view(R, 2 * H), dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G4, K=R,
                        lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4, stride_c=sk,
-                       splits=_splits(H, G4, R, batch=2))
+                       splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
                 if layer > 1 and _DEFER_DWX and ctx.needs_input_grad[0]:
                     store.deferred.append((dw_x, (x, dG)))   # issued behind the next BPTT (fewer CUs held)
                 else:
@@ -327,9 +327,9 @@ class _BiLSTM(torch.autograd.Function):
                 for d, gk in enumerate((gf, gb)):
                     dgd = dg[:, d * G4:]                                         # view, ldb = 8H
                     K.gemm(x, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
-                           ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R))
+                           ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R, items=_tn_items(layer)))
                     K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
-                           M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R))
+                           M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R, items=_tn_items(layer)))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
@@ -381,14 +381,14 @@ class _BiGRU(torch.autograd.Function):
             dg = dG.view(R, 2 * G3)
             hp, rhv = hprev.view(R, 2 * H), rh.view(R, 2 * H)
             K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G2, K=R, lda=n_in, ldb=2 * G3,
-                   ldc=G2, batch=2, stride_a=0, stride_b=G3, stride_c=sk, splits=_splits(n_in, G2, R, batch=2))
+                   ldc=G2, batch=2, stride_a=0, stride_b=G3, stride_c=sk, splits=_splits(n_in, G2, R, batch=2, items=_tn_items(layer)))
             K.gemm(hp, dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G2, K=R, lda=2 * H, ldb=2 * G3,
-                   ldc=G2, batch=2, stride_a=H, stride_b=G3, stride_c=sk, splits=_splits(H, G2, R, batch=2))
+                   ldc=G2, batch=2, stride_a=H, stride_b=G3, stride_c=sk, splits=_splits(H, G2, R, batch=2, items=_tn_items(layer)))
             K.gemm(x, dg[:, G2:], trans_a=True, out=cf, accumulate=True, M=n_in, N=H, K=R, lda=n_in,
                    ldb=2 * G3, ldc=H, batch=2, stride_a=0, stride_b=G3, stride_c=sk,
-                   splits=_splits(n_in, H, R, batch=2))
+                   splits=_splits(n_in, H, R, batch=2, items=_tn_items(layer)))
             K.gemm(rhv, dg[:, G2:], trans_a=True, out=cf[n_in:], accumulate=True, M=H, N=H, K=R, lda=2 * H,
-                   ldb=2 * G3, ldc=H, batch=2, stride_a=H, stride_b=G3, stride_c=sk, splits=_splits(H, H, R, batch=2))
+                   ldb=2 * G3, ldc=H, batch=2, stride_a=H, stride_b=G3, stride_c=sk, splits=_splits(H, H, R, batch=2, items=_tn_items(layer)))
         for d, dn in enumerate(() if batched else ("fw", "bw")):
             gk = store.grads[f"{pre}/{dn}/gru_cell/gates/kernel"]               # [In+H, 2H]
             ck = store.grads[f"{pre}/{dn}/gru_cell/candidate/kernel"]           # [In+H, H]
@@ -397,13 +397,13 @@ class _BiGRU(torch.autograd.Function):
             hp = hprev.view(R, 2 * H)[:, d * H:]
             rhd = rh.view(R, 2 * H)[:, d * H:]
             K.gemm(x, dgg, trans_a=True, out=gk, accumulate=True, M=n_in, N=G2, K=R, lda=n_in,
-                   ldb=2 * G3, ldc=G2, splits=_splits(n_in, G2, R))
+                   ldb=2 * G3, ldc=G2, splits=_splits(n_in, G2, R, items=_tn_items(layer)))
             K.gemm(hp, dgg, trans_a=True, out=gk[n_in:], accumulate=True, M=H, N=G2, K=R, lda=2 * H,
-                   ldb=2 * G3, ldc=G2, splits=_splits(H, G2, R))
+                   ldb=2 * G3, ldc=G2, splits=_splits(H, G2, R, items=_tn_items(layer)))
             K.gemm(x, dgc, trans_a=True, out=ck, accumulate=True, M=n_in, N=H, K=R, lda=n_in,
-                   ldb=2 * G3, ldc=H, splits=_splits(n_in, H, R))
+                   ldb=2 * G3, ldc=H, splits=_splits(n_in, H, R, items=_tn_items(layer)))
             K.gemm(rhd, dgc, trans_a=True, out=ck[n_in:], accumulate=True, M=H, N=H, K=R, lda=2 * H,
-                   ldb=2 * G3, ldc=H, splits=_splits(H, H, R))
+                   ldb=2 * G3, ldc=H, splits=_splits(H, H, R, items=_tn_items(layer)))
         side.__exit__(None, None, None)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -412,9 +412,16 @@ class _BiGRU(torch.autograd.Function):
 
 
 _TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
+# the lowest layer's weight gradients run beside the conv backward's main-stream
+# kernels, which cannot share a CU with a 256 x 256 TN item (VGPRs): its own cap
+_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", str(_TN_ITEMS)))
 
 
-def _splits(M, N, Kdim, batch=1):
+def _tn_items(layer):
+    return _TN_ITEMS_L1 if layer == 1 else _TN_ITEMS
+
+
+def _splits(M, N, Kdim, batch=1, items=None):
     """K slices for a weight-gradient GEMM (f32 partials + a fixed-order
     reduce): enough items for the chip. M, N >= 256 run on the 256 x 256
     ping-pong TN engine (one item per CU, slices of >= 1024 rows), smaller
@@ -425,7 +432,7 @@ def _splits(M, N, Kdim, batch=1):
     5.374-5.402 vs 5.416-5.426 ms, 320 / 384 / 512 5.45 / 5.44-5.48 / 5.56-5.58)."""
     if M >= 256 and N >= 256:
         tiles = -(-M // 256) * -(-N // 256) * batch
-        return int(max(1, min(_TN_ITEMS // tiles, Kdim // 1024)))      # <= 256 items: one round on the chip
+        return int(max(1, min((items or _TN_ITEMS) // tiles, Kdim // 1024)))      # <= 256 items: one round on the chip
     tiles = -(-M // 128) * -(-N // 128) * batch
     return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
 
