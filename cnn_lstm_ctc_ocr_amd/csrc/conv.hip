@@ -395,14 +395,16 @@ extern "C" int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, i
     return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, slab, dtype, ocrk::as_stream(stream));
 }
 
-// Item cap of the 256 x 256 weight-gradient launches (OCRK_CONV_TN_ITEMS,
-// default 256 = one round on the chip): they run beside the main stream's BN
-// backward, whose kernels cannot share a CU with an item (VGPRs).
+// Item cap of the 256 x 256 weight-gradient launches (OCRK_CONV_TN_ITEMS):
+// they run on the side stream beside the main stream's BN backward and data
+// gradients, whose kernels cannot share a CU with an item (VGPRs), so 192
+// items (of 256 CUs) leave those 64 CUs. Same-box A/B of the step: 5.241-5.248
+// ms vs 5.266-5.281 at 256 (one round on the chip); 224: 5.27, 160: 5.24-5.27.
 static int conv_tn_items() {
     static const int n = [] {
         const char* e = getenv("OCRK_CONV_TN_ITEMS");
-        const int v = e ? atoi(e) : 256;
-        return v >= 16 ? v : 256;
+        const int v = e ? atoi(e) : 192;
+        return v >= 16 ? v : 192;
     }();
     return n;
 }

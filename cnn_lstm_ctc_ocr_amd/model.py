@@ -315,7 +315,7 @@ class _BiLSTM(torch.autograd.Function):
                 def dw_x():
                     K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
                            ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
-                           splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer)))
+                           splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer, late=True)))
                 K.gemm(hprev.view(R, 2 * H), dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G4, K=R,
                        lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4, stride_c=sk,
                        splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
@@ -413,12 +413,23 @@ class _BiGRU(torch.autograd.Function):
 
 _TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
 # the lowest layer's weight gradients run beside the conv backward's main-stream
-# kernels, which cannot share a CU with a 256 x 256 TN item (VGPRs): its own cap
-_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", str(_TN_ITEMS)))
+# kernels (BN backward: 175-212 VGPRs), which cannot share a CU with a 256 x 256
+# TN item (2 waves x 216 VGPRs per SIMD): 192 items leave them 64 CUs. Same-box
+# A/B (with the conv weight gradients at 192 too, csrc/conv.hip): 5.215-5.228 vs
+# 5.286-5.288 ms per step; 160: 5.215-5.225, 176: 5.26, 224: 5.25
+_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", "192"))
 
 
-def _tn_items(layer):
-    return _TN_ITEMS_L1 if layer == 1 else _TN_ITEMS
+# an upper layer's dW_x is queued behind the lower BPTT and meets the lower layer's
+# data gradient when that BPTT ends (OCRK_TN_ITEMS_LATE: its own cap; 192: 5.28,
+# 128: 5.34 vs 5.27-5.30 ms at 256)
+_TN_ITEMS_LATE = int(os.environ.get("OCRK_TN_ITEMS_LATE", str(_TN_ITEMS)))
+
+
+def _tn_items(layer, late=False):
+    if layer == 1:
+        return _TN_ITEMS_L1
+    return _TN_ITEMS_LATE if late else _TN_ITEMS
 
 
 def _splits(M, N, Kdim, batch=1, items=None):

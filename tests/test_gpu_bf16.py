@@ -289,14 +289,18 @@ def test_bf16_train_step_at_bench_shape_vs_float64(cuda, cell, sizes):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("cell,layer", [("lstm", 1), ("lstm", 2), ("gru", 1), ("gru", 2)])
-def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer):
+@pytest.mark.parametrize("cell,layer,items", [("lstm", 1, None), ("lstm", 2, None), ("gru", 1, None), ("gru", 2, None),
+                                              ("lstm", 1, 128), ("lstm", 2, 128)])
+def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer, items):
     """The recurrent weight-gradient launches exactly as model._BiLSTM /
     _BiGRU.backward issue them at the bench's R = T*B = 32000 rows (batched
     direction pairs, stride_a / stride_b / stride_c, model._splits' split-K
-    counts), into a non-zero f32 gradient (accumulate) -- against float64."""
+    counts under the model's item caps, or a 128-item cap), into a non-zero
+    f32 gradient (accumulate) -- against float64."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    from cnn_lstm_ctc_ocr_amd.model import _splits
+    from cnn_lstm_ctc_ocr_amd.model import _splits, _tn_items
+    cap_x = items or _tn_items(layer, late=(cell == "lstm"))
+    cap_h = items or _tn_items(layer)
     R = 32000
     H = 512 if (cell == "lstm" or layer == 1) else 256
     n_in = 256 if layer == 1 else (1024 if cell == "lstm" else 1024)
@@ -311,9 +315,9 @@ def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer):
     gk = torch.from_numpy(prev).to(cuda)
     xd, hd, dd = (torch.from_numpy(a).to(cuda).bfloat16() for a in (x, hp, dG))
     Kn.gemm(xd, dd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G, K=R, lda=n_in, ldb=ld, ldc=G, batch=2,
-            stride_a=0, stride_b=ld // 2, stride_c=sk, splits=_splits(n_in, G, R, batch=2))
+            stride_a=0, stride_b=ld // 2, stride_c=sk, splits=_splits(n_in, G, R, batch=2, items=cap_x))
     Kn.gemm(hd, dd, trans_a=True, out=gk[n_in * G:], accumulate=True, M=H, N=G, K=R, lda=2 * H, ldb=ld, ldc=G,
-            batch=2, stride_a=H, stride_b=ld // 2, stride_c=sk, splits=_splits(H, G, R, batch=2))
+            batch=2, stride_a=H, stride_b=ld // 2, stride_c=sk, splits=_splits(H, G, R, batch=2, items=cap_h))
     got = gk.cpu().numpy().reshape(2, n_in + H, G)
     x64, h64, d64 = x.astype(np.float64), hp.astype(np.float64), dG.astype(np.float64)
     for d in range(2):
@@ -321,4 +325,5 @@ def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer):
         dg = d64[:, d * (ld // 2):d * (ld // 2) + G]
         ref[:n_in] += x64.T @ dg
         ref[n_in:] += h64[:, d * H:(d + 1) * H].T @ dg
-        assert _rel(got[d], ref) < 1e-5, (cell, layer, d, _splits(n_in, G, R, batch=2), _splits(H, G, R, batch=2))
+        assert _rel(got[d], ref) < 1e-5, (cell, layer, d, _splits(n_in, G, R, batch=2, items=cap_x),
+                                          _splits(H, G, R, batch=2, items=cap_h))
