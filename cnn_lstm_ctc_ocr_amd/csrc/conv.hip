@@ -417,7 +417,12 @@ static int wgrad_splits(int64_t M, int cin, int cout) {
         return (int)std::max<int64_t>(1, std::min<int64_t>(conv_tn_items() / tiles, M / 2048));
     }
     int64_t tiles = ocrk::cdiv(9 * cin, 128) * ocrk::cdiv(cout, cout <= 32 ? 32 : (cout <= 64 ? 64 : 128));
-    int64_t want = ocrk::cdiv(512, tiles);
+    static const int items = [] {                        // OCRK_CONV_TN4_ITEMS: experiments
+        const char* e = getenv("OCRK_CONV_TN4_ITEMS");
+        const int v = e ? atoi(e) : 512;
+        return v >= 16 ? v : 512;
+    }();
+    int64_t want = ocrk::cdiv(items, tiles);
     int64_t maxs = std::max<int64_t>(1, M / 4096);
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, maxs));
 }
