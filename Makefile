@@ -17,7 +17,21 @@ build/%.o: $(CSRC)/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-clean:
-	rm -rf build $(LIB)
+# tools-only build: experiment toggles + diagnostics (include/ocrk_debug.h);
+# tools load it with OCRK_LIB=tools/libocrk_exp.so. Never the product library.
+EXPOBJ := $(patsubst $(CSRC)/%.hip,build/exp/%.o,$(SRC))
+EXPLIB := tools/libocrk_exp.so
 
-.PHONY: all clean
+exp: $(EXPLIB)
+
+$(EXPLIB): $(EXPOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(EXPOBJ)
+
+build/exp/%.o: $(CSRC)/%.hip $(HDR)
+	@mkdir -p build/exp
+	$(HIPCC) $(HIPFLAGS) -DOCRK_EXPERIMENTS -c $< -o $@
+
+clean:
+	rm -rf build $(LIB) $(EXPLIB)
+
+.PHONY: all exp clean

@@ -261,27 +261,38 @@ def run_c2(args, world, rank, device):
             "loss": round(float(loss.item()), 4)}, elapsed, world * B * args.steps
 
 
-def run_c5(args, world, rank, device, n_crops=2048, beam=16):
-    """BASELINE configs[4] (C5): variable-width crops batched by the serving
-    path's 32-px width buckets (server.py:28-42,64-65: bucket (w, w+32], crops
-    right-padded with uint8 0 to its upper width), INFER forward + beam-16
-    decode per bucket, fp32. Whole buckets are sharded over the ranks (largest
-    first, round robin) -- replicas, no exchange. value = crops/s of
-    the whole job."""
-    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
-    rng = np.random.default_rng(20265)
+def c5_buckets(n_crops=2048, seed=20265):
+    """BASELINE configs[4] (C5) workload on the host: `n_crops` uint8 crops of
+    true width U{65..512}, batched by the serving path's 32-px width buckets
+    (server.py:28-42,64-65: bucket (w, w+32], crops right-padded with uint8 0 to
+    its upper width). Returns [(upper width, images u8 [n, 32, upper, 1], true
+    widths i32 [n])], largest bucket first. tests/test_gpu_configs.py checks
+    this exact workload against the masked float64 graph."""
+    rng = np.random.default_rng(seed)
     true_w = rng.integers(65, 513, n_crops)
     upper = ((true_w - 1) // 32 + 1) * 32                       # bucket (w, w + 32] -> its upper width
     buckets = sorted({int(u) for u in upper}, key=lambda u: -int((upper == u).sum()))
-    mine = [u for i, u in enumerate(buckets) if i % world == rank]
-    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
-    batches = []
-    for u in mine:
+    out = []
+    for u in buckets:
         idx = np.nonzero(upper == u)[0]
         img = np.zeros((len(idx), 32, u, 1), np.uint8)
         for j, i in enumerate(idx):
             img[j, :, :true_w[i]] = rng.integers(0, 256, (32, true_w[i], 1))
-        batches.append((torch.from_numpy(img).to(device), torch.from_numpy(true_w[idx].astype(np.int32))))
+        out.append((u, img, true_w[idx].astype(np.int32)))
+    return out
+
+
+def run_c5(args, world, rank, device, n_crops=2048, beam=16):
+    """BASELINE configs[4] (C5): c5_buckets' variable-width crops, INFER
+    forward + beam-16 decode per bucket, fp32. Whole buckets are sharded over
+    the ranks (largest first, round robin) -- replicas, no exchange (SURVEY
+    8e). value = crops/s of the whole job."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
+    allb = c5_buckets(n_crops)
+    buckets = [u for u, _, _ in allb]
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
+    batches = [(torch.from_numpy(img).to(device), torch.from_numpy(w))
+               for i, (_u, img, w) in enumerate(allb) if i % world == rank]
 
     def run():
         out = []

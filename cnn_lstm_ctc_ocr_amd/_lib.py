@@ -88,7 +88,6 @@ SIGNATURES = {
     "ocrk_lstm_bwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_bwd_persistent_workspace_size": [_i32, _i32],
     "ocrk_lstm_bwd_persistent": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
-    "ocrk_lstm_debug_stamps": [_p],
     "ocrk_lstm_fwd": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_gemm_workspace_size": [_i32, _i32, _i32, _i32],
@@ -175,6 +174,9 @@ def raise_for_status(word):
     raise InvalidArgumentError(OCRK_ERR_INFEASIBLE, f"device status 0x{word:x}: {text}")
 
 
+# include/ocrk_debug.h (exported only by tools/libocrk_exp.so, `make exp`)
+DEBUG_SIGNATURES = {"ocrk_lstm_debug_stamps": [_p]}
+
 _lib = None
 
 
@@ -190,6 +192,9 @@ def lib():
             fn = getattr(handle, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        for name, argtypes in DEBUG_SIGNATURES.items():     # include/ocrk_debug.h: tools build only
+            if hasattr(handle, name):
+                getattr(handle, name).argtypes = argtypes
         _lib = handle
     return _lib
 

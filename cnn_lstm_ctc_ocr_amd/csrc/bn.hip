@@ -583,11 +583,10 @@ static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::c
 // [3,1]/[3,1]); 0 = use the pixel-centric kernel. OCRK_BN_ROUTE=0 disables it.
 constexpr int BN_ROUTE_SEG = 8;
 static int bn_route_variant(int kh, int kw, int sh, int sw, int H, int W) {
-    static int on = -1;
-    if (on < 0) {
+    static const int on = [] {                 // thread-safe once
         const char* e = getenv("OCRK_BN_ROUTE");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     if (!on || sh != kh || H < kh || W < kw) return 0;
     if (kh == 2 && kw == 2 && sw == 2) return 1;
     if (kh == 2 && kw == 2 && sw == 1) return 2;

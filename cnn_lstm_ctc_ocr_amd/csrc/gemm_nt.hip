@@ -362,18 +362,20 @@ int launch_nt(const GemmParams& p, hipStream_t stream) {
 //   9: 256 x 256 x 32 / 4, 8 waves -> 128 KB       10: 256 x 128 x 32 / 4, 8 waves -> 64 KB -> 2
 //  11: 128 x 128 x 32 / 6 -> 96 KB -> 1           12: 128 x 128 x 32 / 5 -> 80 KB -> 2
 //  13: 128 x 128 x 64 / 4 -> 128 KB -> 1          14: 128 x 64 x 64 / 3 -> 72 KB -> 2
-int nt_cfg() {
-    static int c = -2;
-    if (c == -2) {
+#ifdef OCRK_EXPERIMENTS
+int nt_cfg() {                                       // tools-only build (make exp)
+    static const int c = [] {
         const char* e = getenv("OCRK_GEMM_NT_CFG");
-        c = e ? atoi(e) : -1;
-    }
+        return e ? atoi(e) : -1;
+    }();
     return c;
 }
+#endif
 
 template <int AM>
 int dispatch_nt(const GemmParams& p, hipStream_t s) {
-    switch (nt_cfg()) {                                  // experiments (tools/gemm_sweep.sh)
+#ifdef OCRK_EXPERIMENTS
+    switch (nt_cfg()) {                                  // experiments (tools/gemm_sweep.sh, make exp)
         case 0: return launch_nt<256, 128, 64, 3, 2, AM>(p, s);
         case 1: return launch_nt<128, 128, 64, 2, 2, AM>(p, s);
         case 2: return launch_nt<128, 128, 32, 3, 2, AM>(p, s);
@@ -391,6 +393,7 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
         case 14: return launch_nt<128, 64, 64, 3, 2, AM>(p, s);
         default: break;
     }
+#endif
     // measured on MI355X (tools/bench_gemm.py): narrow N -> BK=32, 3 stages;
     // wide N with enough row tiles -> 256 x 256 (8 waves); else 128 x 128 x 64, 2 stages
     if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM>(p, s);
@@ -402,20 +405,18 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_nt_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_GEMM_NT");      // OCRK_GEMM_NT=0: generic engine only
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+    static const int on = [] {                 // thread-safe once OCRK_GEMM_NT=0: generic engine only
+        const char* e = getenv("OCRK_GEMM_NT");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     return on == 1;
 }
 
 bool nt_staged_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_GEMM_NT_STAGED");      // OCRK_GEMM_NT_STAGED=0: direct 2-B stores
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+    static const int on = [] {                 // thread-safe once OCRK_GEMM_NT_STAGED=0: direct 2-B stores
+        const char* e = getenv("OCRK_GEMM_NT_STAGED");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     return on == 1;
 }
 

@@ -522,11 +522,10 @@ int dispatch_pp(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_pp_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_GEMM_PP");      // OCRK_GEMM_PP=0: previous engines only
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+    static const int on = [] {                 // thread-safe once OCRK_GEMM_PP=0: previous engines only
+        const char* e = getenv("OCRK_GEMM_PP");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     return on == 1;
 }
 
@@ -540,8 +539,12 @@ int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
     if (!p.c_bf16 || p.accumulate || p.splits != 1) return -1;
     if (p.N % 8 != 0 || p.K % 8 != 0) return -1;
     if ((int64_t)p.M < 4096) return -1;
+#ifdef OCRK_EXPERIMENTS
     static const int all = [] { const char* e = getenv("OCRK_GEMM_PP"); return e && e[0] == '2'; }();
-    if (!all && (amode != A_ROWK || p.N < 512)) return -1;         // OCRK_GEMM_PP=2: every shape (experiments)
+#else
+    constexpr int all = 0;
+#endif
+    if (!all && (amode != A_ROWK || p.N < 512)) return -1;         // OCRK_GEMM_PP=2: every shape (make exp)
     if (p.N < 96) return -1;
     // 32-bit buffer offsets
     const int64_t a_bytes = (amode == A_ROWK ? (int64_t)p.M * p.lda : (int64_t)p.M * p.convC) * 2;

@@ -291,11 +291,10 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
 }  // namespace
 
 bool gemm_pptn_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("OCRK_GEMM_PPTN");        // OCRK_GEMM_PPTN=0: the 4-wave TN engine
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+    static const int on = [] {                 // thread-safe once OCRK_GEMM_PPTN=0: the 4-wave TN engine
+        const char* e = getenv("OCRK_GEMM_PPTN");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     return on == 1;
 }
 

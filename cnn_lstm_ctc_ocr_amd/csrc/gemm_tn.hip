@@ -241,22 +241,25 @@ int launch_tn(const GemmParams& p, hipStream_t stream) {
     return launch_status("gemm_tn");
 }
 
+#ifdef OCRK_EXPERIMENTS
 int tn_stages() {                                    // OCRK_GEMM_TN_STAGES=3: 3-stage ring (experiments)
-    static int st = -1;
-    if (st < 0) {
+    static const int st = [] {                 // thread-safe once
         const char* e = getenv("OCRK_GEMM_TN_STAGES");
-        st = (e && e[0] == '3') ? 3 : 2;
-    }
+        return (e && e[0] == '3') ? 3 : 2;
+    }();
     return st;
 }
+#endif
 
 template <int AM>
 int dispatch_tn(const GemmParams& p, hipStream_t s) {
+#ifdef OCRK_EXPERIMENTS
     if (tn_stages() == 3) {
         if (p.N <= 32) return launch_tn<128, 32, 64, 3, 4, AM>(p, s);
         if (p.N <= 64) return launch_tn<128, 64, 64, 3, 2, AM>(p, s);
         return launch_tn<128, 128, 64, 3, 2, AM>(p, s);
     }
+#endif
     if (p.N <= 32) return launch_tn<128, 32, 64, 2, 4, AM>(p, s);
     if (p.N <= 64) return launch_tn<128, 64, 64, 2, 2, AM>(p, s);
     return launch_tn<128, 128, 64, 2, 2, AM>(p, s);
@@ -265,11 +268,10 @@ int dispatch_tn(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_tn_enabled() {
-    static int on = -1;
-    if (on < 0) {
+    static const int on = [] {                 // thread-safe once
         const char* e = getenv("OCRK_GEMM_TN");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     return on == 1;
 }
 

@@ -548,7 +548,10 @@ lstm_bwd_step_dma_kernel(const bf16* __restrict__ wh, const bf16* __restrict__ d
 // ------------------------------------------------------------------ C ABI
 long long* g_lstm_dbg = nullptr;   // diagnostics only (ocrk_lstm_debug_stamps)
 
+#ifdef OCRK_EXPERIMENTS
+// include/ocrk_debug.h: exported by the tools-only build (make exp) alone
 extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return OCRK_OK; }
+#endif
 
 // GEMM blocks (2 x 64 rows x 2H bytes) + gx tile (8 KB) + c tile (4 KB)
 static constexpr int lstm_fwd_dma_lds(int H) { return 2 * 64 * 2 * H + 64 * 64 * 2 + 64 * 16 * 4; }

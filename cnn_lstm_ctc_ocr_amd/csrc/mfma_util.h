@@ -96,11 +96,15 @@ __device__ __forceinline__ i32x4_t uniform_rsrc_words(const void* base, int64_t 
 // schedule that keeps DMAs in flight across phases. Hidden from it, the caller's
 // counted vm_wait<N> + barriers are the only ordering (RAW and WAR as the
 // schedule states), and the compiler's own vmcnt waits only over-count.
+// The LDS address is an operand bound to m0 itself ("{m0}"): the compiler writes
+// m0 and knows it is live, so no reserved-register clobber is needed (a clobber
+// list naming m0 "may not be preserved"); the s_nop covers the m0 -> LDS-DMA
+// hazard, which the compiler cannot see inside the asm.
 __device__ __forceinline__ void lds_dma16_asm(const i32x4_t& r, void* lds, unsigned voff) {
     const unsigned a = __builtin_amdgcn_readfirstlane(
         (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-                 :: "v"(voff), "s"(r), "s"(a) : "memory", "m0");
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :: "v"(voff), "s"(r), "{m0}"(a) : "memory");
 }
 
 }  // namespace ocrk

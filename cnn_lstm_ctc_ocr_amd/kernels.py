@@ -288,12 +288,15 @@ def persistent_flags(kind, B, H, device):
 
 
 def reset_persistent_flags():
-    """Re-zero every kept hand-off buffer (after a device error: a loop that gave
-    up leaves its members' counts unequal). In place, so captured graphs stay valid."""
+    """Re-zero every kept hand-off buffer after a device error. Defensive: every
+    member of a loop that gave up still posts all of its flags, so the counts
+    stay equal; but a kernel that faulted or was killed mid-loop would leave
+    them unequal, and the next launch's base would be wrong. In place, so
+    captured graphs stay valid; each owning device is synchronised."""
     for t in _FLAGS.values():
         t.zero_()
-    if _FLAGS:
-        torch.cuda.synchronize()
+    for d in {t.device for t in _FLAGS.values()}:
+        torch.cuda.synchronize(d)
 
 
 _lib.ON_DEVICE_ERROR.append(reset_persistent_flags)

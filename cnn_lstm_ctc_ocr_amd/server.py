@@ -317,7 +317,7 @@ class ReplicaPool:
         self.procs = [ctx.Process(target=_replica_main, args=(r, d, make_recognizer, self.inqs[r], self.outq),
                                   daemon=True) for r, d in enumerate(self.devices)]
         self.assigned = {}                                   # batch id -> replica (in flight)
-        self._pending = []                                   # results read while waiting for control messages
+        self._pending = []                                   # results collected by a poll() that raised
         self._closed = False
         for pr in self.procs:
             pr.start()
@@ -382,23 +382,27 @@ class ReplicaPool:
         self.inqs[r].put((batch_id, np.ascontiguousarray(batch), np.asarray(widths, np.int32)))
 
     def _take(self, msg, out):
+        """File a result into `out`; a batch error is returned (not raised) so
+        poll() can keep the results it has already collected."""
         tag, bid, payload = msg
         if tag == "result":
             self.assigned.pop(bid, None)
             out.append((bid, payload))
         elif tag == "error":
             r = self.assigned.pop(bid, None)
-            raise ReplicaError(f"replica {r} failed on batch {bid}: {payload}")
-        # control messages ("ready", "exit") carry no batch
+            return ReplicaError(f"replica {r} failed on batch {bid}: {payload}")
+        return None                                  # control messages ("ready", "exit") carry no batch
 
     def poll(self, block=False, timeout=600.0):
-        """Finished (batch id, texts) pairs (block: wait for at least one)."""
-        out = []
-        if self._pending:
-            for m in self._pending:
-                self._take(m, out)
-            self._pending = []
-        while True:
+        """Finished (batch id, texts) pairs (block: wait for at least one).
+        A batch that raised in its replica surfaces as ReplicaError; results
+        collected by the same poll are not lost -- they are kept and returned
+        by the next poll()."""
+        out, err = [], None
+        pending, self._pending = self._pending, []
+        for m in pending:
+            err = self._take(m, out) or err
+        while err is None:
             try:
                 msg = self.outq.get_nowait()
             except queue.Empty:
@@ -406,9 +410,12 @@ class ReplicaPool:
                     return out
                 msg = self._get(time.time() + timeout)
                 if msg is None:
+                    self._pending = [("result", bid, texts) for bid, texts in out]
                     raise ReplicaError(f"no result from the replicas within {timeout:.0f} s "
                                        f"({len(self.assigned)} batches in flight)")
-            self._take(msg, out)
+            err = self._take(msg, out)
+        self._pending = [("result", bid, texts) for bid, texts in out]
+        raise err
 
     def close(self):
         self._closed = True

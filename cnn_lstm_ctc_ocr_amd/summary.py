@@ -30,8 +30,10 @@ class SummaryWriter:
             self._fh = open(path, "a", buffering=1)
 
     def scalars(self, step, **values):
-        """Record scalars for `step`; values may be numbers or 0-d / 1-element
-        tensors (device tensors are copied without a sync)."""
+        """Record scalars for `step`; values may be numbers, 0-d / 1-element
+        tensors (device tensors are copied without a sync) or zero-argument
+        callables evaluated once the record's device work has landed (e.g. a
+        rate from two timing events recorded before this call)."""
         if not self.enabled:
             return
         host, ev = {}, None
@@ -47,6 +49,8 @@ class SummaryWriter:
                     host[tag] = float(v.detach().reshape(-1)[0])
             else:
                 host[tag] = v
+                if callable(v) and ev is None and torch.cuda.is_available():
+                    ev = torch.cuda.Event()
         if ev is not None:
             ev.record(torch.cuda.current_stream())
         self._pending.append((ev, int(step), host, time.time()))
@@ -64,7 +68,7 @@ class SummaryWriter:
             self._pending.popleft()
             rec = {"step": step}
             for tag, v in host.items():
-                rec[tag] = float(v[0]) if isinstance(v, torch.Tensor) else v
+                rec[tag] = float(v[0]) if isinstance(v, torch.Tensor) else (v() if callable(v) else v)
             rec["wall_time"] = round(wall, 6)
             self._fh.write(json.dumps(rec) + "\n")
 

@@ -83,12 +83,32 @@ class GradBuckets:
             self.work.wait()
             self.work = None
         if g.is_cuda:
-            # every rank gets the same device status word (MAX over ranks) for
+            # every rank gets the same device status word (the OR over ranks) for
             # this step, so a device error raises on all ranks at the same step
             # (Trainer.poll_status) instead of one rank raising while its peers
-            # block in the next collective (ADVICE r2)
-            dist.all_reduce(K.status_word(g.device), op=dist.ReduceOp.MAX, group=self.group)
+            # block in the next collective
+            or_allreduce_status(K.status_word(g.device), self.group)
         return 1.0 / world
+
+
+_STATUS_BITS = {}
+
+
+def or_allreduce_status(word, group=None):
+    """OR the int32 status word `word` ([1], a bitmask) over the ranks, in place.
+    A MAX all-reduce of the word itself would keep only the numerically largest
+    rank's word; instead its 31 bits are spread into a one-hot vector, that is
+    MAX-reduced in a separate buffer, and the result is OR-ed back into the word,
+    so every rank's bits -- its own included -- survive. Stream-ordered (no host
+    sync)."""
+    key = word.device
+    if key not in _STATUS_BITS:
+        _STATUS_BITS[key] = torch.arange(31, dtype=torch.int32, device=word.device)
+    bits = _STATUS_BITS[key]
+    vec = torch.bitwise_and(torch.bitwise_right_shift(word, bits), 1)
+    dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=group)
+    word.bitwise_or_(torch.bitwise_left_shift(vec, bits).sum(dtype=torch.int32).view(1))
+    return word
 
 
 def allreduce_mean_scale(flat_grad, group=None):
@@ -114,8 +134,8 @@ class Trainer:
       comes AFTER the bad step's update was applied (its infeasible sequences
       contributed zero gradient and +inf loss). Only the bits read are cleared
       (atomic AND-NOT), so errors of steps still in flight are not lost.
-    * data parallel (world_size > 1): the word is MAX-all-reduced with the
-      gradients, and every rank reads the copy of the step `status_lag` (2)
+    * data parallel (world_size > 1): the word is OR-all-reduced with the
+      gradients (or_allreduce_status), and every rank reads the copy of the step `status_lag` (2)
       steps back, waiting for it if needed -- all ranks raise at the same
       step, none is left blocking in a collective."""
 
@@ -205,19 +225,34 @@ class Trainer:
         return loss
 
     def summarize(self, loss, lr, batch):
-        """JSONL scalars every `summary_every` steps (train.py:139)."""
+        """JSONL scalars every `summary_every` steps (train.py:139).
+
+        The record's step is the post-increment global_step, as TF's summary of
+        `sess.run([train_op, global_step])`; `lr` is the rate that step's update
+        used (exponential_decay of the pre-increment count) and `loss` its loss.
+        crops_per_sec is timed on the DEVICE: an event recorded on the current
+        stream at each summary mark, the rate read from the two events' elapsed
+        time once the writer's copies have landed (no sync in the loop)."""
         if self.summary is None:
             return
-        now = time.perf_counter()
+        dev = self.store.device
+        if dev.type == "cuda":
+            now = torch.cuda.Event(enable_timing=True)
+            now.record(torch.cuda.current_stream(dev))
+        else:
+            now = time.perf_counter()
         if self._summary_mark is None:
-            self._summary_mark = (self.global_step - 1, now)
+            self._summary_mark = (self.global_step, now)
         if self.global_step % self.summary_every:
             return
         s0, t0 = self._summary_mark
         crops = (self.global_step - s0) * batch * self.world_size()
         vals = {"learning_rate": lr, "loss": loss}
-        if now > t0 and self.global_step > s0:
-            vals["crops_per_sec"] = round(crops / (now - t0), 2)
+        if self.global_step > s0:
+            if dev.type == "cuda":
+                vals["crops_per_sec"] = lambda: round(crops / max(t0.elapsed_time(now) / 1e3, 1e-9), 2)
+            elif now > t0:
+                vals["crops_per_sec"] = round(crops / (now - t0), 2)
         self.summary.scalars(self.global_step, **vals)
         self._summary_mark = (self.global_step, now)
 

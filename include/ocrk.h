@@ -249,9 +249,6 @@ size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
                              const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
                              unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream);
-/* Diagnostics: when buf != NULL every forward step kernel's workgroups write
- * s_memrealtime stamps ([grid][8] int64) into buf (tools/bench_lstm.py). */
-int ocrk_lstm_debug_stamps(long long* buf);
 /* a7 -- rnn_layer with tf.contrib.rnn.GRUCell (src/weinman/model.py:167-199; [TF1] GRUCell:
  * [r, u] = sig([x, h] Wg + bg), c = tanh([x, r*h] Wc + bc), h' = u h + (1 - u) c) under
  * bidirectional_dynamic_rnn(time_major, sequence_length). gx dtype [T][B][2][3H] = x . [Wg_x | Wc_x]
@@ -293,7 +290,7 @@ int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len
  * G = 4H (LSTM) / 3H (GRU): per 32-row batch slice and direction, the sum of the
  * gate gradients dG_t over its rows and steps -- the layer's bias gradient
  * (model_bu.py:173-180 / model.py:170-180, tf.gradients of the [x,h].W + b
- * sums) fused into the loop; the caller sums the B/32 rows (ocrk_colsum)
+ * sums) fused into the loop; the caller sums the B/32 rows (ocrk_slab_sum)
  * instead of reading dG_t again. */
 /* Hand-off words of the persistent loops (the `flags` argument of the four
  * *_persistent entry points above): NULL = they live in the workspace and are

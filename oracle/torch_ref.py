@@ -18,8 +18,14 @@ cell="gru" restates src/weinman/model.py's GRUCell layers for bench --cell gru):
   h' = u h + (1-u) c; model.py:167-199, 213-214) ->
   dense + ReLU logits (:216-220) -> tf.nn.ctc_loss mean (:224-229, blank 95)
   -> autograd backward -> TF1 Adam (train.py:101-141).
-Sequence-length masking is not restated: the baseline batches are full-width
-(every crop 32 x W, seq_len = T), where dynamic_rnn runs every step.
+Sequence-length masking (forward(widths=...)): bidirectional_dynamic_rnn with
+sequence_length (model_bu.py:187-192, model.py:152-163 for seq_len =
+floor((w-2)/2) - 2): each direction is dynamic_rnn -- for steps s >= len the
+output is 0 and the state is carried -- and the backward direction runs on
+reverse_sequence(x, len) (the first len steps of a row reversed, the rest in
+place) with its outputs reversed back the same way. ctc_loss then uses the same
+per-row lengths (model.py:224-229). Without widths every row is full (seq_len =
+T): the fast path the CPU baseline times.
 """
 import math
 
@@ -64,9 +70,12 @@ class TorchRef:
         self.m = {k: torch.zeros_like(self.p[k]) for k in self.train_names}
         self.v = {k: torch.zeros_like(self.p[k]) for k in self.train_names}
         self.step_count = 0
+        self.seq_len = None
 
-    def forward(self, img_u8, training=True):
-        """img_u8 uint8 [B, 32, W, 1] -> logits [T, B, 96]."""
+    def forward(self, img_u8, training=True, widths=None):
+        """img_u8 uint8 [B, 32, W, 1] -> logits [T, B, 96]. widths ([B] true
+        crop widths): the recurrence is masked by seq_len_from_width(widths)
+        (self.seq_len holds it afterwards), else every row runs all T steps."""
         p = self.p
         x = img_u8.permute(0, 3, 1, 2).float() * (1.0 / 255.0) - 0.5          # NCHW, float32 as TF
         x = x.to(self.dtype)
@@ -82,6 +91,12 @@ class TorchRef:
             else:
                 x = q(F.relu(x))
         h = x[:, :, 0, :].permute(2, 0, 1)                                        # [T, B, 256]
+        T, B = h.shape[0], h.shape[1]
+        self.seq_len = None
+        if widths is not None:
+            w = torch.as_tensor(widths, dtype=torch.long).reshape(-1)
+            self.seq_len = ((w - 2) // 2 - 2).clamp(0, T)                        # model.py:152-163
+            return self._masked_rnn(h, self.seq_len)
         for li, H in enumerate(self.rnn_sizes, start=1):
             outs = []
             for d, rev in (("fw", False), ("bw", True)):
@@ -109,6 +124,62 @@ class TorchRef:
             h = torch.cat(outs, dim=2)
         return F.relu(h @ p["rnn/logits/kernel"] + p["rnn/logits/bias"])
 
+    def _masked_rnn(self, h, seq_len):
+        """rnn_layers with sequence_length (model_bu.py:187-199 / model.py:187-199):
+        per direction, x reversed per row by reverse_sequence for bw, a masked
+        dynamic_rnn (output 0 and state carried for s >= len), outputs reversed
+        back; then the logits (:216-220)."""
+        p = self.p
+        T, B = h.shape[0], h.shape[1]
+        s_idx = torch.arange(T)[:, None]
+        valid = s_idx < seq_len[None, :]                                         # [T, B]
+        rev_idx = torch.where(valid, seq_len[None, :] - 1 - s_idx, s_idx)        # reverse_sequence, involution
+        for li, H in enumerate(self.rnn_sizes, start=1):
+            outs = []
+            for d, rev in (("fw", False), ("bw", True)):
+                n_in = h.shape[2]
+                if rev:
+                    xin = h.gather(0, rev_idx[:, :, None].expand(T, B, n_in))
+                else:
+                    xin = h
+                if self.cell == "gru":
+                    pre = f"rnn/bdrnn{li}/{d}/gru_cell/"
+                    gk, gb = p[pre + "gates/kernel"], p[pre + "gates/bias"]
+                    ck, cb = p[pre + "candidate/kernel"], p[pre + "candidate/bias"]
+                    gxt = (xin @ gk[:n_in] + gb).unbind(0)
+                    cxt = (xin @ ck[:n_in] + cb).unbind(0)
+                    hs = h.new_zeros(B, H)
+                    seq = []
+                    for t in range(T):
+                        r, u = torch.sigmoid(gxt[t] + hs @ gk[n_in:]).chunk(2, dim=1)
+                        c = torch.tanh(cxt[t] + (r * hs) @ ck[n_in:])
+                        hn = u * hs + (1 - u) * c
+                        m = valid[t][:, None]
+                        seq.append(torch.where(m, hn, torch.zeros_like(hn)))
+                        hs = torch.where(m, hn, hs)
+                else:
+                    k = p[f"rnn/bdrnn{li}/{d}/lstm_cell/kernel"]
+                    b = p[f"rnn/bdrnn{li}/{d}/lstm_cell/bias"]
+                    gxt = (xin @ k[:n_in] + b).unbind(0)
+                    wh = k[n_in:]
+                    hs = h.new_zeros(B, H)
+                    cs = h.new_zeros(B, H)
+                    seq = []
+                    for t in range(T):
+                        i, j, f, o = (gxt[t] + hs @ wh).chunk(4, dim=1)
+                        cn = torch.sigmoid(f + 1.0) * cs + torch.sigmoid(i) * torch.tanh(j)
+                        hn = torch.sigmoid(o) * torch.tanh(cn)
+                        m = valid[t][:, None]
+                        seq.append(torch.where(m, hn, torch.zeros_like(hn)))
+                        hs = torch.where(m, hn, hs)
+                        cs = torch.where(m, cn, cs)
+                out = torch.stack(seq)
+                if rev:
+                    out = out.gather(0, rev_idx[:, :, None].expand(T, B, H))
+                outs.append(out)
+            h = torch.cat(outs, dim=2)
+        return F.relu(h @ p["rnn/logits/kernel"] + p["rnn/logits/bias"])
+
     def _gru_dir(self, h, pre, H, rev):
         """One direction of the GRU layer; the input halves of both matmuls hoisted."""
         p = self.p
@@ -130,21 +201,21 @@ class TorchRef:
         return torch.stack(seq)
 
     def loss(self, logits, labels, label_len, per_sequence=False):
-        """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised);
-        per_sequence=True: the [B] losses."""
+        """mean over the batch of tf.nn.ctc_loss (blank = C-1, loss not length-normalised)
+        over the last forward's seq_len (all T without widths); per_sequence=True: the [B] losses."""
         T, B, _ = logits.shape
         lp = F.log_softmax(logits, dim=2)
-        seq = torch.full((B,), T, dtype=torch.long)
+        seq = torch.full((B,), T, dtype=torch.long) if self.seq_len is None else self.seq_len
         if per_sequence:
             return F.ctc_loss(lp, labels, seq, label_len, blank=logits.shape[2] - 1, reduction="none")
         return F.ctc_loss(lp, labels, seq, label_len, blank=logits.shape[2] - 1, reduction="sum") / B
 
-    def loss_and_grads(self, img_u8, labels, label_len):
+    def loss_and_grads(self, img_u8, labels, label_len, widths=None):
         """TRAIN-mode forward + backward without an update: (mean loss, {name: grad},
         per-sequence losses [B], logits [T, B, C]) as numpy float64 / self.dtype."""
         for k in self.train_names:
             self.p[k].grad = None
-        logits = self.forward(img_u8, True)
+        logits = self.forward(img_u8, True, widths)
         losses = self.loss(logits, labels, label_len, per_sequence=True)
         loss = losses.sum() / logits.shape[1]
         loss.backward()
@@ -168,17 +239,18 @@ class TorchRef:
                 self.p[k].sub_(lr_t * self.m[k] / (self.v[k].sqrt() + eps))
         return float(loss.detach())
 
-    def greedy(self, img_u8):
+    def greedy(self, img_u8, widths=None):
         """validate._get_output (validate.py:81-92) on CPU: INFER forward +
-        greedy decode (first max, merge repeats, drop blank)."""
+        greedy decode (first max, merge repeats, drop blank) over seq_len."""
         with torch.no_grad():
-            logits = self.forward(img_u8, training=False)
+            logits = self.forward(img_u8, training=False, widths=widths)
         best = logits.argmax(dim=2).t()                                           # [B, T]
+        lens = [logits.shape[0]] * best.shape[0] if self.seq_len is None else self.seq_len.tolist()
         blank = logits.shape[2] - 1
         out = []
-        for row in best.tolist():
+        for row, n in zip(best.tolist(), lens):
             seq, prev = [], -1
-            for k in row:
+            for k in row[:n]:
                 if k != blank and k != prev:
                     seq.append(k)
                 prev = k

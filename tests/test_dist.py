@@ -116,3 +116,26 @@ def test_bucketed_allreduce_over_paramstore_layout():
                             1e-4, 1)
     b, _, _ = G.adam_update(p_.copy(), mean, np.zeros_like(mean), np.zeros_like(mean), 1e-4, 1)
     np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-12)
+
+
+def _status_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cnn_lstm_ctc_ocr_amd.train import or_allreduce_status
+    # rank 0: CTC_INFEASIBLE | LSTM_FWD_TIMEOUT; rank 1: LSTM_BWD_TIMEOUT (include/ocrk.h)
+    word = torch.tensor([0x12 if rank == 0 else 0x20], dtype=torch.int32)
+    or_allreduce_status(word)
+    out[rank] = int(word[0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_status_word_is_or_reduced_over_ranks():
+    """The device status word is a bitmask: the data-parallel reduction keeps
+    every rank's bits (a MAX of the words would leave 0x20 on both ranks and
+    lose the infeasible-label and forward-timeout bits)."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_status_worker, args=(2, port, out), nprocs=2, join=True)
+    assert out[0] == out[1] == 0x32

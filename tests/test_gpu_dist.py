@@ -115,3 +115,46 @@ def test_two_rank_train_step_updates_agree(cuda, tmp_path):
     d_ref = store.flat.cpu().numpy() - p_init
     d = p0 - p_init
     assert np.linalg.norm(d - d_ref) <= 1e-3 * np.linalg.norm(d_ref)
+
+
+def _status_worker(rank, world, port, outdir):
+    """Rank 1's first batch carries an infeasible label as DEVICE tensors (no
+    host check): only its CTC kernel sets CTC_INFEASIBLE. Both ranks must raise
+    InvalidArgumentError in the same Trainer.step call (the OR-reduced word read
+    status_lag = 2 steps back), and step on cleanly afterwards."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OCRK_LSTM_PERSISTENT="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, _lib
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    dev = torch.device("cuda:0")
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=SIZES, dtype=torch.float32), device=dev, seed=5)
+    tr = Trainer(store)
+    img, labels = _shard(rank)
+    x = torch.from_numpy(img).to(dev)
+    wd = torch.full((B,), W, dtype=torch.int32, device=dev)
+    good = (torch.zeros(B, 8, dtype=torch.int32, device=dev), torch.full((B,), 3, dtype=torch.int32, device=dev))
+    good[0][:, :3] = torch.tensor([4, 5, 6], dtype=torch.int32)
+    bad = (torch.full((B, 40), 7, dtype=torch.int32, device=dev), torch.full((B,), 40, dtype=torch.int32, device=dev))
+    raised = []
+    for i in range(6):
+        try:
+            tr.step(x, wd, bad if (i == 0 and rank == 1) else good)
+        except _lib.InvalidArgumentError:
+            raised.append(i)
+    torch.cuda.synchronize()
+    tr.check_status()                                   # nothing left set after the raise
+    np.save(os.path.join(outdir, f"s{rank}.npy"), np.array(raised))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_status_raises_on_every_rank_at_the_same_step(cuda, tmp_path):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_status_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    s0, s1 = np.load(tmp_path / "s0.npy"), np.load(tmp_path / "s1.npy")
+    assert s0.tolist() == s1.tolist() == [3]             # step 0's word, read status_lag = 2 steps later

@@ -461,3 +461,52 @@ def test_torch_cpu_restatement_matches_oracle(cell):
     for name in ("rnn/logits/kernel", "rnn/bdrnn1/bw/" + rnn, "convnet/conv8/batch_norm/gamma",
                  "convnet/conv1/kernel"):
         np.testing.assert_allclose(tr.p[name].grad.numpy(), grads_ref[name], rtol=1e-7, atol=1e-10, err_msg=name)
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_torch_cpu_restatement_masked_matches_oracle(cell):
+    """The sequence_length-masked restatement (oracle/torch_ref.py: dynamic_rnn
+    stop-and-carry, reverse_sequence for the backward direction,
+    model_bu.py:187-192 / model.py:152-163) equals the NumPy oracle on a RAGGED
+    batch: logits (including the zero-output padded steps), the per-row CTC loss
+    over seq_len and gradients through both directions -- the float64 graph
+    the fp32 C5 / ragged GPU tests compare against."""
+    import torch
+
+    from oracle.torch_ref import TorchRef
+    rng = np.random.default_rng(11)
+    sizes = (32, 32) if cell == "lstm" else (32, 16)
+    vals = M.init_params(seed=4, cell=cell, rnn_sizes=sizes)
+    for k in vals:
+        if "_cell/" in k and "kernel" in k:
+            vals[k] = (vals[k] * 20).astype(np.float32)
+    B, W = 4, 96
+    widths = np.array([96, 41, 70, 57], np.int32)                 # seq_len 45, 17, 32, 25
+    img = np.zeros((B, 32, W, 1), np.uint8)
+    for b, w in enumerate(widths):
+        img[b, :, :w] = rng.integers(0, 256, (32, w, 1))
+    labels = [list(rng.integers(0, 95, n)) for n in (6, 3, 5, 4)]
+    ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, cell, sizes)
+    loss_ref, grads_ref, losses_ref, logits_ref, seq_ref = ref.loss_and_grads(
+        G.preprocess(img).astype(np.float64), widths, labels)
+    assert len(set(seq_ref.tolist())) == B
+    tr = TorchRef(vals, sizes, dtype=torch.float64, cell=cell)
+    lab = torch.zeros(B, 6, dtype=torch.long)
+    for i, l in enumerate(labels):
+        lab[i, :len(l)] = torch.tensor(l)
+    ln = torch.tensor([len(l) for l in labels])
+    logits = tr.forward(torch.from_numpy(img), True, widths=widths)
+    assert tr.seq_len.tolist() == seq_ref.tolist()
+    np.testing.assert_allclose(logits.detach().numpy(), logits_ref, rtol=1e-9, atol=1e-9)
+    losses = tr.loss(logits, lab, ln, per_sequence=True)
+    np.testing.assert_allclose(losses.detach().numpy(), losses_ref, rtol=1e-9)
+    (losses.sum() / B).backward()
+    rnn = "lstm_cell/kernel" if cell == "lstm" else "gru_cell/candidate/kernel"
+    for name in ("rnn/logits/kernel", "rnn/bdrnn1/bw/" + rnn, "rnn/bdrnn2/fw/" + rnn, "convnet/conv8/batch_norm/gamma",
+                 "convnet/conv1/kernel"):
+        np.testing.assert_allclose(tr.p[name].grad.numpy(), grads_ref[name], rtol=1e-7, atol=1e-10, err_msg=name)
+    # full widths through the masked route equal the unmasked fast path
+    full = np.full(B, W, np.int32)
+    a = tr.forward(torch.from_numpy(img), False, widths=full).detach().numpy()
+    b = tr.forward(torch.from_numpy(img), False).detach().numpy()
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)

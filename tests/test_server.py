@@ -145,7 +145,7 @@ class _FailingFactory:
             if self.mode == "die":
                 import os
                 os._exit(7)
-            if self.mode == "raise":
+            if self.mode == "raise" or (self.mode == "raise99" and int(widths[0]) == 99):
                 raise ValueError("bad batch")
             return [str(int(w)) for w in widths]
         return rec
@@ -180,3 +180,23 @@ def test_replica_pool_batch_error_names_the_replica():
         pool.submit(1, 5, np.zeros((1, 32, 64, 1), np.uint8), [64])
         with pytest.raises(ReplicaError, match="replica 1 failed on batch 5: ValueError: bad batch"):
             pool.poll(block=True, timeout=60)
+
+
+def test_replica_pool_keeps_results_collected_before_an_error():
+    """A poll() that raises for one replica's batch does not lose the results
+    it had already collected from the other: the next poll() returns them."""
+    import time
+
+    import numpy as np
+    import pytest
+
+    from cnn_lstm_ctc_ocr_amd.server import ReplicaError, ReplicaPool
+    with ReplicaPool(["dev0", "dev1"], _FailingFactory("raise99"), timeout=60) as pool:
+        pool.submit(0, 1, np.zeros((1, 32, 64, 1), np.uint8), [64])
+        pool.submit(1, 2, np.zeros((1, 32, 128, 1), np.uint8), [99])
+        time.sleep(2.0)                                    # both replies queued before the poll
+        with pytest.raises(ReplicaError, match="failed on batch 2"):
+            pool.poll(block=True, timeout=60)
+        got = pool.poll(block=True, timeout=60)
+        assert got == [(1, ["64"])]
+        assert not pool.assigned

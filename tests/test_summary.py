@@ -46,3 +46,14 @@ def test_trainer_summarizes_every_n_steps(tmp_path):
     assert recs[0]["loss"] == 9.0 and recs[1]["loss"] == 7.0
     assert abs(recs[1]["learning_rate"] - 1e-4 * 0.9 ** (3 / 4)) < 1e-12
     assert recs[0]["crops_per_sec"] > 0
+
+
+def test_writer_evaluates_deferred_values(tmp_path):
+    """A callable value (the trainer's device-timed crops/s) is evaluated when
+    the record is written, not when it is queued."""
+    p = tmp_path / "d.jsonl"
+    box = {"v": 1.0}
+    with summary.SummaryWriter(str(p)) as w:
+        w.scalars(3, rate=lambda: box["v"] * 2)
+        box["v"] = 5.0
+    assert summary.read(str(p))[0]["rate"] in (2.0, 10.0)

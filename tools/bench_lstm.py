@@ -1,6 +1,8 @@
 """Micro-benchmark of the recurrent step kernels (diagnostics, not the product path)."""
 import sys, os, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# debug stamps (include/ocrk_debug.h) live in the tools-only build: `make exp`
+os.environ.setdefault("OCRK_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libocrk_exp.so"))
 from cnn_lstm_ctc_ocr_amd import kernels as K, _lib
 
 def run(B, H=512, n_in=1024, T=125, reps=3, dt=torch.bfloat16):

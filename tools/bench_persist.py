@@ -9,6 +9,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# debug stamps (include/ocrk_debug.h) live in the tools-only build: `make exp`
+os.environ.setdefault("OCRK_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libocrk_exp.so"))
 from cnn_lstm_ctc_ocr_amd import _lib, kernels as K  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256

@@ -1,3 +1,5 @@
+# OCRK_GEMM_NT_CFG is honoured by the tools-only build only (make exp)
+export OCRK_LIB=tools/libocrk_exp.so
 set -o pipefail
 mkdir -p gpurun_out
 OCRK_GEMM_NT=0 timeout -k 10 120 python tools/bench_gemm.py > gpurun_out/bg_old.log 2>&1 || exit $?
