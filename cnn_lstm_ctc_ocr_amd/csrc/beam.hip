@@ -24,6 +24,8 @@
 //     no candidate list is materialised.
 //   * Emitted prefixes are appended to a per-sequence arena (parent id,
 //     label) in global memory; TopPaths walks it back with LabelSeq's merge.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -416,7 +418,299 @@ ctc_beam_kernel(const float* __restrict__ logits, const int* __restrict__ seq_le
     }
 }
 
+// ---------------------------------------------------------------------------
+// K <= 16, C <= 128 (BASELINE configs[4]'s beam 16): ONE WAVE per sequence,
+// four sequences per workgroup, no workgroup barrier and no LDS. The same
+// semantics as ctc_beam_kernel (which stays the form for K > 16), restated for
+// 64 lanes:
+//   * beam j lives in lane j's registers (hash, parent hash, label, arena id,
+//     total / blank / label log-probs); per-index reads are v_readlane (uniform
+//     index) or ds_bpermute (per-lane index);
+//   * lane l holds the log-softmax of labels l and l + 64, and for each of them
+//     16-bit parent masks: act (child (r, l) already a beam), own (l == lab[r]);
+//   * the wipe pass's counts (count_better above) are per-label-lane sums over
+//     the branch masks plus a wave sum;
+//   * the selection is a 16-round extraction: the candidates of one label over
+//     the parents ranked in beam order (totals non-increasing, so a label's
+//     children come in key order -- own-label children, which use the blank-
+//     ending probability, are a separate head on their parent's lane) and the
+//     updated beams are sorted heads; each round takes the wave-minimum 64-bit
+//     key (total desc : TF insertion order) and advances that head. The keys
+//     come out in rank order, so the next beam needs no sort.
+// The block form spent ~20 workgroup barriers and a 6-digit radix select per
+// frame: 4.08 ms per C5 launch, ~16 us per frame.
+constexpr int WB_K = 16;
+constexpr int WB_WAVES = 4;
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rlf(float v, int l) {
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), l));
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const unsigned lo = (unsigned)__shfl((int)(unsigned)v, src, 64);
+    const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, o, 64);
+        const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), o, 64);
+        const uint64_t u = ((uint64_t)hi << 32) | lo;
+        v = u < v ? u : v;
+    }
+    return rl64(v, 0);
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return rli(v, 0);
+}
+
+__global__ void __launch_bounds__(64 * WB_WAVES)
+ctc_beam_wave_kernel(const float* __restrict__ logits, const int* __restrict__ seq_len, int T, int B, int C,
+                     int K, int top_paths, int merge_repeated, int64_t* __restrict__ out,
+                     int* __restrict__ out_len, float* __restrict__ log_probs, int2* __restrict__ arena_all) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * WB_WAVES + (threadIdx.x >> 6);
+    if (b >= B) return;                                  // whole waves only: no workgroup barrier below
+    const int L = min(max(seq_len[b], 0), T);
+    const int blank = C - 1;
+    int2* arena = arena_all + (size_t)b * (1 + (size_t)T * K);
+    const int L0 = lane, L1 = lane + 64;
+    const bool ok0 = L0 < blank, ok1 = L1 < blank;       // the non-blank labels this lane holds
+
+    // beam j in lane j (j < n)
+    uint64_t bh = ROOT_HASH, bph = 0;
+    int blab = -1, bid = 0;
+    float bot = 0.f, bob = 0.f, bol = -INFINITY;
+    int n = 1, next_id = 1;
+    if (lane == 0) arena[0] = make_int2(-1, -1);
+
+    auto load_row = [&](int t, float& a0, float& a1) {
+        const float* row = logits + ((size_t)t * B + b) * C;
+        a0 = L0 < C ? row[L0] : -INFINITY;
+        a1 = L1 < C ? row[L1] : -INFINITY;
+    };
+    float n0 = -INFINITY, n1 = -INFINITY;
+    if (L > 0) load_row(0, n0, n1);
+
+    for (int t = 0; t < L; ++t) {
+        const float v0 = n0, v1 = n1;
+        if (t + 1 < L) load_row(t + 1, n0, n1);          // the next frame's loads in flight over this one
+        // ---- log-softmax of the frame (Step(): max removed, then norm_offset), the block form's order
+        const float m = rlf(wave_max(fmaxf(v0, v1)), 0);
+        const float e0 = L0 < C ? expf(v0 - m) : 0.f;
+        const float e1 = L1 < C ? expf(v1 - m) : 0.f;
+        const float z = rlf(wave_sum(e0), 0) + rlf(wave_sum(e1), 0);
+        const float norm = logf(z);
+        const float x0 = (v0 - m) - norm, x1 = (v1 - m) - norm;
+        const float xb = blank < 64 ? rlf(x0, blank) : rlf(x1, blank - 64);
+        auto xval = [&](int l) {                         // x[l] for a per-lane label (all lanes call)
+            const float a = __shfl(x0, l & 63, 64), c2 = __shfl(x1, l & 63, 64);
+            return l < 64 ? a : c2;
+        };
+
+        // ---- parent of each beam: the beam whose hash is its parent hash
+        int p = -1;
+        for (int j = 0; j < n; ++j)
+            if (p < 0 && blab >= 0 && rl64(bh, j) == bph) p = j;
+        if (lane >= n) p = -1;
+
+        // ---- loop 1: every beam extended by blank / its own label
+        const int ps = p < 0 ? 0 : p;
+        const int plab = __shfl(blab, ps, 64);
+        const float pob = __shfl(bob, ps, 64), pot = __shfl(bot, ps, 64);
+        const float xl = xval(blab < 0 ? 0 : blab);
+        float nl = bol, nb = -INFINITY, nt = INFINITY;
+        if (lane < n) {
+            if (blab >= 0) {
+                if (p >= 0) nl = log_sum_exp(nl, blab == plab ? pob : pot);
+                nl += xl;
+            }
+            nb = bot + xb;
+            nt = log_sum_exp(nb, nl);
+        }
+
+        // ---- per-label parent masks, has-kid mask, own-label-child-active mask
+        unsigned act0 = 0u, act1 = 0u, own0 = 0u, own1 = 0u, hk = 0u, ownact = 0u;
+        for (int j = 0; j < n; ++j) {
+            const int lj = rli(blab, j), pj = rli(p, j);
+            if (lj < 0) continue;
+            if (pj >= 0) {
+                if (lj == L0) act0 |= 1u << pj;
+                if (lj == L1) act1 |= 1u << pj;
+                if (pj < j) hk |= 1u << pj;
+                if (lj == rli(blab, pj)) ownact |= 1u << pj;
+            }
+            if (lj == L0) own0 |= 1u << j;
+            if (lj == L1) own1 |= 1u << j;
+        }
+        const unsigned all_n = n >= 32 ? ~0u : ((1u << n) - 1u);
+        // with a full beam no child at or below the weakest updated beam can enter
+        const float tau = n == K ? -rlf(wave_max(lane < n ? -nt : -INFINITY), 0) : -INFINITY;
+
+        // ---- wipe pass (count_better, per label lane), parents in rank order
+        unsigned W = 0u;
+        auto count_better = [&](float thr, bool ge, int jr, int pp, int llim) {
+            int c = 0;
+            if (lane < n) c += ge ? (nt >= thr) : (nt > thr || (nt == thr && lane < jr));
+            const unsigned R = ((1u << pp) - 1u) & ~W;
+            for (unsigned m2 = R; m2; m2 &= m2 - 1u) {
+                const int r = __builtin_ctz(m2);
+                const float otr = rlf(bot, r), obr = rlf(bob, r);
+                if (ok0 && !((act0 >> r) & 1u)) {
+                    const float v = x0 + (((own0 >> r) & 1u) ? obr : otr);
+                    c += ge ? (v >= thr) : (v > thr);
+                }
+                if (ok1 && !((act1 >> r) & 1u)) {
+                    const float v = x1 + (((own1 >> r) & 1u) ? obr : otr);
+                    c += ge ? (v >= thr) : (v > thr);
+                }
+            }
+            const float otp = rlf(bot, pp), obp = rlf(bob, pp);
+            if (ok0 && L0 < llim && !((act0 >> pp) & 1u)) {
+                const float v = x0 + (((own0 >> pp) & 1u) ? obp : otp);
+                c += ge ? (v >= thr) : (v > thr);
+            }
+            if (ok1 && L1 < llim && !((act1 >> pp) & 1u)) {
+                const float v = x1 + (((own1 >> pp) & 1u) ? obp : otp);
+                c += ge ? (v >= thr) : (v > thr);
+            }
+            return wave_sum_i(c);
+        };
+        for (unsigned hm = hk; hm; hm &= hm - 1u) {
+            const int pp = __builtin_ctz(hm);
+            if ((W >> pp) & 1u) continue;
+            if (count_better(rlf(bot, pp), true, 0, pp, 0) >= K) continue;   // p gated
+            for (int j = pp + 1; j < n; ++j) {
+                if (rli(p, j) != pp) continue;
+                if (count_better(rlf(nt, j), false, j, pp, rli(blab, j)) >= K) W |= 1u << j;
+            }
+        }
+
+        // ---- selection: K rounds of the wave-minimum key over the sorted heads
+        const unsigned avail0 = ok0 ? (all_n & ~(act0 | own0 | W)) : 0u;
+        const unsigned avail1 = ok1 ? (all_n & ~(act1 | own1 | W)) : 0u;
+        int ptr0 = avail0 ? __builtin_ctz(avail0) : 32, ptr1 = avail1 ? __builtin_ctz(avail1) : 32;
+        // own-label child of the beam in this lane
+        float vo = xl + bob;
+        bool own_live = lane < n && blab >= 0 && !((W >> lane) & 1u) && !((ownact >> lane) & 1u) && vo > tau;
+        bool beam_live = lane < n;
+        uint64_t selk = ~0ull;
+        int ns = 0;
+        for (int k = 0; k < K; ++k) {
+            const float o0 = __shfl(bot, ptr0 & 63, 64), o1 = __shfl(bot, ptr1 & 63, 64);
+            uint64_t key = ~0ull;
+            if (ptr0 < n) {
+                const float v = x0 + o0;
+                if (v > tau) key = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + ptr0 * C + L0);
+                else ptr0 = 32;                          // the rest of this label's parents rank lower
+            }
+            uint64_t key1 = ~0ull;
+            if (ptr1 < n) {
+                const float v = x1 + o1;
+                if (v > tau) key1 = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + ptr1 * C + L1);
+                else ptr1 = 32;
+            }
+            const uint64_t keyo = own_live ? ((desc_bits(vo) << ORDER_BITS) | (uint64_t)(n + lane * C + blab)) : ~0ull;
+            const uint64_t keyb = beam_live ? ((desc_bits(nt) << ORDER_BITS) | (uint64_t)lane) : ~0ull;
+            uint64_t mine = key < key1 ? key : key1;
+            mine = mine < keyo ? mine : keyo;
+            mine = mine < keyb ? mine : keyb;
+            const uint64_t kmin = wave_min_u64(mine);
+            if (kmin == ~0ull) break;
+            if (lane == k) selk = kmin;
+            ++ns;
+            if (mine == kmin) {
+                if (key == kmin) {
+                    const unsigned rest = avail0 & ~((2u << ptr0) - 1u);
+                    ptr0 = rest ? __builtin_ctz(rest) : 32;
+                } else if (key1 == kmin) {
+                    const unsigned rest = avail1 & ~((2u << ptr1) - 1u);
+                    ptr1 = rest ? __builtin_ctz(rest) : 32;
+                } else if (keyo == kmin) {
+                    own_live = false;
+                } else {
+                    beam_live = false;
+                }
+            }
+        }
+
+        // ---- the next beam, in rank order (the extraction order)
+        const int o = (int)(selk & ((1u << ORDER_BITS) - 1));
+        const bool sel = lane < ns;
+        const bool isnew = sel && o >= n;
+        const int q = o - n, r = isnew ? q / C : 0, l = isnew ? q - r * C : 0;
+        const int src = isnew ? r : (sel ? o : 0);
+        const uint64_t sh_ = shfl64(bh, src), sph = shfl64(bph, src);
+        const int slab = __shfl(blab, src, 64), sid = __shfl(bid, src, 64);
+        const float sot = __shfl(bot, src, 64), sob = __shfl(bob, src, 64);
+        const float snt = __shfl(nt, src, 64), snb = __shfl(nb, src, 64), snl = __shfl(nl, src, 64);
+        const float xnew = xval(l);
+        const uint64_t newmask = __ballot(isnew);
+        const int nid = next_id + __popcll(newmask & ((1ull << lane) - 1ull));
+        if (isnew) {
+            const float val = xnew + (l == slab ? sob : sot);
+            bh = child_hash(sh_, l); bph = sh_; blab = l; bid = nid;
+            bot = val; bob = -INFINITY; bol = val;
+            arena[nid] = make_int2(sid, l);
+        } else if (sel) {
+            bh = sh_; bph = sph; blab = slab; bid = sid;
+            bot = snt; bob = snb; bol = snl;
+        }
+        next_id += __popcll(newmask);
+        n = ns;
+    }
+
+    // ---- TopPaths: walk the arena back, LabelSeq(merge_repeated); -1 fill by the whole wave
+    int len = 0;
+    if (lane < top_paths) {
+        int64_t* ov = out + ((size_t)lane * B + b) * T;
+        if (lane < n) {
+            int e = bid, prev = -1;
+            while (e > 0) {
+                const int2 a = arena[e];
+                if (!merge_repeated || a.y != prev) ++len;
+                prev = a.y;
+                e = a.x;
+            }
+            e = bid; prev = -1;
+            int pos = len;
+            while (e > 0) {
+                const int2 a = arena[e];
+                if (!merge_repeated || a.y != prev) ov[--pos] = a.y;
+                prev = a.y;
+                e = a.x;
+            }
+            log_probs[(size_t)b * top_paths + lane] = bot;
+        } else {
+            log_probs[(size_t)b * top_paths + lane] = -INFINITY;
+        }
+        out_len[(size_t)lane * B + b] = len;
+    }
+    for (int k = 0; k < top_paths; ++k) {
+        const int lk = rli(len, k);
+        int64_t* ov = out + ((size_t)k * B + b) * T;
+        for (int i = lk + lane; i < T; i += 64) ov[i] = -1;
+    }
+}
+
 }  // namespace
+
+// OCRK_BEAM_WAVE=0: the block form for every beam width (A/B)
+static bool wave_beam_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("OCRK_BEAM_WAVE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 extern "C" size_t ocrk_ctc_beam_workspace_size(int T, int B, int beam_width) {
     if (T < 0 || B < 0 || beam_width < 1) return 0;
@@ -438,8 +732,13 @@ extern "C" int ocrk_ctc_beam_decode(const float* logits, const int* seq_len, int
                  "ocrk_ctc_beam_decode: null pointer");
     OCRK_REQUIRE(ws_bytes >= ocrk_ctc_beam_workspace_size(T, B, beam_width),
                  "ocrk_ctc_beam_decode: workspace too small");
-    ctc_beam_kernel<<<B, BEAM_THREADS, 0, ocrk::as_stream(stream)>>>(
-        logits, seq_len, T, B, C, beam_width, top_paths, merge_repeated, out, out_len, log_probs,
-        reinterpret_cast<int2*>(ws));
+    if (beam_width <= WB_K && wave_beam_enabled())
+        ctc_beam_wave_kernel<<<(unsigned)ocrk::cdiv(B, WB_WAVES), 64 * WB_WAVES, 0, ocrk::as_stream(stream)>>>(
+            logits, seq_len, T, B, C, beam_width, top_paths, merge_repeated, out, out_len, log_probs,
+            reinterpret_cast<int2*>(ws));
+    else
+        ctc_beam_kernel<<<B, BEAM_THREADS, 0, ocrk::as_stream(stream)>>>(
+            logits, seq_len, T, B, C, beam_width, top_paths, merge_repeated, out, out_len, log_probs,
+            reinterpret_cast<int2*>(ws));
     return ocrk::launch_status("ocrk_ctc_beam_decode");
 }

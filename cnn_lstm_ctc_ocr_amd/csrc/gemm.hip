@@ -6,6 +6,8 @@
 // other LDS buffer after them (one barrier per k-step). LDS rows are padded by
 // 8 elements (16 B for bf16) so the per-lane 16-B fragment reads of a 16-row
 // group fall on distinct bank groups.
+#include <type_traits>
+
 #include "gemm.h"
 #include "mfma_util.h"
 
@@ -44,9 +46,16 @@ __device__ __forceinline__ const CT* b_addr(const GemmParams& p, const CT* B, in
     else return B + (int64_t)k * p.ldb + n;
 }
 
-template <typename CT, int AM, int BMD, int TBM, int TBN>
+// X3 (CT = float): fp32 operands split at staging into bf16 hi / lo LDS images
+// ([row][k], k-contiguous, the hi image at [0, ELEMS), lo at [ELEMS, 2 ELEMS))
+// and multiplied as ah.bh + ah.bl + al.bh on v_mfma_f32_16x16x32_bf16
+// (mfma_util.h split2_bf16): the fp32 serving path at 3/16 of the bf16 MFMA
+// cost per product instead of the f32 MFMA's 16/1 (X3 = false: exact fp32
+// products on v_mfma_f32_16x16x4_f32, OCRK_F32_MFMA=1).
+template <typename CT, int AM, int BMD, int TBM, int TBN, bool X3 = false>
 __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
-    using RT = typename RawT<CT>::T;
+    static_assert(!X3 || sizeof(CT) == 4, "bf16x3 splits fp32 operands");
+    using RT = typename std::conditional<X3, unsigned short, typename RawT<CT>::T>::type;
     constexpr int BK = 32, LDK = BK + 8;
     constexpr int WM = TBM / 2, WN = TBN / 2, TM = WM / 16, TN = WN / 16;
     constexpr bool A_K = (AM == A_ROWK || AM == A_IM2COL || AM == A_IM2COL_FLIP);
@@ -65,8 +74,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
     constexpr int B_ELEMS = B_TR ? BK * LDB_R : TBN * LDK;
     constexpr int NVA = (TBM * BK / 8 + 255) / 256;
     constexpr int NVB = (TBN * BK / 8 + 255) / 256;
-    __shared__ __attribute__((aligned(16))) RT sA[2][A_ELEMS];
-    __shared__ __attribute__((aligned(16))) RT sB[2][B_ELEMS];
+    __shared__ __attribute__((aligned(16))) RT sA[2][X3 ? 2 * A_ELEMS : A_ELEMS];
+    __shared__ __attribute__((aligned(16))) RT sB[2][X3 ? 2 * B_ELEMS : B_ELEMS];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -107,7 +116,54 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
             }
         }
     };
+    auto store_tiles_x3 = [&](int buf) {
+        if constexpr (X3) {
+#pragma unroll
+            for (int v = 0; v < NVA; ++v) {
+                int idx = tid + 256 * v;
+                if (idx < TBM * BK / 8) {
+                    u32x4 hi, lo;
+                    split8_bf16(ra[v], hi, lo);
+                    if constexpr (A_K) {
+                        const int o = (idx >> 2) * LDK + 8 * (idx & 3);
+                        *reinterpret_cast<u32x4*>(&sA[buf][o]) = hi;
+                        *reinterpret_cast<u32x4*>(&sA[buf][A_ELEMS + o]) = lo;
+                    } else {
+                        int kk = idx / (TBM / 8), r0 = 8 * (idx % (TBM / 8));
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            sA[buf][(r0 + i) * LDK + kk] = (unsigned short)(hi[i >> 1] >> (16 * (i & 1)));
+                            sA[buf][A_ELEMS + (r0 + i) * LDK + kk] = (unsigned short)(lo[i >> 1] >> (16 * (i & 1)));
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < NVB; ++v) {
+                int idx = tid + 256 * v;
+                if (idx < TBN * BK / 8) {
+                    u32x4 hi, lo;
+                    split8_bf16(rb[v], hi, lo);
+                    if constexpr (B_K) {
+                        const int o = (idx >> 2) * LDK + 8 * (idx & 3);
+                        *reinterpret_cast<u32x4*>(&sB[buf][o]) = hi;
+                        *reinterpret_cast<u32x4*>(&sB[buf][B_ELEMS + o]) = lo;
+                    } else {
+                        int kk = idx / (TBN / 8), r0 = 8 * (idx % (TBN / 8));
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            sB[buf][(r0 + i) * LDK + kk] = (unsigned short)(hi[i >> 1] >> (16 * (i & 1)));
+                            sB[buf][B_ELEMS + (r0 + i) * LDK + kk] = (unsigned short)(lo[i >> 1] >> (16 * (i & 1)));
+                        }
+                    }
+                }
+            }
+        }
+    };
     auto store_tiles = [&](int buf) {
+        if constexpr (X3) {
+            store_tiles_x3(buf);
+        } else {
 #pragma unroll
         for (int v = 0; v < NVA; ++v) {
             int idx = tid + 256 * v;
@@ -142,6 +198,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
                 }
             }
         }
+        }
     };
 
     floatx4 acc[TM][TN];
@@ -159,7 +216,30 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
-        if constexpr (BF) {
+        if constexpr (X3) {
+            // k-contiguous hi / lo images, lane (i16, g) holds k = 8g .. 8g + 7 of its row
+            bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const RT* ap = &sA[buf][(wm * WM + i * 16 + i16) * LDK + 8 * g];
+                ah[i] = *reinterpret_cast<const bf16x8*>(ap);
+                al[i] = *reinterpret_cast<const bf16x8*>(ap + A_ELEMS);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const RT* bp = &sB[buf][(wn * WN + j * 16 + i16) * LDK + 8 * g];
+                bh[j] = *reinterpret_cast<const bf16x8*>(bp);
+                bl[j] = *reinterpret_cast<const bf16x8*>(bp + B_ELEMS);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        } else if constexpr (BF) {
             bf16x8 af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
@@ -460,12 +540,26 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
     return splits > 1 ? (size_t)batch * splits * M * N * sizeof(float) : 0;
 }
 
+// fp32 GEMMs on the bf16x3 split (default) or the exact f32 MFMA (OCRK_F32_MFMA=1)
+static bool f32_exact_mfma() {
+    static const bool on = [] {
+        const char* e = getenv("OCRK_F32_MFMA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 template <typename CT, int AM, int BMD>
 static int launch_tiles(const GemmParams& p0, hipStream_t stream) {
     GemmParams p = p0;
     int TBM = 128, TBN = p.N <= 32 ? 32 : (p.N <= 64 ? 64 : 128);
     dim3 grid((unsigned)cdiv(p.M, TBM), (unsigned)cdiv(p.N, TBN), (unsigned)(p.batch * p.splits));
-    if (TBN == 32) gemm_kernel<CT, AM, BMD, 128, 32><<<grid, 256, 0, stream>>>(p);
+    constexpr bool F32 = sizeof(CT) == 4;
+    if (F32 && !f32_exact_mfma()) {
+        if (TBN == 32) gemm_kernel<CT, AM, BMD, 128, 32, F32><<<grid, 256, 0, stream>>>(p);
+        else if (TBN == 64) gemm_kernel<CT, AM, BMD, 128, 64, F32><<<grid, 256, 0, stream>>>(p);
+        else gemm_kernel<CT, AM, BMD, 128, 128, F32><<<grid, 256, 0, stream>>>(p);
+    } else if (TBN == 32) gemm_kernel<CT, AM, BMD, 128, 32><<<grid, 256, 0, stream>>>(p);
     else if (TBN == 64) gemm_kernel<CT, AM, BMD, 128, 64><<<grid, 256, 0, stream>>>(p);
     else gemm_kernel<CT, AM, BMD, 128, 128><<<grid, 256, 0, stream>>>(p);
     int st = launch_status("gemm");

@@ -66,6 +66,32 @@ __device__ __forceinline__ bf16x8 frag_perm(const unsigned short* row, int g) {
     return __builtin_bit_cast(bf16x8, v);
 }
 
+// fp32 operands on the bf16 MFMA ("bf16x3"): x = hi + lo with hi = bf16(x) and
+// lo = bf16(x - hi) (both round-to-nearest-even), so |x - hi - lo| <= 2^-17 |x|
+// (2^-9 from hi, times 2^-8 from lo); a product a.b is taken as
+// ah.bh + ah.bl + al.bh (the dropped al.bl is <= 2^-18 |a.b|) with f32
+// accumulation: ~2^-16 relative per product, against fp32's 2^-24 -- 3
+// v_mfma_f32_16x16x32_bf16 (16 cycles each, 2.5 PF dense) instead of the f32
+// MFMA (v_mfma_f32_16x16x4_f32, 157 TF): 5.3x the rate per product.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2_bf16(float x0, float x1, unsigned& hi, unsigned& lo) {
+    const bf16x2_t h = __builtin_convertvector(f32x2_t{x0, x1}, bf16x2_t);
+    const f32x2_t hf = __builtin_convertvector(h, f32x2_t);
+    const bf16x2_t l = __builtin_convertvector(f32x2_t{x0 - hf[0], x1 - hf[1]}, bf16x2_t);
+    hi = __builtin_bit_cast(unsigned, h);
+    lo = __builtin_bit_cast(unsigned, l);
+}
+__device__ __forceinline__ void split8_bf16(const V8<float>& x, u32x4& hi, u32x4& lo) {
+    unsigned h[4], l[4];
+    split2_bf16(x.q0[0], x.q0[1], h[0], l[0]);
+    split2_bf16(x.q0[2], x.q0[3], h[1], l[1]);
+    split2_bf16(x.q1[0], x.q1[1], h[2], l[2]);
+    split2_bf16(x.q1[2], x.q1[3], h[3], l[3]);
+    hi = u32x4{h[0], h[1], h[2], h[3]};
+    lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
 // Buffer resource from provably wave-uniform words (readfirstlane; the byte
 // count clamped with integer ops -- HIP's min<int64_t> lowers to v_min_f64, a
 // VALU value). A descriptor the compiler cannot prove uniform is kept in VGPRs

@@ -338,11 +338,40 @@ def check_status(device, reset=True):
     _lib.raise_for_status(read_status(device, reset))
 
 
-def lstm_fwd(gx, whT, seq_len, T, B, H, dtype):
+def lstm_f32_persistent_ok(B, H):
+    """Run the fp32 forward loop as one persistent launch on the bf16x3 split
+    (csrc/lstm_f32x3.hip)? H = 512, B % 32 == 0 and the grid co-resident;
+    OCRK_LSTM_PERSISTENT=0 selects the per-step fp32 kernels."""
+    import os
+    if os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
+        return False
+    key = ("f32", B, H)
+    if key not in _PERSISTENT:
+        _PERSISTENT[key] = bool(_lib.lib().ocrk_lstm_fwd_persistent_f32_supported(B, H))
+    return _PERSISTENT[key]
+
+
+def lstm_fwd(gx, whT, seq_len, T, B, H, dtype, save=True):
+    """One bidirectional LSTM layer's time loop. Returns (out, hprev, cprev, acts);
+    save=False (no backward will run): the fp32 persistent loop skips the saved
+    tensors and returns None for them."""
     _chk(gx, whT, seq_len)
     if gx.dtype != dtype or whT.dtype != dtype:
         raise TypeError(f"lstm_fwd: gx and whT must be {dtype} (got {gx.dtype}, {whT.dtype})")
     dev = gx.device
+    if dtype == torch.float32 and lstm_f32_persistent_ok(B, H):
+        out = torch.empty(T, B, 2 * H, dtype=dtype, device=dev)       # padded steps written as zeros by the kernel
+        hprev = cprev = acts = None
+        if save:
+            hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)
+            cprev = torch.empty(T, B, 2, H, dtype=torch.float32, device=dev)
+            acts = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
+        nb = _lib.lib().ocrk_lstm_fwd_persistent_f32_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        call("ocrk_lstm_fwd_persistent_f32", ptr(gx), ptr(whT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
+             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_fwd_f32", B, H, dev)),
+             ptr(ws), nb, _stream(gx))
+        return out, hprev, cprev, acts
     if lstm_persistent_ok(B, H, dtype):
         out = torch.empty(T, B, 2 * H, dtype=dtype, device=dev)       # padded steps written as zeros by the kernel
         hprev = torch.empty(T, B, 2, H, dtype=dtype, device=dev)

@@ -280,7 +280,7 @@ class _BiLSTM(torch.autograd.Function):
             out, hprev, cprev, acts = K.lstm_fwd_fused_x(x, wxT, bias, whT, seq_len, T, B, H)
         else:
             gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
-            out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt)
+            out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt, save=any(ctx.needs_input_grad))
         ctx.store, ctx.layer, ctx.H = store, layer, H
         ctx.save_for_backward(x, seq_len, hprev, cprev, acts)
         return out

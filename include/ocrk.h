@@ -244,6 +244,20 @@ int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* wxT, const f
  * (direction, 32-row batch slice) group, dc kept in registers. Same dG_t as
  * ocrk_lstm_bwd (dg_state/dc_state not needed); err: the device status word
  * (OCRK_STATUS_LSTM_BWD_TIMEOUT / _CENSUS). */
+/* a7' in fp32 (model_bu.py:187-192 in the reference's float32; the serving path
+ * server.py:78-145): the forward time loop as one persistent launch, h . W_h on the
+ * bf16 MFMA through the bf16x3 split (hi/lo bf16 operands, ah.bh + ah.bl + al.bh,
+ * f32 accumulate; ~2^-16 relative per product). gx f32 [T][B][2][4H] (bias included),
+ * whT f32 [2][4H][H]; out f32 [T][B][2H] (zeros past each row's length);
+ * hprev_t / cprev_t f32 [T][B][2][H] and acts_t f32 [T][B][2][4H] for the BPTT, or
+ * all three NULL (inference). H = 512, B % 32 == 0, grid 2 (B/32) (H/32) co-resident;
+ * flags as ocrk_lstm_fwd_persistent (ocrk_persistent_flags_size(B, H)); status bits
+ * OCRK_STATUS_LSTM_FWD_TIMEOUT / _CENSUS. */
+int ocrk_lstm_fwd_persistent_f32_supported(int B, int H);
+size_t ocrk_lstm_fwd_persistent_f32_workspace_size(int B, int H);
+int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, const int* seq_len, int T, int B, int H,
+                                 float* out, float* hprev_t, float* cprev_t, float* acts_t, unsigned* err,
+                                 unsigned* flags, void* ws, size_t ws_bytes, void* stream);
 int ocrk_lstm_bwd_persistent_supported(int B, int H);
 size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,

@@ -159,3 +159,49 @@ def test_fused_input_projection_forward(cuda, B):
     assert np.all(out[seq[1]:, 1] == 0)
     # the saved tensors the BPTT reads: activations of the unfused path within bf16 noise
     np.testing.assert_allclose(fus[2].cpu().numpy(), unf[2].cpu().numpy(), atol=5e-2)
+
+
+@pytest.mark.parametrize("T,B,n_in", [(19, 64, 64), (23, 160, 256)])
+def test_f32_persistent_fwd_matches_oracle_and_step_kernels(cuda, monkeypatch, T, B, n_in):
+    """The fp32 forward loop (csrc/lstm_f32x3.hip: one persistent launch, h.W_h on
+    the bf16x3 split) against the float64 oracle (lstm_dir_fwd, ragged lengths,
+    reverse direction) and the per-step fp32 kernels (exact f32 MFMA): outputs
+    and every saved tensor <= 5e-5 relative, padded steps exactly zero; the
+    inference form (no saved tensors) writes the same outputs."""
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    H = 512
+    rng = np.random.default_rng(3 + B)
+    x = rng.standard_normal((T, B, n_in)).astype(np.float32)
+    ks = [(rng.standard_normal((n_in + H, 4 * H)) * 0.05).astype(np.float32) for _ in range(2)]
+    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
+    seq = rng.integers(1, T + 1, B).astype(np.int32)
+    seq[:3] = [T, 1, T - 1]
+    outs, caches = zip(*[G.lstm_dir_fwd(x.astype(np.float64), seq, ks[d].astype(np.float64),
+                                        bs[d].astype(np.float64), d == 1) for d in range(2)])
+    ref = np.concatenate(outs, axis=2)
+    gx = torch.from_numpy((np.einsum("tbi,dig->tbdg", x.astype(np.float64),
+                                     np.stack([k[:n_in] for k in ks]).astype(np.float64)) +
+                           np.stack(bs)[None, None]).astype(np.float32)).to(cuda).reshape(T * B, 8 * H)
+    whT = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))).to(cuda)
+    seq_d = torch.from_numpy(seq).to(cuda)
+    assert K.lstm_f32_persistent_ok(B, H)
+    K.lstm_error_word(cuda).zero_()
+    step, pers = _both(K, monkeypatch, lambda: K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.float32))
+    assert K.lstm_error_word(cuda).item() == 0
+    out = pers[0].cpu().numpy()
+    assert np.linalg.norm(out - ref) / np.linalg.norm(ref) < 5e-5
+    for b in range(B):
+        assert np.all(out[seq[b]:, b] == 0)
+    for a, p in zip(step, pers):
+        a, p = a.cpu().numpy(), p.cpu().numpy()
+        assert np.linalg.norm(a - p) / max(np.linalg.norm(a), 1e-30) < 5e-5
+    hp = pers[1].cpu().numpy()                                # h_{s-1} saved in time order
+    for d in range(2):
+        for s in range(T):
+            t_idx, valid, _xs, h_prev, _c, _a = caches[d][s]
+            rows = np.nonzero(valid)[0]
+            np.testing.assert_allclose(hp[t_idx[rows], rows, d], h_prev[rows], rtol=0, atol=2e-5)
+    o2, h2, c2, a2 = K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.float32, save=False)
+    assert h2 is None and c2 is None and a2 is None
+    assert torch.equal(o2, pers[0])
+    K._PERSISTENT.clear()
