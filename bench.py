@@ -27,6 +27,9 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
 PEAK_F32_TFLOPS = 157.3       # f32 MFMA = f32 vector peak
+# fp32 GEMMs run as the bf16x3 split (3 bf16 MFMA products per fp32 product,
+# csrc/mfma_util.h): their roofline is the bf16 dense peak / 3
+PEAK_F32X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
 
 
@@ -584,7 +587,7 @@ def main():
         work = sum(w for _, _, w in probe)
     avg_ms = sum(ms) / max(len(ms), 1)
     achieved = work / max(sum(ms), 1e-9) / 1e9          # FLOP/ms -> TFLOP/s
-    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32X3_TFLOPS
 
     if args.breakdown and rank == 0:
         rows = [(n, sum(v) / probed, len(v) // probed) for n, v in rows.items()]
@@ -619,7 +622,7 @@ def main():
                    "collective": "one bucketed SUM all-reduce of the flat fp32 gradient per step "
                                  "(RCCL over xGMI, backend nccl)" if world > 1 else "none"},
         "world_size_seen": dist.get_world_size() if world > 1 else 1,
-        "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": peak,
+        "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_per_step": len(ms) // max(probed, 1), "avg_launch_ms": round(avg_ms, 4),
                      "algorithmic_flop_per_launch": work / max(len(ms), 1),
@@ -629,6 +632,9 @@ def main():
                          f" in {probed} of the {args.steps} timed steps (every {every}th)")},
         "loss": round(float(loss.item()), 4),
     }
+    if dtype != torch.bfloat16:
+        result["roofline"]["peak_note"] = ("fp32 operands on the bf16x3 split (3 bf16 MFMA products per fp32 "
+                                           "product): peak = bf16 dense 2500 / 3 TFLOP/s")
     if args.roofline == "conv" and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             pmc = json.load(fh)

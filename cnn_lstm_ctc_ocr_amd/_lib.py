@@ -36,6 +36,8 @@ SIGNATURES = {
     "ocrk_last_error": [],
     "ocrk_preprocess": [_p, _i64, _p, _i32, _p],
     "ocrk_status_clear": [_p, ctypes.c_uint32, _p],
+    "ocrk_set_f32_gemm_mode": [_i32],
+    "ocrk_f32_gemm_exact": [],
     "ocrk_ctc_workspace_size": [_i32, _i32, _i32],
     "ocrk_ctc_loss": [_p, _p, _p, _p, _i32, _i32, _i32, _i32, _f32, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_ctc_greedy_decode": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p],

@@ -456,20 +456,32 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src, 64);
     return ((uint64_t)hi << 32) | lo;
 }
+// DPP row rotations (8, 4, 2, 1 within each 16-lane row: no LDS crossbar round
+// trip) give every lane its row's result; the four rows meet through v_readlane.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_min_step(uint64_t v) {
+    const uint64_t u = ((uint64_t)dpp_u<CTRL>((unsigned)(v >> 32)) << 32) | dpp_u<CTRL>((unsigned)v);
+    return u < v ? u : v;
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, o, 64);
-        const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), o, 64);
-        const uint64_t u = ((uint64_t)hi << 32) | lo;
-        v = u < v ? u : v;
-    }
-    return rl64(v, 0);
+    v = dpp_min_step<0x128>(v);
+    v = dpp_min_step<0x124>(v);
+    v = dpp_min_step<0x122>(v);
+    v = dpp_min_step<0x121>(v);
+    const uint64_t a = rl64(v, 0), b = rl64(v, 16), c = rl64(v, 32), d = rl64(v, 48);
+    const uint64_t ab = a < b ? a : b, cd = c < d ? c : d;
+    return ab < cd ? ab : cd;
 }
 __device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return rli(v, 0);
+    v += (int)dpp_u<0x128>((unsigned)v);
+    v += (int)dpp_u<0x124>((unsigned)v);
+    v += (int)dpp_u<0x122>((unsigned)v);
+    v += (int)dpp_u<0x121>((unsigned)v);
+    return (rli(v, 0) + rli(v, 16)) + (rli(v, 32) + rli(v, 48));
 }
 
 __global__ void __launch_bounds__(64 * WB_WAVES)

@@ -76,6 +76,8 @@ int splitk_finish(const GemmParams& p, hipStream_t stream);
 // (gemm_nt.hip). Returns -1 when it does not cover the call (the caller then
 // uses the generic engine), else a status. OCRK_GEMM_NT=0 disables it.
 int gemm_nt(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream);
+// fp32 operands: exact f32 MFMA (OCRK_F32_MFMA=1) instead of the bf16x3 split
+bool f32_exact_mfma();
 
 // 8-wave ping-pong engine (gemm_pp.hip): 256 x {256,128} x 64 tiles for the
 // large bf16 A_ROWK / A_IM2COL / A_IM2COL_FLIP x B_NK GEMMs (N >= 96). Returns

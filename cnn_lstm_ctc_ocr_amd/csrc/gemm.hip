@@ -6,6 +6,8 @@
 // other LDS buffer after them (one barrier per k-step). LDS rows are padded by
 // 8 elements (16 B for bf16) so the per-lane 16-B fragment reads of a 16-row
 // group fall on distinct bank groups.
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm.h"
@@ -540,13 +542,16 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
     return splits > 1 ? (size_t)batch * splits * M * N * sizeof(float) : 0;
 }
 
-// fp32 GEMMs on the bf16x3 split (default) or the exact f32 MFMA (OCRK_F32_MFMA=1)
-static bool f32_exact_mfma() {
-    static const bool on = [] {
+// fp32 GEMMs on the bf16x3 split (mode 0, the default) or the exact f32 MFMA
+// (mode 1: ocrk_set_f32_gemm_mode, or OCRK_F32_MFMA=1 for the whole process)
+static std::atomic<int> g_f32_mode{0};
+
+bool f32_exact_mfma() {
+    static const bool env = [] {
         const char* e = getenv("OCRK_F32_MFMA");
         return e && e[0] == '1';
     }();
-    return on;
+    return env || g_f32_mode.load(std::memory_order_relaxed) == 1;
 }
 
 template <typename CT, int AM, int BMD>
@@ -611,6 +616,13 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
 // Generic dense GEMM used by the recurrent projections and the logits layer:
 // C[b] = alpha * op(A[b]) . op(B[b]) + bias (ReLU), op per trans flags:
 //   trans_a = 0: A is [M][K] (lda), 1: A is [K][M];  trans_b = 0: B is [K][N], 1: B is [N][K].
+extern "C" int ocrk_set_f32_gemm_mode(int mode) {
+    OCRK_REQUIRE(mode == 0 || mode == 1, "ocrk_set_f32_gemm_mode: mode %d not 0 (bf16x3) or 1 (exact)", mode);
+    return ocrk::g_f32_mode.exchange(mode);
+}
+
+extern "C" int ocrk_f32_gemm_exact(void) { return ocrk::f32_exact_mfma() ? 1 : 0; }
+
 extern "C" size_t ocrk_gemm_workspace_size(int M, int N, int batch, int splits) {
     return ocrk::gemm_splitk_ws_bytes(M, N, batch, splits);
 }

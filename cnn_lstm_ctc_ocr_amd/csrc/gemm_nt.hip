@@ -33,7 +33,11 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, u
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4>
+// F32 (the fp32 serving / parity path): A and B are fp32, staged by the same
+// LDS-DMA ring (BK = 32 -> 128-B rows, the bf16 BK = 64 geometry), and every
+// MFMA fragment is split at the read into bf16 hi / lo (mfma_util.h
+// split8_bf16) for the three bf16 products ah.bh + ah.bl + al.bh.
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false>
 __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
     // (its second pass over the accumulators would spill); launch_nt routes
@@ -42,7 +46,9 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     constexpr int WAVES_N = NW / WAVES_M;
     constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
     constexpr int TM = WM / 16, TN = WN / 16;
-    constexpr int ROWB = BK * 2;                          // bytes per LDS row
+    constexpr int ESZ = F32 ? 4 : 2;                      // operand element bytes
+    constexpr int EPC = 16 / ESZ;                         // elements per 16-B chunk
+    constexpr int ROWB = BK * ESZ;                        // bytes per LDS row
     constexpr int RPI = 1024 / ROWB;                      // rows per wave instruction
     constexpr int CPR = ROWB / 16;                        // 16-B chunks per row
     constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
@@ -53,6 +59,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     constexpr int BBLK = BN / RPI;                        // B row blocks per stage
     constexpr int NPS = NA + NB;
     static_assert((BK == 32 || BK == 64) && S >= 2, "BK 32 or 64, >= 2 stages");
+    static_assert(!F32 || BK == 32, "fp32 operands: BK = 32 (128-B rows)");
     static_assert(BM % (NW * RPI) == 0 && BN % RPI == 0 && (BN < NW * RPI || BN % (NW * RPI) == 0), "tile");
     static_assert(TM >= 1 && TN >= 1, "wave tile");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -63,8 +70,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     if (!tix.valid) return;
     const int m0 = tix.bm * BM, n0 = tix.bn * BN;
     const int zb = blockIdx.z / p.splits, zs = blockIdx.z - zb * p.splits;
-    const bf16* A = reinterpret_cast<const bf16*>(p.A) + zb * p.strideA;
-    const bf16* B = reinterpret_cast<const bf16*>(p.B) + zb * p.strideB;
+    const char* A = reinterpret_cast<const char*>(p.A) + zb * p.strideA * ESZ;
+    const char* B = reinterpret_cast<const char*>(p.B) + zb * p.strideB * ESZ;
     const int kbeg = zs * p.k_chunk;
     const int kend = min(p.K, kbeg + p.k_chunk);
     const int nk = max(0, (kend - kbeg + BK - 1) / BK);
@@ -73,13 +80,13 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     int64_t a_elems, b_elems = (int64_t)p.N * p.ldb;
     if constexpr (AM == A_ROWK) a_elems = (int64_t)p.M * p.lda;
     else a_elems = (int64_t)p.M * p.convC;               // NHWC source with M = B*H*W pixels
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, a_elems * 2);
-    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, b_elems * 2);
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A, a_elems * ESZ);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B, b_elems * ESZ);
 
     // this lane's row within its instruction and the chunk it fetches (global side of the swizzle);
     // instruction rows start at multiples of RPI, so row & (RPI-1) == lrow
     const int lrow = lane / CPR;
-    const int chunk = BK == 64 ? ((lane & 7) ^ lrow) : ((lane & 3) ^ ((lrow >> 2) & 3));
+    const int chunk = ROWB == 128 ? ((lane & 7) ^ lrow) : ((lane & 3) ^ ((lrow >> 2) & 3));
 
     // per-lane row geometry of each DMA instruction, as 32-bit byte offsets
     // (every operand here is < 2 GB) with NT_BADROW for rows past M / N
@@ -89,24 +96,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         const int m = m0 + (i * NW + wave) * RPI + lrow;
         ahw[i] = 0;
         if constexpr (AM == A_ROWK) {
-            aoff[i] = m < p.M ? (unsigned)((int64_t)m * p.lda * 2) : NT_BADROW;
+            aoff[i] = m < p.M ? (unsigned)((int64_t)m * p.lda * ESZ) : NT_BADROW;
         } else {
             const int W = p.convW, H = p.convH;
             const int mm = m < p.M ? m : 0;
             const int w = mm % W, h = (mm / W) % H;
             ahw[i] = ((unsigned)h << 16) | (unsigned)w;
-            aoff[i] = m < p.M ? (unsigned)((int64_t)mm * p.convC * 2) : NT_BADROW;
+            aoff[i] = m < p.M ? (unsigned)((int64_t)mm * p.convC * ESZ) : NT_BADROW;
         }
     }
     unsigned boff[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         const int n = n0 + ((i * NW + wave) % BBLK) * RPI + lrow;
-        boff[i] = n < p.N ? (unsigned)((int64_t)n * p.ldb * 2) : NT_BADROW;
+        boff[i] = n < p.N ? (unsigned)((int64_t)n * p.ldb * ESZ) : NT_BADROW;
     }
 
     auto issue = [&](int kt, int stage) {
-        const int k = kbeg + kt * BK + 8 * chunk;
+        const int k = kbeg + kt * BK + EPC * chunk;
         const bool kok = k < kend;
         char* sa = smem + stage * STAGE;
         char* sb = sa + A_BYTES;
@@ -118,14 +125,14 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
             const int kh = tap / 3, kw = tap - kh * 3;
             if constexpr (AM == A_IM2COL_FLIP) { dh = 1 - kh; dw = 1 - kw; }
             else { dh = kh - 1; dw = kw - 1; }
-            tap_off = ((dh * p.convW + dw) * C + cch) * 2;
+            tap_off = ((dh * p.convW + dw) * C + cch) * ESZ;
         }
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             bool ok = kok && aoff[i] != NT_BADROW;
             unsigned voff;
             if constexpr (AM == A_ROWK) {
-                voff = aoff[i] + (unsigned)(k * 2);
+                voff = aoff[i] + (unsigned)(k * ESZ);
             } else {
                 const int hh = (int)(ahw[i] >> 16) + dh, ww = (int)(ahw[i] & 0xffff) + dw;
                 ok = ok && hh >= 0 && hh < p.convH && ww >= 0 && ww < p.convW;
@@ -136,7 +143,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const bool ok = kok && boff[i] != NT_BADROW;
-            lds_dma16(rb, sb + (((i * NW + wave) % BBLK) * RPI) * ROWB, ok ? boff[i] + (unsigned)(k * 2) : NT_OOB);
+            lds_dma16(rb, sb + (((i * NW + wave) % BBLK) * RPI) * ROWB, ok ? boff[i] + (unsigned)(k * ESZ) : NT_OOB);
         }
     };
 
@@ -150,7 +157,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     for (int st = 0; st < S - 1; ++st)
         if (st < nk) issue(st, st);
     const int i16 = lane & 15, g = lane >> 4;
-    const int swz = BK == 64 ? (lane & 7) : ((i16 >> 2) & 3);
+    const int swz = ROWB == 128 ? (lane & 7) : ((i16 >> 2) & 3);
     for (int kt = 0; kt < nk; ++kt) {
         // stage kt landed: the stages issued after it (up to S-2 of them) may stay in flight
         const int ahead = min(S - 2, nk - 1 - kt);
@@ -176,6 +183,34 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
         const char* sa = smem + (kt % S) * STAGE;
         const char* sb = sa + A_BYTES;
+        if constexpr (F32) {
+            // lane group g holds k = 8g .. 8g + 7 = fp32 chunks 2g, 2g + 1 of its row
+            const int s0 = ((2 * g) ^ swz) * 16, s1 = ((2 * g + 1) ^ swz) * 16;
+            auto frag = [&](const char* row, bf16x8& hi, bf16x8& lo) {
+                V8<float> v;
+                v.q0 = *reinterpret_cast<const f32x4*>(row + s0);
+                v.q1 = *reinterpret_cast<const f32x4*>(row + s1);
+                u32x4 h, l;
+                split8_bf16(v, h, l);
+                hi = __builtin_bit_cast(bf16x8, h);
+                lo = __builtin_bit_cast(bf16x8, l);
+            };
+            bf16x8 bh[TN], bl[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) frag(sb + (wn * WN + j * 16 + i16) * ROWB, bh[j], bl[j]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                bf16x8 ah, al;
+                frag(sa + (wm * WM + i * 16 + i16) * ROWB, ah, al);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int kk = 0; kk < BK / 32; ++kk) {
             const int slot = ((kk * 4 + g) ^ swz) * 16;
@@ -211,7 +246,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         return;
     }
     const float* bias = p.bias ? p.bias + zb * p.strideBias : nullptr;
-    const bf16* mask = reinterpret_cast<const bf16*>(p.mask);
+    const bf16* mask = reinterpret_cast<const bf16*>(p.mask);   // bf16 path only (F32: no mask, gemm_nt)
     float* Cf = reinterpret_cast<float*>(p.C) + zb * p.strideC;
     bf16* Cb = reinterpret_cast<bf16*>(p.C) + zb * p.strideC;
     // Staged epilogue (bf16 C): the tile goes through LDS (pitch TP bytes, after
@@ -339,17 +374,25 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     }
 }
 
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4>
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false>
 int launch_nt(const GemmParams& p, hipStream_t stream) {
-    if constexpr (NW == 8) {
+    if constexpr (NW == 8 && !F32) {
         if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
     }
-    constexpr int LDS = S * (BM + BN) * BK * 2;
+    constexpr int LDS = S * (BM + BN) * BK * (F32 ? 4 : 2);
     static DeviceOnce configured;
-    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW>), LDS);
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32>), LDS);
     dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
-    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW><<<grid, NW * 64, LDS, stream>>>(p);
+    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");
+}
+
+// fp32 operands on the bf16x3 split (BK = 32: 128-B fp32 rows)
+template <int AM>
+int dispatch_nt_f32(const GemmParams& p, hipStream_t s) {
+    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM, 4, true>(p, s);
+    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM, 4, true>(p, s);
+    return launch_nt<128, 128, 32, 2, 2, AM, 4, true>(p, s);
 }
 
 // Tile configurations (OCRK_GEMM_NT_CFG picks one for experiments; by default
@@ -422,7 +465,23 @@ bool nt_staged_enabled() {
 
 // Runs the NT engine when it covers (mode, dtype); returns -1 when it does not.
 int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t stream) {
-    if (!gemm_nt_enabled() || dtype != OCRK_BF16 || bmode != B_NK) return -1;
+    if (!gemm_nt_enabled() || bmode != B_NK) return -1;
+    if (dtype == OCRK_F32) {
+        // fp32: the bf16x3 split on this ring (the generic engine keeps the short-K
+        // shapes, the masked data gradients and OCRK_F32_MFMA=1)
+        if (f32_exact_mfma() || p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 512 && p0.N > 64)) return -1;
+        GemmParams p = p0;
+        p.epi_staged = 0;
+        if (amode == A_ROWK) {
+            if (p.lda % 4 != 0 || p.ldb % 4 != 0) return -1;
+            return dispatch_nt_f32<A_ROWK>(p, stream);
+        }
+        if (p.convC % 4 != 0 || p.ldb % 4 != 0) return -1;
+        if (amode == A_IM2COL) return dispatch_nt_f32<A_IM2COL>(p, stream);
+        if (amode == A_IM2COL_FLIP) return dispatch_nt_f32<A_IM2COL_FLIP>(p, stream);
+        return -1;
+    }
+    if (dtype != OCRK_BF16) return -1;
     GemmParams p = p0;
     // 16-B row chunks of C (and of the mask) must be aligned and never straddle N
     p.epi_staged = nt_staged_enabled() && p.c_bf16 && p.splits == 1 && p.N % 8 == 0 && p.ldc % 8 == 0 &&

@@ -338,12 +338,36 @@ def check_status(device, reset=True):
     _lib.raise_for_status(read_status(device, reset))
 
 
+class f32_exact:
+    """Context manager: fp32 GEMMs / convs with exact f32 MFMA products while
+    inside (ocrk_set_f32_gemm_mode(1)), and the fp32 recurrence on the per-step
+    f32 kernels; the default outside is the bf16x3 split (include/ocrk.h).
+    Process-wide: not for concurrent threads with different needs."""
+
+    def __init__(self, on=True):
+        self.on = on
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = _lib.lib().ocrk_set_f32_gemm_mode(1 if self.on else 0)
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().ocrk_set_f32_gemm_mode(self.prev)
+        return False
+
+
+def f32_mode_exact():
+    return bool(_lib.lib().ocrk_f32_gemm_exact())
+
+
 def lstm_f32_persistent_ok(B, H):
     """Run the fp32 forward loop as one persistent launch on the bf16x3 split
-    (csrc/lstm_f32x3.hip)? H = 512, B % 32 == 0 and the grid co-resident;
-    OCRK_LSTM_PERSISTENT=0 selects the per-step fp32 kernels."""
+    (csrc/lstm_f32x3.hip)? H = 512, B % 32 == 0 and the grid co-resident; not
+    in exact fp32 mode (f32_exact); OCRK_LSTM_PERSISTENT=0 selects the per-step
+    fp32 kernels."""
     import os
-    if os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
+    if os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0" or f32_mode_exact():
         return False
     key = ("f32", B, H)
     if key not in _PERSISTENT:
@@ -682,6 +706,12 @@ def edit_distance(hyp, hyp_len, labels, label_len, totals=None):
     `totals` (i32 [3]) when given."""
     _chk(hyp, hyp_len, labels, label_len)
     B = hyp.shape[0]
+    # a batch whose decodes are all empty (or all-empty labels) has a 0-column
+    # tensor, i.e. no storage: give the kernel one padding column (lengths rule)
+    if hyp.shape[1] == 0:
+        hyp = torch.full((B, 1), -1, dtype=hyp.dtype, device=hyp.device)
+    if labels.shape[1] == 0:
+        labels = torch.zeros((B, 1), dtype=labels.dtype, device=labels.device)
     dist = torch.empty(B, dtype=torch.float32, device=hyp.device)
     if totals is not None:
         _chk(totals)

@@ -182,7 +182,16 @@ class Trainer:
         return 1
 
     def loss_and_grads(self, image, width, label):
-        """Forward + backward only; gradients land in store.flat_grad."""
+        """Forward + backward only; gradients land in store.flat_grad. A float32
+        store trains with exact fp32 products (kernels.f32_exact; the fp32 serving
+        path's bf16x3 split is within 1e-4 on logits but its ~2^-16 per-product
+        error is amplified ~200x into the conv-tower gradients by the BN backward)."""
+        if self.store.cfg.dtype == torch.float32:
+            with K.f32_exact():
+                return self._loss_and_grads(image, width, label)
+        return self._loss_and_grads(image, width, label)
+
+    def _loss_and_grads(self, image, width, label):
         store = self.store
         if host_labels(label) and not (isinstance(width, torch.Tensor) and width.is_cuda):
             check_feasible_host(label, width)

@@ -42,6 +42,19 @@ enum ocrk_status {
 
 enum ocrk_dtype { OCRK_F32 = 0, OCRK_BF16 = 1 };
 
+/* How OCRK_F32 operands are multiplied by every GEMM / implicit-GEMM conv entry point
+ * (process-wide; returns the previous mode or an error code):
+ *   0 (default) "bf16x3": each fp32 operand split into bf16 hi + lo and a product taken
+ *     as ah.bh + ah.bl + al.bh on the bf16 MFMA, f32 accumulation (~2^-16 relative per
+ *     product): the fp32 serving path (server.py:78-145 runs float32), logits within
+ *     1e-4 of the float64 graph;
+ *   1 "exact": v_mfma_f32_16x16x4_f32, exact fp32 products -- fp32 training
+ *     (train.Trainer on a float32 store), whose conv-tower gradients amplify product
+ *     errors through the BN backward. Also forced by OCRK_F32_MFMA=1.
+ * No reference counterpart (TF1 computes float32 on the CPU). */
+int ocrk_set_f32_gemm_mode(int mode);
+int ocrk_f32_gemm_exact(void);
+
 /* Device status word: a caller-owned, zero-initialised u32 in device memory.
  * Kernels OR these bits into it (agent-scope atomics) when a sequence cannot
  * be processed or a bounded device wait gives up, and still run to completion

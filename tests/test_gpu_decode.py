@@ -119,3 +119,15 @@ def test_get_testing_matches_oracle(cuda):
     assert abs(float(loss) - want_loss) < 1e-3 * max(1.0, abs(want_loss))
     assert abs(float(cer) - want_cer) < 1e-6
     assert abs(float(serr) - want_serr) < 1e-6
+
+
+def test_edit_distance_all_empty_decodes(cuda):
+    """A batch whose decodes are all empty (an untrained model emitting only
+    blanks) has a 0-column hypothesis tensor: the distance is each label's
+    length, as tf.edit_distance(normalize=False) gives for an empty hypothesis."""
+    from cnn_lstm_ctc_ocr_amd import decode
+    hyp = torch.empty(3, 0, dtype=torch.int64, device=cuda)
+    lab = torch.tensor([[1, 2, 3], [4, 0, 0], [0, 0, 0]], dtype=torch.int32, device=cuda)
+    ln = torch.tensor([3, 1, 0], dtype=torch.int32, device=cuda)
+    d = decode.edit_distance(hyp, torch.zeros(3, dtype=torch.int32, device=cuda), lab, ln)
+    assert d.cpu().tolist() == [3.0, 1.0, 0.0]

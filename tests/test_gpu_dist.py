@@ -158,3 +158,50 @@ def test_two_rank_status_raises_on_every_rank_at_the_same_step(cuda, tmp_path):
     mp.start_processes(_status_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     s0, s1 = np.load(tmp_path / "s0.npy"), np.load(tmp_path / "s1.npy")
     assert s0.tolist() == s1.tolist() == [3]             # step 0's word, read status_lag = 2 steps later
+
+
+def _bench_route_worker(rank, world, port, outdir):
+    """The bench's route: bf16 store, LSTM 512/512, persistent forward and BPTT
+    loops (B = 32 per rank: a 32-workgroup grid, so two ranks' loops fit the one
+    GPU side by side), side-stream weight gradients and the hook-started
+    recurrent bucket."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, kernels as K
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    dev = torch.device("cuda:0")
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.bfloat16), device=dev, seed=5)
+    assert K.lstm_persistent_ok(B, 512, torch.bfloat16)
+    tr = Trainer(store)
+    g = _grads(store, tr, rank, dev)
+    assert tr.buckets.work is None
+    tr.check_status()                                   # no hand-off wait gave up
+    np.save(os.path.join(outdir, f"g{rank}.npy"), g)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_bench_route_persistent_loops(cuda, tmp_path):
+    """the DP tests forced the per-step recurrent kernels. Here two
+    ranks run the bf16 persistent loops concurrently on the box's GPU; the
+    reduced gradient equals the sum of the two shards' gradients computed one
+    process at a time (every kernel's reductions run in a fixed order, so each
+    shard's gradient is reproducible) times 1/2."""
+    import torch.multiprocessing as mp
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_bench_route_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    g0, g1 = np.load(tmp_path / "g0.npy"), np.load(tmp_path / "g1.npy")
+    np.testing.assert_array_equal(g0, g1)
+    ref = []
+    for r in range(2):
+        store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.bfloat16), device=cuda, seed=5)
+        ref.append(_grads(store, Trainer(store), r, cuda))
+    want = (ref[0] + ref[1]) / 2
+    err = np.linalg.norm(g0 - want) / np.linalg.norm(want)
+    assert err < 1e-6, err

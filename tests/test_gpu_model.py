@@ -45,10 +45,13 @@ def test_forward_train_mode_loss_and_grads_fp32(cuda, cell):
     x = G.preprocess(img).astype(np.float64)
     loss_ref, grads_ref, _, logits_ref, seq_ref = ref.loss_and_grads(x, widths, labels)
     store.zero_grad()
-    feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN, store)
-    logits = model.rnn_layers(feats, seq, 95, store)
-    loss = model.ctc_loss_layer(logits, labels, seq)
-    loss.backward()
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    with K.f32_exact():                           # fp32 training precision (train.Trainer does the same)
+        feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN,
+                                          store)
+        logits = model.rnn_layers(feats, seq, 95, store)
+        loss = model.ctc_loss_layer(logits, labels, seq)
+        loss.backward()
     torch.cuda.synchronize()
     assert seq.cpu().numpy().tolist() == seq_ref.tolist()
     lg = logits.detach().cpu().numpy()
@@ -145,11 +148,14 @@ def test_ragged_batch_pads_inside_rnn_layers(cuda):
     ref = M.RefModel({k: v.astype(np.float64) for k, v in vals.items()}, "lstm", SIZES)
     loss_ref, grads_ref, _, logits_ref, _ = ref.loss_and_grads(G.preprocess(img).astype(np.float64), widths, labels)
     store.zero_grad()
-    feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN, store)
-    logits = model.rnn_layers(feats, seq, 95, store)
-    assert logits.shape[1] == 5
-    loss = model.ctc_loss_layer(logits, labels, seq)
-    loss.backward()
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    with K.f32_exact():
+        feats, seq = model.convnet_layers(torch.from_numpy(img).to(cuda), torch.from_numpy(widths), model.TRAIN,
+                                          store)
+        logits = model.rnn_layers(feats, seq, 95, store)
+        assert logits.shape[1] == 5
+        loss = model.ctc_loss_layer(logits, labels, seq)
+        loss.backward()
     lg = logits.detach().cpu().numpy()
     assert np.linalg.norm(lg - logits_ref) / np.linalg.norm(logits_ref) < 1e-4
     assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-4

@@ -33,11 +33,15 @@ def test_gemm_modes(cuda, dtype, ta, tb, M, N, K):
         A = torch.from_numpy(A).bfloat16().float().numpy()
         B = torch.from_numpy(B).bfloat16().float().numpy()
     ref = (A.T if ta else A).astype(np.float64) @ (B.T if tb else B).astype(np.float64) + bias
+    # fp32 operands run on the bf16x3 split (mfma_util.h: ~2^-16 relative per product,
+    # f32 accumulation): 2e-5 relative L2 on standard-normal operands; bf16 operands
+    # are exact products with f32 accumulation
+    tol = 2e-5 if dtype == torch.float32 else 2e-6
     out = Kn.gemm(_t(A, cuda, dtype), _t(B, cuda, dtype), trans_a=ta, trans_b=tb, bias=_t(bias, cuda))
-    assert _rel(out.cpu().numpy(), ref) < 2e-6
+    assert _rel(out.cpu().numpy(), ref) < tol
     out = Kn.gemm(_t(A, cuda, dtype), _t(B, cuda, dtype), trans_a=ta, trans_b=tb, bias=_t(bias, cuda), relu=True,
                   splits=3)
-    assert _rel(out.cpu().numpy(), np.maximum(ref, 0)) < 2e-6
+    assert _rel(out.cpu().numpy(), np.maximum(ref, 0)) < tol
 
 
 def test_gemm_accumulate_and_bf16_out(cuda):
@@ -48,7 +52,7 @@ def test_gemm_accumulate_and_bf16_out(cuda):
     C = rng.standard_normal((128, 32)).astype(np.float32)
     c = _t(C, cuda)
     Kn.gemm(_t(A, cuda), _t(B, cuda), out=c, accumulate=True)
-    np.testing.assert_allclose(c.cpu().numpy(), C + A @ B, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(c.cpu().numpy(), C + A @ B, rtol=1e-4, atol=1e-4)     # bf16x3 fp32 products
     ob = Kn.gemm(_t(A, cuda), _t(B, cuda), out_dtype=torch.bfloat16)
     np.testing.assert_allclose(ob.float().cpu().numpy(), A @ B, rtol=1e-2, atol=1e-2)
 
