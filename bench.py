@@ -297,13 +297,27 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
     batches = [(torch.from_numpy(img).to(device), torch.from_numpy(w))
                for i, (_u, img, w) in enumerate(allb) if i % world == rank]
 
+    # the beam search of bucket i runs on a second stream, beside the forward of
+    # bucket i + 1 (it is latency-bound on ~B/4 workgroups: one wave per sequence)
+    dec_stream = torch.cuda.Stream(device) if args.c5_pipeline else None
+
     def run():
         out = []
+        main = torch.cuda.current_stream(device)
         for img, w in batches:
             with torch.no_grad():
                 feats, seq = model.convnet_layers(img, w, model.INFER, store)
                 logits = model.rnn_layers(feats, seq, 95, store)
-                out.append(decode.ctc_beam_search_decoder_raw(logits, seq, beam_width=beam))
+                if dec_stream is None:
+                    out.append(decode.ctc_beam_search_decoder_raw(logits, seq, beam_width=beam))
+                    continue
+                dec_stream.wait_stream(main)
+                with torch.cuda.stream(dec_stream):
+                    out.append(decode.ctc_beam_search_decoder_raw(logits, seq, beam_width=beam))
+                logits.record_stream(dec_stream)
+                seq.record_stream(dec_stream)
+        if dec_stream is not None:
+            main.wait_stream(dec_stream)
         return out
     for _ in range(max(1, args.warmup // 2)):
         run()
@@ -325,7 +339,9 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
             "data": f"synthetic: {n_crops} uint8 crops, true widths U{{65..512}}, server-style 32-px buckets",
             "config": {"workload": "C5: bucketed INFER + CTC beam search (beam 16), LSTM 512/512",
                        "buckets": len(buckets), "crops": n_crops, "beam_width": beam,
-                       "parallelism": f"replicas x{world} (whole buckets per rank)"}}, elapsed, n_crops
+                       "parallelism": f"replicas x{world} (whole buckets per rank)",
+                       "decode": "second stream, beside the next bucket's forward" if args.c5_pipeline
+                       else "in line"}}, elapsed, n_crops
 
 
 def _free_port():
@@ -453,6 +469,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
                     help="c3: the headline train step (default); c2: B=64 fp32 fwd+CTC+greedy; "
                          "c5: bucketed 32x{64..512} crops, beam-16 decode")
+    ap.add_argument("--c5-pipeline", type=int, default=1,
+                    help="c5: 1 = each bucket's beam search on a second stream beside the next bucket's forward")
     ap.add_argument("--cell", default="lstm", choices=["lstm", "gru"],
                     help="lstm: model_bu.py's BiLSTM 512/512 (BASELINE.json's config); gru: model.py's BiGRU 512/256")
     ap.add_argument("--no-cpu-baseline", action="store_true")

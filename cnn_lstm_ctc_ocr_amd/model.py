@@ -227,6 +227,7 @@ class side_work:
 
 
 _DEFER_DWX = os.environ.get("OCRK_DEFER_DWX", "0") == "1"
+_DX_FIRST = os.environ.get("OCRK_DX_FIRST", "0") == "1"
 
 
 def _run_deferred(store):
@@ -300,9 +301,16 @@ class _BiLSTM(torch.autograd.Function):
         late = [] if _side_enabled("OCRK_SIDE_STREAM") else None
         dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer),
                         defer=late)
+        R = T * B
+        dx = None
+        # the lowest layer's data gradient first (OCRK_DX_FIRST=1): the side stream's
+        # weight-gradient GEMMs start behind it instead of taking the CUs it needs
+        # (it gates the whole conv-tower backward); upper layers keep dx beside dW_h
+        dx_first = _DX_FIRST and layer == 1 and ctx.needs_input_grad[0]
+        if dx_first:
+            dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
         _run_deferred(store)                                 # an upper layer's dW_x, now behind this BPTT
         pre = f"rnn/bdrnn{layer}"
-        R = T * B
         _issue(store, late)                                  # the bias partials' ordered sum
         with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
             gf, gb = store.grads[f"{pre}/fw/lstm_cell/kernel"], store.grads[f"{pre}/bw/lstm_cell/kernel"]
@@ -330,8 +338,7 @@ class _BiLSTM(torch.autograd.Function):
                            ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R, items=_tn_items(layer)))
                     K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
                            M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R, items=_tn_items(layer)))
-        dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and not dx_first:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
