@@ -67,12 +67,23 @@ def work_gemm(args):
     return 2.0 * args[2] * args[3] * args[4] * args[19]
 
 
+def work_dw(args):
+    # the recurrent weight gradients dW = x^T dG, h_prev^T dG (trans_a, M, N >= 256:
+    # gemm_pptn_kernel<A_COLK>, the step's largest kernel class); None filters the
+    # other ocrk_gemm launches out of the probe
+    if args[0] != 1 or args[2] < 256 or args[3] < 256:
+        return None
+    return work_gemm(args)
+
+
 ROOFLINE_OPS = {
     # conv2-conv5 run on the row-walking kernels (ocrk_conv3x3_fwd_rowstats for the BN layers)
     "conv": (("ocrk_conv3x3_fwd", "ocrk_conv3x3_fwd_rowstats"), work_conv_fwd,
              "conv2-conv8 forward launches (row-walking conv2-conv5, implicit GEMM conv6-conv8; MFMA bf16)"),
     "lstm": ("ocrk_lstm_fwd", work_lstm_fwd, "recurrent h.W_h time loop, both directions (MFMA bf16)"),
     "gemm": ("ocrk_gemm", work_gemm, "dense GEMM launches"),
+    "dw": ("ocrk_gemm", work_dw, "recurrent weight-gradient GEMMs dW = [x, h_prev]^T dG, both directions batched "
+           "(gemm_pptn_kernel<A_COLK>, side stream; MFMA bf16)"),
 }
 
 
@@ -458,6 +469,8 @@ def main():
     ap.add_argument("--width", type=int, default=256)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--roofline", default="conv", choices=sorted(ROOFLINE_OPS))
+    ap.add_argument("--roofline-also", default="dw",
+                    help="comma-separated further roofline kinds reported in roofline_also (same timed steps)")
     ap.add_argument("--mode", default="eager", choices=["graph", "eager"],
                     help="graph: forward+backward captured once as a HIP graph and replayed per step "
                          "(all-reduce + Adam eager); eager: every launch issued from Python each step")
@@ -522,15 +535,22 @@ def main():
     rng = np.random.default_rng(1234 + rank)                # per-rank seed = base + rank
     img, widths, labels = synthetic_batch(rng, B, W, T, device)
 
-    op_name, work_fn, op_desc = ROOFLINE_OPS[args.roofline]
-    probe = []
+    kinds = [args.roofline] + [k for k in args.roofline_also.split(",") if k and k != args.roofline]
+    probes = {k: [] for k in kinds}
     table = {}
-
+    op_name, work_fn, op_desc = ROOFLINE_OPS[args.roofline]
+    probe = probes[args.roofline]
     op_names = op_name if isinstance(op_name, tuple) else (op_name,)
+    # one probe per entry point: kinds sharing an entry point (gemm, dw) cannot both be armed
+    armed = {}
+    for k in kinds:
+        names = ROOFLINE_OPS[k][0]
+        for name in (names if isinstance(names, tuple) else (names,)):
+            armed.setdefault(name, k)
 
     def arm_probes():
-        for name in op_names:
-            _lib.PROBES[name] = (work_fn, probe)
+        for name, k in armed.items():
+            _lib.PROBES[name] = (ROOFLINE_OPS[k][1], probes[k])
         if args.breakdown:
             for name in _lib.SIGNATURES:
                 if name not in op_names and not name.endswith(("_size", "version", "last_error", "tiles")) \
@@ -544,7 +564,8 @@ def main():
         trainer.step(img, widths, labels)
         arm_probes()
         def drop_warmup_records():          # only the captured launches are timed
-            probe.clear()
+            for r in probes.values():
+                r.clear()
             for r in table.values():
                 r.clear()
         graphed = trainer.graphed(img, widths, labels, before_capture=drop_warmup_records)
@@ -586,26 +607,29 @@ def main():
     def read(records):
         return [a.elapsed_ms(b) for a, b, _ in records]
 
+    mss = {k: read(r) for k, r in probes.items()}
     if args.mode == "graph":
         # the timers in the graph hold the last timed step; K more replays, each
         # read back after a sync, complete the average over K steps
-        ms = read(probe)
         rows = {n: read(r) for n, r in table.items() if r}
         for _ in range(args.steps - 1):
             run_step()
             torch.cuda.synchronize()
-            ms += read(probe)
+            for k, r in probes.items():
+                mss[k] += read(r)
             for n, r in table.items():
                 if r:
                     rows[n] += read(r)
-        work = sum(w for _, _, w in probe) * args.steps
+        works = {k: sum(w for _, _, w in r) * args.steps for k, r in probes.items()}
     else:
-        ms = read(probe)
         rows = {n: read(r) for n, r in table.items() if r}
-        work = sum(w for _, _, w in probe)
+        works = {k: sum(w for _, _, w in r) for k, r in probes.items()}
+    ms, work = mss[args.roofline], works[args.roofline]
     avg_ms = sum(ms) / max(len(ms), 1)
     achieved = work / max(sum(ms), 1e-9) / 1e9          # FLOP/ms -> TFLOP/s
-    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32X3_TFLOPS
+    # bf16 step: the bf16 dense peak; an fp32 store trains with exact f32 MFMA
+    # products (train.Trainer -> kernels.f32_exact): the f32 peak
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
 
     if args.breakdown and rank == 0:
         rows = [(n, sum(v) / probed, len(v) // probed) for n, v in rows.items()]
@@ -651,8 +675,18 @@ def main():
         "loss": round(float(loss.item()), 4),
     }
     if dtype != torch.bfloat16:
-        result["roofline"]["peak_note"] = ("fp32 operands on the bf16x3 split (3 bf16 MFMA products per fp32 "
-                                           "product): peak = bf16 dense 2500 / 3 TFLOP/s")
+        result["roofline"]["peak_note"] = "fp32 training runs exact f32 MFMA products: f32 dense peak"
+    for k in kinds[1:]:
+        m_k, w_k = mss[k], works[k]
+        if not m_k:
+            continue
+        a_k = w_k / max(sum(m_k), 1e-9) / 1e9
+        result.setdefault("roofline_also", []).append(
+            {"bound": "mfma", "kernel": ROOFLINE_OPS[k][2], "achieved": round(a_k, 2), "peak": round(peak, 1),
+             "unit": "TFLOP/s", "frac": round(a_k / peak, 4), "launches_per_step": len(m_k) // max(probed, 1),
+             "avg_launch_ms": round(sum(m_k) / len(m_k), 4), "algorithmic_flop_per_launch": w_k / len(m_k),
+             "timing": "HIP events bracketing each launch on its stream (incl. any wait for CUs the "
+                       "launch's workgroups spend queued behind other streams' kernels)"})
     if args.roofline == "conv" and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             pmc = json.load(fh)

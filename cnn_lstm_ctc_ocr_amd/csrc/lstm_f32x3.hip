@@ -6,9 +6,9 @@
 // f32 accumulation) -- the per-step fp32 kernels (csrc/lstm.hip) took 8.3 us
 // per step on the f32 MFMA plus a launch each.
 //
-// Work split (H = 512): 2 directions x B/32 batch slices = groups, each of 16
-// member workgroups owning 32 hidden units (as lstm_persistent.hip), but 8
-// waves: wave w owns units 4w..4w+3 x 4 gates = one 16-column MFMA N-tile, its
+// Work split (H = 512): 2 directions x B/RB batch slices = groups (RB = 16 rows
+// when that grid is co-resident, B <= 128, else 32), each of 16 member
+// workgroups owning 32 hidden units (as lstm_persistent.hip), but 8 waves: wave w owns units 4w..4w+3 x 4 gates = one 16-column MFMA N-tile, its
 // W_h^T slice split once into hi / lo bf16 B fragments resident in VGPRs (2 x 16
 // k-steps x 4 VGPRs = 128). Per step a member
 //   1. waits until the group published h_{s-1} (flag words, bounded spin);
@@ -25,8 +25,6 @@
 //      asked (training), the tensors the BPTT reads.
 // The hand-off form, the XCC census and the counting flag words are
 // persist.h's, exactly as the bf16 loop uses them.
-#include <type_traits>
-
 #include "common.h"
 #include "mfma_util.h"
 #include "persist.h"
@@ -44,26 +42,35 @@ __device__ __forceinline__ void put4(gu32* p, unsigned v, bool local) {
 constexpr int X3_KS = 16;                       // H = 512
 constexpr int X3_THREADS = 512;
 
+}  // namespace
+
+// RB = batch rows per group slice: 32, or 16 when the grid 2 (B/16) (H/32) still
+// fits one workgroup per CU (B <= 128 at H = 512) -- half the staged rows and half
+// the MFMAs per member per step (one M-tile), on twice the CUs.
+template <int RB>
 __global__ void __launch_bounds__(X3_THREADS, 1)
 lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __restrict__ whT,
                                  unsigned short* __restrict__ hx, const int* __restrict__ seq_len, int T, int B,
                                  float* __restrict__ out, float* __restrict__ hprev_t, float* __restrict__ cprev_t,
                                  float* __restrict__ acts_t, unsigned* __restrict__ flags,
                                  unsigned* __restrict__ err, unsigned spin_limit) {
+    static_assert(RB == 16 || RB == 32, "row slices of 16 or 32");
     constexpr int KS = X3_KS;
     constexpr int H = KS * 32;
     constexpr int G4 = 4 * H;
     constexpr int NU = H / PHU;                         // members per group (16)
+    constexpr int MT = RB / 16;                         // MFMA M-tiles per member
     constexpr int LDH = H + 8;                          // padded staged row (bf16 elements)
     constexpr int LDG = 4 * PHU + 4;                    // padded gate row (floats)
-    __shared__ __attribute__((aligned(16))) unsigned short sh[2 * PBR * LDH];    // [hi | lo][row][k]
-    __shared__ __attribute__((aligned(16))) float sG[PBR * LDG];                 // [row][gate][unit]
-    __shared__ int s_len[PBR];
+    constexpr int CELLS = RB * 16;                      // cell threads: (row, 2 units) each
+    constexpr int DPW = 2 * RB / 8;                     // staging DMAs per wave (both planes)
+    __shared__ __attribute__((aligned(16))) unsigned short sh[2 * RB * LDH];     // [hi | lo][row][k]
+    __shared__ __attribute__((aligned(16))) float sG[RB * LDG];                  // [row][gate][unit]
 
     int group, member;
-    persistent_role(2 * (B / PBR), NU, group, member);
+    persistent_role(2 * (B / RB), NU, group, member);
     const int dir = group & 1, bs = group >> 1;
-    const int u0 = member * PHU, b0 = bs * PBR;
+    const int u0 = member * PHU, b0 = bs * RB;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     gu32* gflags = (gu32*)(flags) + group * NU;
@@ -87,13 +94,12 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
         for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(bh[ks]), "v"(bl[ks]));   // settled before the loop
     }
 
-    // ---- the cell item of this thread: row er, units eu, eu + 1 (all 4 gates)
-    const int er = tid >> 4, eu = 2 * (tid & 15);
+    // ---- the cell item of this thread (tid < CELLS): row er, units eu, eu + 1 (all 4 gates)
+    const bool cell = tid < CELLS;
+    const int er = cell ? tid >> 4 : 0, eu = 2 * (tid & 15);
     const int elen = seq_len[b0 + er];
     asm volatile("" ::"v"(elen));
     float cst[2] = {0.f, 0.f}, hst[2] = {0.f, 0.f};
-    if (tid < PBR) s_len[tid] = seq_len[b0 + tid];
-    __syncthreads();
 
     const int64_t hx_plane = (int64_t)2 * 2 * B * H;    // elements per plane ([parity][dir][B][H])
     auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, (int)(2 * hx_plane * 2), 0x00020000);
@@ -104,7 +110,7 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
         const bool valid = s < elen;
         const int t = step_time(dir, s, elen);
         float gxv[4][2];
-        auto load_gx = [&]() {
+        auto load_gx = [&]() {                           // 4 buffer loads (out of range reads 0 when idle)
             const int64_t e = (((int64_t)t * B + b0 + er) * 2 + dir) * G4 + u0 + eu;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -114,7 +120,9 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
                 gxv[q][1] = v[1];
             }
         };
-        floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+        floatx4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
         if (s > 0) {
             // 1. wait until every member of the group published h_{s-1} (flag >= base + s)
             if (w == 0) {
@@ -135,30 +143,28 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
             const int64_t hbase = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
             const int wu = __builtin_amdgcn_readfirstlane(w);
             const unsigned lo16 = (unsigned)(lane * 16);
-            auto stage = [&](auto aux) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int pr = wu * 8 + q, plane = pr >> 5, r = pr & 31;
-                    const unsigned off = (unsigned)(((int64_t)plane * hx_plane + hbase + (int64_t)r * H) * 2) + lo16;
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        hx_rsrc, (__attribute__((address_space(3))) void*)(sh + (plane * PBR + r) * LDH), 16, off, 0, 0,
-                        decltype(aux)::value);
-                }
-            };
-            if (local) stage(std::integral_constant<int, 2>{});          // nt: the group's XCD L2
-            else stage(std::integral_constant<int, 16>{});               // sc1: any placement
+#define X3_STAGE(AUX)                                                                                  \
+    _Pragma("unroll") for (int q = 0; q < DPW; ++q) {                                                 \
+        const int pr = wu * DPW + q, plane = pr / RB, r = pr % RB;                                    \
+        const unsigned off = (unsigned)(((int64_t)plane * hx_plane + hbase + (int64_t)r * H) * 2) + lo16; \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
+            hx_rsrc, (__attribute__((address_space(3))) void*)(sh + (plane * RB + r) * LDH), 16, off, 0, 0, AUX); \
+    }
+            if (local) { X3_STAGE(2) }                           // nt: the group's XCD L2
+            else { X3_STAGE(16) }                                // sc1: any placement
+#undef X3_STAGE
             asm volatile("" ::: "memory");
-            load_gx();                                          // 4 loads behind the 8 DMAs
+            load_gx();                                          // 4 loads behind the staging DMAs
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             __syncthreads();
             // 3. gates += h_{s-1} . W_h on the bf16x3 split
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     const unsigned short* ap = &sh[(16 * mt + c) * LDH + ks * 32 + 8 * g];
                     const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ap);
-                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(ap + PBR * LDH);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(ap + RB * LDH);
                     acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks], acc[mt], 0, 0, 0);
                     acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks], acc[mt], 0, 0, 0);
                     acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks], acc[mt], 0, 0, 0);
@@ -169,7 +175,7 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
         }
         // 4. gate pre-activations through LDS: lane (c, g) holds rows 16 mt + 4 g + r of column c
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 sG[(16 * mt + 4 * g + r) * LDG + (c >> 2) * PHU + 4 * w + (c & 3)] = acc[mt][r];
@@ -202,7 +208,7 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
         }
 
         // 6. publish h_s as its hi / lo split (one 4-B store per plane), drain, barrier, flag
-        {
+        if (cell) {
             unsigned hi, lo;
             split2_bf16(hn[0], hn[1], hi, lo);
             const int64_t o = ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu;
@@ -214,39 +220,58 @@ lstm_fwd_persistent_f32x3_kernel(const float* __restrict__ gx, const float* __re
         if (tid == 0) raise_flag(gflags + member, base + (unsigned)(s + 1), local);
 
         // 7. the layer output (zeros past the length) and, for the BPTT, the saved tensors
-        {
+        if (cell) {
             const f32x2_t ov = {valid ? hn[0] : 0.f, valid ? hn[1] : 0.f};
             *reinterpret_cast<f32x2_t*>(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu) = ov;
-        }
-        if (save) {
-            const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
-            *reinterpret_cast<f32x2_t*>(hprev_t + tb * H + u0 + eu) = f32x2_t{hp[0], hp[1]};
-            *reinterpret_cast<f32x2_t*>(cprev_t + tb * H + u0 + eu) = f32x2_t{cp[0], cp[1]};
+            if (save) {
+                const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+                *reinterpret_cast<f32x2_t*>(hprev_t + tb * H + u0 + eu) = f32x2_t{hp[0], hp[1]};
+                *reinterpret_cast<f32x2_t*>(cprev_t + tb * H + u0 + eu) = f32x2_t{cp[0], cp[1]};
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<f32x2_t*>(acts_t + tb * G4 + q * H + u0 + eu) = f32x2_t{a4[q][0], a4[q][1]};
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<f32x2_t*>(acts_t + tb * G4 + q * H + u0 + eu) = f32x2_t{a4[q][0], a4[q][1]};
+            }
         }
     }
 }
 
-}  // namespace
+// rows per member for batch B: 16 when that grid is co-resident, else 32
+template <int RB>
+static bool x3_fits(int B, int H, int cus) {
+    int per_cu = 0;
+    if (B % RB ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_fwd_persistent_f32x3_kernel<RB>, X3_THREADS, 0) !=
+            hipSuccess)
+        return false;
+    return 2L * (B / RB) * (H / PHU) <= (long)cus * per_cu;
+}
+
+static int x3_rows(int B, int H) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (x3_fits<16>(B, H, cus)) return 16;
+    if (x3_fits<32>(B, H, cus)) return 32;
+    return 0;
+}
 
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_f32_workspace_size(int B, int H) {
-    // flag word + XCC word per workgroup (128-B block), then the hi / lo h exchange planes
-    return persistent_counter_bytes(B, H) + (size_t)2 * 2 * 2 * B * H * sizeof(unsigned short);
+    // flag word + XCC word per workgroup at 16-row slices (the larger count; 128-B block),
+    // then the hi / lo h exchange planes
+    const size_t counters = ((size_t)2 * 2 * (B / 16) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128;
+    return counters + (size_t)2 * 2 * 2 * B * H * sizeof(unsigned short);
+}
+
+// the counting hand-off words of this loop (sized for 16-row slices)
+extern "C" size_t ocrk_lstm_fwd_persistent_f32_flags_size(int B, int H) {
+    return (B > 0 && B % 16 == 0 && H > 0 && H % PHU == 0)
+               ? ((size_t)2 * 2 * (B / 16) * (H / PHU) * sizeof(unsigned) + 127) / 128 * 128 : 0;
 }
 
 extern "C" int ocrk_lstm_fwd_persistent_f32_supported(int B, int H) {
-    if (B <= 0 || B % PBR || H != 32 * X3_KS) return 0;
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_fwd_persistent_f32x3_kernel, X3_THREADS, 0) !=
-        hipSuccess)
-        return 0;
-    const long grid = 2L * (B / PBR) * (H / PHU);
-    return grid <= (long)cus * per_cu ? 1 : 0;
+    if (B <= 0 || H != 32 * X3_KS) return 0;
+    return x3_rows(B, H) ? 1 : 0;
 }
 
 extern "C" int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, const int* seq_len, int T, int B,
@@ -262,13 +287,18 @@ extern "C" int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, c
     OCRK_REQUIRE((int64_t)T * B * 8 * H * 4 < 0x7fffffffll, "ocrk_lstm_fwd_persistent_f32: gx exceeds 2 GB");
     OCRK_REQUIRE(T >= 1, "ocrk_lstm_fwd_persistent_f32: T=%d", T);
     hipStream_t st = ocrk::as_stream(stream);
-    const size_t counters = persistent_counter_bytes(B, H);
+    const size_t counters = ocrk_lstm_fwd_persistent_f32_flags_size(B, H);
     unsigned* cnt = flags ? flags : (unsigned*)ws;
     unsigned short* hx = (unsigned short*)((char*)ws + counters);
     if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
         return ocrk::launch_status("ocrk_lstm_fwd_persistent_f32 memset");
-    const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
-    lstm_fwd_persistent_f32x3_kernel<<<grid, X3_THREADS, 0, st>>>(gx, whT, hx, seq_len, T, B, out, hprev_t, cprev_t,
-                                                                   acts_t, cnt, err, recur_spin_limit());
+    const int rb = x3_rows(B, H);
+    const unsigned grid = 2u * (unsigned)(B / rb) * (unsigned)(H / PHU);
+    if (rb == 16)
+        lstm_fwd_persistent_f32x3_kernel<16><<<grid, X3_THREADS, 0, st>>>(gx, whT, hx, seq_len, T, B, out, hprev_t,
+                                                                         cprev_t, acts_t, cnt, err, recur_spin_limit());
+    else
+        lstm_fwd_persistent_f32x3_kernel<32><<<grid, X3_THREADS, 0, st>>>(gx, whT, hx, seq_len, T, B, out, hprev_t,
+                                                                         cprev_t, acts_t, cnt, err, recur_spin_limit());
     return ocrk::launch_status("ocrk_lstm_fwd_persistent_f32");
 }

@@ -272,7 +272,7 @@ _STATUS = {}
 _FLAGS = {}
 
 
-def persistent_flags(kind, B, H, device):
+def persistent_flags(kind, B, H, device, size_fn="ocrk_persistent_flags_size"):
     """The counting hand-off words of one persistent entry point (include/ocrk.h,
     ocrk_persistent_flags_size): zeroed once per (entry point, B, H, device,
     stream) and kept, so the loops need no clearing launch in front of them.
@@ -282,7 +282,7 @@ def persistent_flags(kind, B, H, device):
     key = (kind, B, H, device, torch.cuda.current_stream(device).cuda_stream)
     t = _FLAGS.get(key)
     if t is None:
-        nb = _lib.lib().ocrk_persistent_flags_size(B, H)
+        nb = getattr(_lib.lib(), size_fn)(B, H)
         t = _FLAGS[key] = torch.zeros(max(int(nb), 16) // 4, dtype=torch.int32, device=device)
     return t
 
@@ -363,7 +363,7 @@ def f32_mode_exact():
 
 def lstm_f32_persistent_ok(B, H):
     """Run the fp32 forward loop as one persistent launch on the bf16x3 split
-    (csrc/lstm_f32x3.hip)? H = 512, B % 32 == 0 and the grid co-resident; not
+    (csrc/lstm_f32x3.hip)? H = 512, B % 16 == 0 and the grid co-resident; not
     in exact fp32 mode (f32_exact); OCRK_LSTM_PERSISTENT=0 selects the per-step
     fp32 kernels."""
     import os
@@ -393,7 +393,8 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype, save=True):
         nb = _lib.lib().ocrk_lstm_fwd_persistent_f32_workspace_size(B, H)
         ws = _ws(nb, dev)
         call("ocrk_lstm_fwd_persistent_f32", ptr(gx), ptr(whT), ptr(seq_len), T, B, H, ptr(out), ptr(hprev),
-             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_fwd_f32", B, H, dev)),
+             ptr(cprev), ptr(acts), ptr(lstm_error_word(dev)),
+             ptr(persistent_flags("lstm_fwd_f32", B, H, dev, "ocrk_lstm_fwd_persistent_f32_flags_size")),
              ptr(ws), nb, _stream(gx))
         return out, hprev, cprev, acts
     if lstm_persistent_ok(B, H, dtype):

@@ -263,11 +263,15 @@ int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* wxT, const f
  * f32 accumulate; ~2^-16 relative per product). gx f32 [T][B][2][4H] (bias included),
  * whT f32 [2][4H][H]; out f32 [T][B][2H] (zeros past each row's length);
  * hprev_t / cprev_t f32 [T][B][2][H] and acts_t f32 [T][B][2][4H] for the BPTT, or
- * all three NULL (inference). H = 512, B % 32 == 0, grid 2 (B/32) (H/32) co-resident;
- * flags as ocrk_lstm_fwd_persistent (ocrk_persistent_flags_size(B, H)); status bits
+ * all three NULL (inference). H = 512, B % 16 == 0, grid 2 (B/RB) (H/32) co-resident
+ * (RB = 16 or 32 rows per member); flags: ocrk_lstm_fwd_persistent_f32_flags_size(B, H)
+ * zeroed words kept by the caller (or NULL: cleared per launch); status bits
  * OCRK_STATUS_LSTM_FWD_TIMEOUT / _CENSUS. */
 int ocrk_lstm_fwd_persistent_f32_supported(int B, int H);
 size_t ocrk_lstm_fwd_persistent_f32_workspace_size(int B, int H);
+/* The caller-kept counting hand-off words of this loop (it slices the batch by 16 rows
+ * when that grid is co-resident, B <= 128 at H = 512, else by 32). */
+size_t ocrk_lstm_fwd_persistent_f32_flags_size(int B, int H);
 int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, const int* seq_len, int T, int B, int H,
                                  float* out, float* hprev_t, float* cprev_t, float* acts_t, unsigned* err,
                                  unsigned* flags, void* ws, size_t ws_bytes, void* stream);
