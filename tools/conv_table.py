@@ -20,6 +20,7 @@ LAYERS = [("conv2", 30, 254, 32, 32), ("conv3", 15, 127, 32, 64), ("conv4", 15, 
           ("conv5", 7, 126, 64, 128), ("conv6", 7, 126, 128, 128), ("conv7", 3, 125, 128, 256),
           ("conv8", 3, 125, 256, 256)]
 PEAK = 2500.0   # dense bf16 TFLOP/s, MI355X_MICROARCH.md
+HBM = 8.0       # TB/s, HBM3E spec
 
 
 def rows(root, name):
@@ -66,8 +67,11 @@ def main():
         return out
 
     fetch, write = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
-    lines = ["| layer | kernel | us | TFLOP/s | MFMA frac | algorithmic MB | counter MB | counter / algorithmic |",
-             "|---|---|---|---|---|---|---|---|"]
+    # each kernel against min(MFMA peak, AI x HBM bandwidth), AI = algorithmic
+    # FLOP / algorithmic bytes (input + output activations + weights)
+    lines = ["| layer | kernel | us | TFLOP/s | MFMA frac | AI FLOP/B | roofline TFLOP/s | roofline frac | "
+             "algorithmic MB | counter MB | counter / algorithmic |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     tot_us = tot_fl = 0.0
     for name, H, W, cin, cout in LAYERS:
         M = B * H * W
@@ -77,12 +81,15 @@ def main():
         rd = 2 * sum(fetch[name]) / max(len(fetch[name]), 1)
         wr = sum(write[name]) / max(len(write[name]), 1)
         tf = fl / us / 1e6
+        ai = fl / alg
+        roof = min(PEAK, ai * HBM)
         tot_us += us
         tot_fl += fl
         lines.append(f"| {name} {cin}->{cout} | `{names.get(name, '?')}` | {us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | "
-                     f"{alg / 1e6:.1f} | {(rd + wr) / 1e6:.1f} | {(rd + wr) / alg:.2f} |")
+                     f"{ai:.0f} | {roof:.0f} | {tf / roof:.3f} | {alg / 1e6:.1f} | {(rd + wr) / 1e6:.1f} | "
+                     f"{(rd + wr) / alg:.2f} |")
     tf = tot_fl / tot_us / 1e6
-    lines.append(f"| all | | {tot_us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | | | |")
+    lines.append(f"| all | | {tot_us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | | | | | | |")
     txt = "\n".join(lines) + "\n"
     with open(a.out, "w") as fh:
         fh.write(txt)

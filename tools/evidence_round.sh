@@ -14,5 +14,8 @@ timeout -k 10 200 python3 -u bench.py --config c2 --no-cpu-baseline > "$out/benc
 grep '^{' "$out/bench_c2.log" | tail -1 > "$out/bench_c2.json"
 timeout -k 10 300 python3 -u bench.py --config c5 --no-cpu-baseline > "$out/bench_c5.log" 2>&1 || exit $?
 grep '^{' "$out/bench_c5.log" | tail -1 > "$out/bench_c5.json"
+# the C3 train step at the reference's precision (fp32 store: exact f32 MFMA products)
+timeout -k 10 300 python3 -u bench.py --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline --no-cer > "$out/bench_fp32.log" 2>&1 || exit $?
+grep '^{' "$out/bench_fp32.log" | tail -1 > "$out/bench_fp32.json"
 bash tools/profile_round.sh "$tag" || exit $?
 python3 tools/timeline.py "$(find gpurun_out/prof_$tag/trace -name '*kernel_trace.csv' | head -1)" > "$out/step_timeline.txt" || exit $?

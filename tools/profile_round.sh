@@ -21,5 +21,7 @@ python3 tools/pmc_traffic.py --fetch "$out/fetch" --write "$out/write" --match "
     --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- ${pmc[*]}" --out "$out/pmc_conv.json" || exit $?
 find "$out/trace" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
 python3 tools/conv_table.py --trace "$out/trace" --fetch "$out/fetch" --write "$out/write" --out "$out/conv_layers.md" || exit $?
+python3 tools/kernel_table.py --trace "$out/trace" --fetch "$out/fetch" --write "$out/write" --steps 7 --pmc-steps 2 \
+    --out "$out/kernel_table.md" || exit $?
 grep '^{' "$out/trace.log" | tail -1 > "$out/bench_under_trace.json"
 true
