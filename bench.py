@@ -240,18 +240,21 @@ def run_c2(args, world, rank, device):
     """BASELINE configs[1] (C2): B=64 synthetic 32x256 crops, INFER forward +
     CTC loss + greedy decode, fp32 (test.py:75-104's evaluation graph with the
     greedy decoder of validate.py:81-92). One line, value = crops/s."""
-    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, model, validate
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
     B, W = 64, 256
     T = (W - 2) // 2 - 2
     store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.float32), device=device, seed=0)
     img, widths, labels = synthetic_batch(np.random.default_rng(1234 + rank), B, W, T, device)
 
     def step():
+        # the decode stays on the device (ctc_greedy_decoder_raw: [B, T] labels then -1):
+        # validate._get_output's host read of the longest decode (its dense width) would
+        # serialise every batch's launches behind the previous batch's kernels
         with torch.no_grad():
             feats, seq = model.convnet_layers(img, widths, model.INFER, store)
             logits = model.rnn_layers(feats, seq, 95, store)
             loss = model.ctc_loss_layer(logits, labels, seq, check=False)
-            dense = validate._get_output(logits, seq)[0]
+            dense = decode.ctc_greedy_decoder_raw(logits, seq)[0]
         return loss, dense
     for _ in range(args.warmup):
         step()
@@ -271,6 +274,7 @@ def run_c2(args, world, rank, device):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (uint8 crops, labels len U{2..19}; reference initialisers)",
             "config": {"workload": "C2: INFER fwd + CTC loss + greedy, LSTM 512/512", "per_gpu_batch": B,
+                       "decode_output": "device [B, T] dense (-1 padded), read back after the timed steps",
                        "image": f"32x{W}", "parallelism": f"dp{world}"},
             "loss": round(float(loss.item()), 4)}, elapsed, world * B * args.steps
 

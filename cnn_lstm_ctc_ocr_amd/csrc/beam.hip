@@ -516,10 +516,10 @@ ctc_beam_wave_kernel(const float* __restrict__ logits, const int* __restrict__ s
         const float v0 = n0, v1 = n1;
         if (t + 1 < L) load_row(t + 1, n0, n1);          // the next frame's loads in flight over this one
         // ---- log-softmax of the frame (Step(): max removed, then norm_offset), the block form's order
-        const float m = rlf(wave_max(fmaxf(v0, v1)), 0);
+        const float m = wave_max_dpp(fmaxf(v0, v1));
         const float e0 = L0 < C ? expf(v0 - m) : 0.f;
         const float e1 = L1 < C ? expf(v1 - m) : 0.f;
-        const float z = rlf(wave_sum(e0), 0) + rlf(wave_sum(e1), 0);
+        const float z = wave_sum_dpp(e0) + wave_sum_dpp(e1);
         const float norm = logf(z);
         const float x0 = (v0 - m) - norm, x1 = (v1 - m) - norm;
         const float xb = blank < 64 ? rlf(x0, blank) : rlf(x1, blank - 64);
@@ -606,51 +606,54 @@ ctc_beam_wave_kernel(const float* __restrict__ logits, const int* __restrict__ s
             }
         }
 
-        // ---- selection: K rounds of the wave-minimum key over the sorted heads
+        // ---- selection: K rounds of the wave-minimum key over the sorted heads. Each
+        //      round only the winning lane advances one head; its next key's parent total
+        //      is a v_readlane at the (uniform) winner's pointer -- no LDS round trip.
         const unsigned avail0 = ok0 ? (all_n & ~(act0 | own0 | W)) : 0u;
         const unsigned avail1 = ok1 ? (all_n & ~(act1 | own1 | W)) : 0u;
         int ptr0 = avail0 ? __builtin_ctz(avail0) : 32, ptr1 = avail1 ? __builtin_ctz(avail1) : 32;
-        // own-label child of the beam in this lane
-        float vo = xl + bob;
-        bool own_live = lane < n && blab >= 0 && !((W >> lane) & 1u) && !((ownact >> lane) & 1u) && vo > tau;
-        bool beam_live = lane < n;
+        auto label_key = [&](float xv, int ptr, int lab, float o) {
+            if (ptr >= n) return ~0ull;
+            const float v = xv + o;
+            // the rest of this label's parents rank lower: nothing further can beat tau either
+            return v > tau ? ((desc_bits(v) << ORDER_BITS) | (uint64_t)(n + ptr * C + lab)) : ~0ull;
+        };
+        uint64_t key0 = label_key(x0, ptr0, L0, __shfl(bot, ptr0 & 63, 64));
+        uint64_t key1 = label_key(x1, ptr1, L1, __shfl(bot, ptr1 & 63, 64));
+        // own-label child of the beam in this lane, and the beam itself
+        const float vo = xl + bob;
+        uint64_t keyo = (lane < n && blab >= 0 && !((W >> lane) & 1u) && !((ownact >> lane) & 1u) && vo > tau)
+                            ? ((desc_bits(vo) << ORDER_BITS) | (uint64_t)(n + lane * C + blab)) : ~0ull;
+        uint64_t keyb = lane < n ? ((desc_bits(nt) << ORDER_BITS) | (uint64_t)lane) : ~0ull;
         uint64_t selk = ~0ull;
         int ns = 0;
         for (int k = 0; k < K; ++k) {
-            const float o0 = __shfl(bot, ptr0 & 63, 64), o1 = __shfl(bot, ptr1 & 63, 64);
-            uint64_t key = ~0ull;
-            if (ptr0 < n) {
-                const float v = x0 + o0;
-                if (v > tau) key = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + ptr0 * C + L0);
-                else ptr0 = 32;                          // the rest of this label's parents rank lower
-            }
-            uint64_t key1 = ~0ull;
-            if (ptr1 < n) {
-                const float v = x1 + o1;
-                if (v > tau) key1 = (desc_bits(v) << ORDER_BITS) | (uint64_t)(n + ptr1 * C + L1);
-                else ptr1 = 32;
-            }
-            const uint64_t keyo = own_live ? ((desc_bits(vo) << ORDER_BITS) | (uint64_t)(n + lane * C + blab)) : ~0ull;
-            const uint64_t keyb = beam_live ? ((desc_bits(nt) << ORDER_BITS) | (uint64_t)lane) : ~0ull;
-            uint64_t mine = key < key1 ? key : key1;
+            uint64_t mine = key0 < key1 ? key0 : key1;
             mine = mine < keyo ? mine : keyo;
             mine = mine < keyb ? mine : keyb;
             const uint64_t kmin = wave_min_u64(mine);
             if (kmin == ~0ull) break;
             if (lane == k) selk = kmin;
             ++ns;
-            if (mine == kmin) {
-                if (key == kmin) {
+            const int win = __builtin_ctzll(__ballot(mine == kmin));          // the one lane holding it
+            if (lane == win) {
+                if (key0 == kmin) {
                     const unsigned rest = avail0 & ~((2u << ptr0) - 1u);
                     ptr0 = rest ? __builtin_ctz(rest) : 32;
                 } else if (key1 == kmin) {
                     const unsigned rest = avail1 & ~((2u << ptr1) - 1u);
                     ptr1 = rest ? __builtin_ctz(rest) : 32;
                 } else if (keyo == kmin) {
-                    own_live = false;
+                    keyo = ~0ull;
                 } else {
-                    beam_live = false;
+                    keyb = ~0ull;
                 }
+            }
+            const int p0w = rli(ptr0, win), p1w = rli(ptr1, win);
+            const float o0w = rlf(bot, p0w & 63), o1w = rlf(bot, p1w & 63);
+            if (lane == win) {
+                key0 = label_key(x0, ptr0, L0, o0w);
+                key1 = label_key(x1, ptr1, L1, o1w);
             }
         }
 

@@ -469,7 +469,9 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
     if (dtype == OCRK_F32) {
         // fp32: the bf16x3 split on this ring (the generic engine keeps the short-K
         // shapes, the masked data gradients and OCRK_F32_MFMA=1)
-        if (f32_exact_mfma() || p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 512 && p0.N > 64)) return -1;
+        // (K >= 256 here: the first recurrent layer's input projection, K = 256, ran 3x
+        // slower on the generic engine's bf16x3 staging -- 463 vs ~150 us per C5 bucket)
+        if (f32_exact_mfma() || p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 256 && p0.N > 64)) return -1;
         GemmParams p = p0;
         p.epi_staged = 0;
         if (amode == A_ROWK) {

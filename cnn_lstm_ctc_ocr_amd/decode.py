@@ -26,6 +26,12 @@ def ctc_greedy_decoder(inputs, sequence_length, merge_repeated=True):
     return [out[:, :width]], neg.unsqueeze(1)
 
 
+def ctc_greedy_decoder_raw(inputs, sequence_length, merge_repeated=True):
+    """The same decode without the host sync for the output width: (out i64
+    [B, T] (labels then -1), out_len i32 [B], neg_sum_logits f32 [B])."""
+    return K.ctc_greedy_decode(_f32(inputs), sequence_length.to(torch.int32).contiguous(), merge_repeated)
+
+
 def ctc_beam_search_decoder(inputs, sequence_length, beam_width=100, top_paths=1, merge_repeated=True):
     """Returns (decoded, log_probability): decoded is a list of top_paths
     dense i64 [B, max_len_k] tensors (-1 padded), log_probability f32
