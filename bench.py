@@ -256,6 +256,15 @@ def run_c2(args, world, rank, device):
             loss = model.ctc_loss_layer(logits, labels, seq, check=False)
             dense = decode.ctc_greedy_decoder_raw(logits, seq)[0]
         return loss, dense
+    if args.c2_mode == "graph":
+        # the same launches captured once (infer.InferGraph on the resident batch) and
+        # replayed: one graph launch per batch instead of the Python walk over ~45 ops
+        from cnn_lstm_ctc_ocr_amd.infer import InferGraph
+        g = InferGraph(store, image=img, widths=widths, labels=labels, n_classes=95)
+
+        def step():   # noqa: F811
+            g.replay()
+            return g.loss, g.decoded
     for _ in range(args.warmup):
         step()
     if world > 1:
@@ -275,6 +284,8 @@ def run_c2(args, world, rank, device):
             "data": "synthetic (uint8 crops, labels len U{2..19}; reference initialisers)",
             "config": {"workload": "C2: INFER fwd + CTC loss + greedy, LSTM 512/512", "per_gpu_batch": B,
                        "decode_output": "device [B, T] dense (-1 padded), read back after the timed steps",
+                       "execution": "hipGraph replay per batch (infer.InferGraph)" if args.c2_mode == "graph"
+                       else "eager launches",
                        "image": f"32x{W}", "parallelism": f"dp{world}"},
             "loss": round(float(loss.item()), 4)}, elapsed, world * B * args.steps
 
@@ -316,13 +327,28 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
     # bucket i + 1 (it is latency-bound on ~B/4 workgroups: one wave per sequence)
     dec_stream = torch.cuda.Stream(device) if args.c5_pipeline else None
 
+    graphs = None
+    if args.c5_mode == "graph":
+        # one captured INFER forward per bucket shape (infer.InferGraph on the resident
+        # bucket), the beam search launched eagerly beside it
+        from cnn_lstm_ctc_ocr_amd.infer import InferGraph
+        graphs = [InferGraph(store, image=img, widths=w.to(device), decoder=None, n_classes=95)
+                  for img, w in batches]
+
+    def forward(i):
+        if graphs is not None:
+            g = graphs[i].replay()
+            return g.logits, g.seq_len
+        img, w = batches[i]
+        feats, seq = model.convnet_layers(img, w, model.INFER, store)
+        return model.rnn_layers(feats, seq, 95, store), seq
+
     def run():
         out = []
         main = torch.cuda.current_stream(device)
-        for img, w in batches:
+        for i in range(len(batches)):
             with torch.no_grad():
-                feats, seq = model.convnet_layers(img, w, model.INFER, store)
-                logits = model.rnn_layers(feats, seq, 95, store)
+                logits, seq = forward(i)
                 if dec_stream is None:
                     out.append(decode.ctc_beam_search_decoder_raw(logits, seq, beam_width=beam))
                     continue
@@ -356,7 +382,9 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
                        "buckets": len(buckets), "crops": n_crops, "beam_width": beam,
                        "parallelism": f"replicas x{world} (whole buckets per rank)",
                        "decode": "second stream, beside the next bucket's forward" if args.c5_pipeline
-                       else "in line"}}, elapsed, n_crops
+                       else "in line",
+                       "execution": "hipGraph replay of each bucket's forward (infer.InferGraph)"
+                       if args.c5_mode == "graph" else "eager launches"}}, elapsed, n_crops
 
 
 def _free_port():
@@ -475,6 +503,12 @@ def main():
     ap.add_argument("--roofline", default="conv", choices=sorted(ROOFLINE_OPS))
     ap.add_argument("--roofline-also", default="dw",
                     help="comma-separated further roofline kinds reported in roofline_also (same timed steps)")
+    ap.add_argument("--c5-mode", default="eager", choices=["graph", "eager"],
+                    help="C5: each bucket's INFER forward launched eagerly (default) or replayed as a captured "
+                         "HIP graph (measured slower: 22.5k vs 32.3k crops/s, profiles/r4_ab3.txt)")
+    ap.add_argument("--c2-mode", default="graph", choices=["graph", "eager"],
+                    help="C2: the INFER forward + loss + greedy decode replayed as one captured HIP graph "
+                         "per batch (default), or launched eagerly")
     ap.add_argument("--mode", default="eager", choices=["graph", "eager"],
                     help="graph: forward+backward captured once as a HIP graph and replayed per step "
                          "(all-reduce + Adam eager); eager: every launch issued from Python each step")

@@ -722,6 +722,229 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
     bias_partials<4>(bpart, bsum, reinterpret_cast<float*>(sA), (bs * 2 + dir) * G4, H, u0);
 }
 
+// ------------------------------------------ backward, 16-row / 64-unit members
+// The gather BPTT above stages, per member and step, the group's dz rows of its
+// 32 batch rows: 32 x 4H bf16 = 128 KB per CU per step at H = 512 -- the step's
+// floor (~100 GB/s per CU from L2 into LDS, MI355X_MICROARCH.md handoff-payload).
+// That volume is rows x 4H whatever the unit slice, so here a member owns 16
+// batch rows and 64 hidden units (groups = 2 x B/16 of 8 members: the same B
+// workgroups, one per CU at B = 256) and stages 64 KB. 8 waves: wave w takes
+// gate q = w >> 1, k-half kh = w & 1 (256 of the gate's 512 columns): its W_h
+// slice [64 units][256 k] is resident (4 N-tiles x 8 k-steps = 128 VGPRs), it
+// stages ITS 16 dz rows x 256 columns (8 KB, 8 LDS-DMA wave instructions of two
+// 512-B rows, unpadded, 16-B pieces XOR-swizzled by row on the global side so a
+// fragment read of 16 rows hits 16 distinct bank groups) and multiplies them
+// wave-locally (32 MFMAs); the eight K-slice partials meet in LDS in a fixed
+// order. Cell: 2 units of one row per thread. Hand-off form, census, counting
+// flags, late epilogue loads and bias partials as the gather kernel.
+constexpr int R16_ROWS = 16, R16_UNITS = 64;
+
+__global__ void __launch_bounds__(512, 1)
+lstm_bwd_r16_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len, int T,
+                    int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
+                    const bf16* __restrict__ acts_t, bf16* __restrict__ dG_t, unsigned* __restrict__ flags,
+                    unsigned* __restrict__ err, unsigned spin_limit, float* __restrict__ bpart) {
+    constexpr int H = 512, G4 = 4 * H;
+    constexpr int RB = R16_ROWS, UM = R16_UNITS;
+    constexpr int NU = H / UM;                          // members per group (8)
+    constexpr int KW = 256;                             // k columns per wave
+    constexpr int KSW = KW / 32;                        // k-steps per wave (8)
+    constexpr int LDP = UM + 4;                         // partial row pitch (floats)
+    __shared__ __attribute__((aligned(16))) unsigned short sA[8 * RB * KW];   // [wave][row][swizzled 16-B slots]
+    __shared__ __attribute__((aligned(16))) float sP[8 * RB * LDP];           // [wave][row][unit]
+
+    int group, member;
+    persistent_role(2 * (B / RB), NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * UM, b0 = bs * RB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const int kbase = (w >> 1) * H + (w & 1) * KW;      // this wave's dz / W_h columns
+    gu32* gflags = (gu32*)(flags) + group * NU;
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
+
+    // resident B fragments: N-tile j = units u0 + 16 j + c; k = kbase + 32 ks + 8 g
+    bf16x8 bw[4][KSW];
+    const bf16* wdir = wh + (size_t)dir * H * G4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bf16* row = wdir + (size_t)(u0 + 16 * j + c) * G4 + kbase + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KSW; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KSW; ++ks) asm volatile("" ::"v"(bw[j][ks]));   // settled before the loop
+
+    // the cell item: row er, units eu, eu + 1 (all 4 gates)
+    const int er = tid >> 5, eu = 2 * (tid & 31);
+    const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));
+    float dcs[2] = {0.f, 0.f};
+    float bsum[4][2] = {};
+    const int64_t zx_elems = (int64_t)2 * 2 * B * G4;
+    auto zx_rsrc = __builtin_amdgcn_make_buffer_rsrc(dzx, 0, (int)(zx_elems * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t act_rsrc = uniform_rsrc(acts_t, (int64_t)T * B * 2 * G4 * 2);
+    const __amdgpu_buffer_rsrc_t cp_rsrc = uniform_rsrc(cprev_t, (int64_t)T * B * 2 * H * 4);
+    const __amdgpu_buffer_rsrc_t do_rsrc = uniform_rsrc(dout, (int64_t)T * B * 2 * H * 2);
+    // DMA lane geometry (fixed over the steps): instruction d covers rows 2d, 2d + 1;
+    // lane l writes row 2d + (l >> 5), slot l & 31, fetching the global 16-B piece
+    // (l & 31) ^ row of that row's wave columns
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    unsigned short* sa = sA + wu * RB * KW;
+    unsigned dma_off[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const int r = 2 * d + (lane >> 5);
+        dma_off[d] = (unsigned)((r * G4 + kbase + 8 * ((lane & 31) ^ (r & 15))) * 2);
+    }
+
+    for (int i = 0; i < T; ++i) {
+        const int s = T - 1 - i;
+        const bool valid = s < elen;
+        const int t = step_time(dir, s, elen);
+        const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        unsigned la[4], ldo;
+        u32x2 lcp;
+        auto load_late = [&]() {                        // 6 buffer loads
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                la[k] = __builtin_amdgcn_raw_buffer_load_b32(act_rsrc, (int)((tb * G4 + k * H + u0 + eu) * 2), 0, 0);
+            lcp = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(cp_rsrc, (int)((tb * H + u0 + eu) * 4), 0, 0));
+            ldo = __builtin_amdgcn_raw_buffer_load_b32(
+                do_rsrc, (int)((((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu) * 2), 0, 0);
+        };
+        floatx4 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (i > 0) {
+            // 1. wait until every member of the group published dz_{i-1} (flag >= i)
+            if (w == 0) {
+                unsigned spins = 0;
+                while (true) {
+                    unsigned f = base + (unsigned)i;
+                    if (lane < NU) f = poll_word(gflags + lane, local);
+                    if (__all(reached(f, base + (unsigned)i))) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            // 2. this wave's 16 rows x 256 columns of dz_{i-1}, wave-local (8 LDS-DMA)
+            const unsigned rb = (unsigned)(((int64_t)(((i - 1) & 1) * 2 + dir) * B + b0) * G4 * 2);
+            if (local) {
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        zx_rsrc, (__attribute__((address_space(3))) void*)(sa + d * 2 * KW), 16, rb + dma_off[d], 0, 0, 2);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        zx_rsrc, (__attribute__((address_space(3))) void*)(sa + d * 2 * KW), 16, rb + dma_off[d], 0, 0, 16);
+            }
+            asm volatile("" ::: "memory");
+            load_late();                                 // 6 loads behind the 8 DMAs
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            // 3. dh partial of this wave's K slice: [16 rows] x [64 units]
+#pragma unroll
+            for (int ks = 0; ks < KSW; ++ks) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(&sa[c * KW + 8 * ((4 * ks + g) ^ c)]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][ks], acc[j], 0, 0, 0);
+            }
+        } else {
+            load_late();
+        }
+        // 4. the eight partials meet in LDS: lane (c, g) holds rows 4 g + r of units 16 j + c
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sP[(w * RB + 4 * g + r) * LDP + 16 * j + c] = acc[j][r];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the epilogue operands landed
+        __syncthreads();
+        float pa[4][2], pcp[2], pdo[2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pa[k][0] = __uint_as_float(la[k] << 16);
+            pa[k][1] = __uint_as_float(la[k] & 0xffff0000u);
+        }
+        pcp[0] = __uint_as_float(lcp[0]);
+        pcp[1] = __uint_as_float(lcp[1]);
+        pdo[0] = __uint_as_float(ldo << 16);
+        pdo[1] = __uint_as_float(ldo & 0xffff0000u);
+
+        // 5. the cell's gradient for (row er, units eu, eu + 1)
+        float dz[4][2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float p[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) p[q] = sP[(q * RB + er) * LDP + eu + e];
+            const float dh = (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) + pdo[e];
+            const float ai = pa[0][e], aj = pa[1][e], af = pa[2][e], ao = pa[3][e];
+            const float cp = pcp[e];
+            const float cc = af * cp + ai * aj;
+            const float tc = tanh_fast(cc);
+            const float dc = dcs[e] + dh * ao * (1.f - tc * tc);
+            dz[3][e] = valid ? dh * tc * ao * (1.f - ao) : 0.f;
+            dz[0][e] = valid ? dc * aj * ai * (1.f - ai) : 0.f;
+            dz[1][e] = valid ? dc * ai * (1.f - aj * aj) : 0.f;
+            dz[2][e] = valid ? dc * cp * af * (1.f - af) : 0.f;
+            dcs[e] = valid ? dc * af : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bsum[k][0] += dz[k][0];
+            bsum[k][1] += dz[k][1];
+        }
+        // 6. publish dz (4-B stores, one per gate), drain, barrier, one lane raises the flag
+        unsigned zv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) zv[k] = (unsigned)bf16_bits(dz[k][0]) | ((unsigned)bf16_bits(dz[k][1]) << 16);
+        {
+            const int64_t zbase = ((int64_t)((i & 1) * 2 + dir) * B + b0 + er) * G4 + u0 + eu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                gu32* pz = (gu32*)(dzx + zbase + k * H);
+                if (local) *pz = zv[k];
+                else __hip_atomic_store(pz, zv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) raise_flag(gflags + member, base + (unsigned)(i + 1), local);
+        // 7. time-order copy for the weight-gradient GEMMs (drains behind the next step)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) *reinterpret_cast<unsigned*>(dG_t + tb * G4 + k * H + u0 + eu) = zv[k];
+    }
+    // bias partials of this 16-row slice: the 16 rows of every (gate, unit) meet in LDS
+    if (bpart) {
+        __syncthreads();
+        float* red = sP;                                 // [row][4 gates x 64 units], free after the loop
+        constexpr int LDR = 4 * UM + 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            red[er * LDR + k * UM + eu] = bsum[k][0];
+            red[er * LDR + k * UM + eu + 1] = bsum[k][1];
+        }
+        __syncthreads();
+        if (tid < 4 * UM) {
+            float sum = 0.f;
+            for (int r = 0; r < RB; ++r) sum += red[r * LDR + tid];
+            bpart[(int64_t)(bs * 2 + dir) * G4 + (tid / UM) * H + u0 + (tid % UM)] = sum;
+        }
+    }
+}
+
 // ---------------------------------------------------- backward, K-split form
 // The same BPTT with the recurrent product split over the members by K
 // instead of by output unit (opt-in, OCRK_LSTM_BWD_KSPLIT=1; the default is the
@@ -1092,7 +1315,25 @@ extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
     return counters + (ksplit > gather ? ksplit : gather);
 }
 
+// the 16-row / 64-unit BPTT (H = 512): default where its grid (B workgroups) is co-resident;
+// OCRK_LSTM_BWD_R16=0 keeps the 32-row gather kernel (read per call: A/B and tests)
+static bool lstm_bwd_r16(int B, int H) {
+    const char* e = getenv("OCRK_LSTM_BWD_R16");
+    if ((e && e[0] == '0') || H != 512 || B % PBR || lstm_bwd_ksplit()) return false;   // flag words as the gather form
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_r16_kernel, 512, 0) != hipSuccess) return false;
+    return 2L * (B / R16_ROWS) * (H / R16_UNITS) <= (long)cus * per_cu;
+}
+
+extern "C" int ocrk_lstm_bwd_persistent_slices(int B, int H) {
+    if (lstm_bwd_r16(B, H)) return B / R16_ROWS;
+    return B % PBR == 0 ? B / PBR : 0;
+}
+
 extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
+    if (lstm_bwd_r16(B, H)) return 1;
     if (B % PBR || H % PHU || !(H == 256 || H == 512)) return 0;
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -1118,6 +1359,13 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     bf16* zx = (bf16*)((char*)ws + counters);
     if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
         return ocrk::launch_status("ocrk_lstm_bwd_persistent memset");
+    if (lstm_bwd_r16(B, H)) {
+        // counters: 2 (B/16) x 8 members = the same count as 2 (B/32) x 16
+        lstm_bwd_r16_kernel<<<2u * (unsigned)(B / R16_ROWS) * (unsigned)(H / R16_UNITS), 512, 0, st>>>(
+            (const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t, (const bf16*)acts_t, (bf16*)dG_t, cnt, err,
+            lstm_spin_limit(), dbias_part);
+        return ocrk::launch_status("ocrk_lstm_bwd_persistent");
+    }
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (lstm_bwd_ksplit()) {
         const char* pe = getenv("OCRK_LSTM_BWD_PB16");            // partial products exchanged in bf16

@@ -464,12 +464,13 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None, defer=None):
     if lstm_persistent_ok(B, H, dtype):
         nb = _lib.lib().ocrk_lstm_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)
-        part = torch.empty(B // 32, 2 * 4 * H, dtype=torch.float32, device=dev) if dbias is not None else None
+        slices = _lib.lib().ocrk_lstm_bwd_persistent_slices(B, H)     # B/16 (16-row members) or B/32
+        part = torch.empty(slices, 2 * 4 * H, dtype=torch.float32, device=dev) if dbias is not None else None
         call("ocrk_lstm_bwd_persistent", ptr(wh), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev), ptr(acts), ptr(dG),
              ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd", B, H, dev)), ptr(part), ptr(ws), nb,
              _stream(dout))
         if dbias is not None:
-            _bias_parts(part, B // 32, 2 * 4 * H, dbias, defer)
+            _bias_parts(part, slices, 2 * 4 * H, dbias, defer)
         return dG
     dg_state = torch.zeros(2, 2, B, 4 * H, dtype=dtype, device=dev)
     dc_state = torch.zeros(2, B, H, dtype=torch.float32, device=dev)

@@ -103,7 +103,8 @@ class Recognizer:
     0.022 beam-16 there -- bench.py's cer_vs_ref). A bf16 store is refused
     unless allow_bf16=True states that approximate strings are acceptable."""
 
-    def __init__(self, store, decoder="greedy", beam_width=16, merge_repeated=True, allow_bf16=False):
+    def __init__(self, store, decoder="greedy", beam_width=16, merge_repeated=True, allow_bf16=False,
+                 graphs=False):
         if decoder not in ("greedy", "beam"):
             raise ValueError("decoder is 'greedy' or 'beam'")
         if store.cfg.dtype != torch.float32 and not allow_bf16:
@@ -113,10 +114,31 @@ class Recognizer:
         self.decoder = decoder
         self.beam_width = beam_width
         self.merge_repeated = merge_repeated
+        self.graphs = {} if graphs else None      # (bs, W) -> infer.InferGraph
+
+    def _graphed(self, batch, widths):
+        key = tuple(batch.shape)
+        g = self.graphs.get(key)
+        if g is None or g.version != self.store.version:
+            from .infer import InferGraph
+            g = self.graphs[key] = InferGraph(self.store, batch=key[0], width=key[2],
+                                              decoder="greedy" if self.decoder == "greedy" else None,
+                                              merge_repeated=self.merge_repeated)
+        return g.run(torch.from_numpy(np.ascontiguousarray(batch, dtype=np.uint8)),
+                     torch.from_numpy(np.asarray(widths, np.int32)))
 
     def labels(self, batch, widths):
-        """Dense int64 [bs, max_len] (-1 padded) device tensor."""
+        """Dense int64 [bs, max_len] (-1 padded) device tensor. graphs=True: the
+        forward of each (bs, W) bucket shape is captured once (infer.InferGraph)
+        and replayed per batch."""
         dev = self.store.device
+        if self.graphs is not None:
+            g = self._graphed(batch, widths)
+            if self.decoder == "greedy":
+                width = int(g.decoded_len.max().item()) if g.decoded_len.numel() else 0
+                return g.decoded[:, :width].clone()
+            out, _ = decode.ctc_beam_search_decoder(g.logits, g.seq_len, self.beam_width, 1, self.merge_repeated)
+            return out[0]
         with torch.no_grad():
             image = torch.from_numpy(np.ascontiguousarray(batch, dtype=np.uint8)).to(dev, non_blocking=True)
             width = torch.from_numpy(np.asarray(widths, np.int32)).to(dev, non_blocking=True)

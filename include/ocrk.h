@@ -276,6 +276,10 @@ int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, const int* s
                                  float* out, float* hprev_t, float* cprev_t, float* acts_t, unsigned* err,
                                  unsigned* flags, void* ws, size_t ws_bytes, void* stream);
 int ocrk_lstm_bwd_persistent_supported(int B, int H);
+/* Rows of dbias_part the BPTT launch writes: B/16 when it runs the 16-row / 64-unit
+ * member form (H = 512, its B-workgroup grid co-resident; 64 KB of dz gathered per CU
+ * per step instead of 128 KB), else B/32. */
+int ocrk_lstm_bwd_persistent_slices(int B, int H);
 size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int T, int B, int H, const void* dout,
                              const float* cprev_t, const void* acts_t, void* dG_t, unsigned* err,
@@ -317,11 +321,12 @@ size_t ocrk_gru_bwd_persistent_workspace_size(int B, int H);
 int ocrk_gru_bwd_persistent(const void* whg, const void* whc, const int* seq_len, int T, int B, int H,
                             const void* dout, const void* hprev_t, const void* acts_t, void* dG_t, unsigned* err,
                             unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream);
-/* dbias_part (the two BPTT entry points; NULL = skipped): f32 [B/32][2][G] with
- * G = 4H (LSTM) / 3H (GRU): per 32-row batch slice and direction, the sum of the
+/* dbias_part (the two BPTT entry points; NULL = skipped): f32 [S][2][G] with
+ * S = ocrk_lstm_bwd_persistent_slices(B, H) for the LSTM (B/16 or B/32), B/32 for the GRU,
+ * G = 4H (LSTM) / 3H (GRU): per batch slice and direction, the sum of the
  * gate gradients dG_t over its rows and steps -- the layer's bias gradient
  * (model_bu.py:173-180 / model.py:170-180, tf.gradients of the [x,h].W + b
- * sums) fused into the loop; the caller sums the B/32 rows (ocrk_slab_sum)
+ * sums) fused into the loop; the caller sums the S rows (ocrk_slab_sum)
  * instead of reading dG_t again. */
 /* Hand-off words of the persistent loops (the `flags` argument of the four
  * *_persistent entry points above): NULL = they live in the workspace and are

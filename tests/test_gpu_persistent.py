@@ -64,6 +64,25 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
     scale = dstep.float().abs().max().item()
     assert (dstep.float() - dpers.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
     # gate gradients against the oracle's BPTT (dz = dL/d[i,j,f,o] pre-activations)
+    dz_ref = _bptt_ref(caches, ks, dout_np, T, B, H, n_in)
+    got = dpers.float().cpu().numpy()
+    assert np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
+    # the K-split form of the persistent BPTT (OCRK_LSTM_BWD_KSPLIT=1, opt-in) against
+    # the gather default: same bounds against the oracle and the per-step kernels
+    monkeypatch.setenv("OCRK_LSTM_BWD_KSPLIT", "1")
+    dgat = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("OCRK_LSTM_BWD_KSPLIT")
+    assert K.lstm_error_word(cuda).item() == 0
+    assert (dstep.float() - dgat.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
+    gg = dgat.float().cpu().numpy()
+    assert np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
+    print(f"dz rel err vs oracle: gather {np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref):.3e} "
+          f"K-split {np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref):.3e}")
+
+
+def _bptt_ref(caches, ks, dout_np, T, B, H, n_in):
+    """The oracle's BPTT gate gradients dz [T, B, 2, 4H] (ref_graph.lstm_dir_fwd caches)."""
     dz_ref = np.zeros((T, B, 2, 4 * H), np.float32)
     for d in range(2):
         dh = np.zeros((B, H), np.float32)
@@ -80,20 +99,67 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
             dz_ref[t_idx, rows, d] = np.where(v, dz, dz_ref[t_idx, rows, d])
             dh = np.where(v, dz @ ks[d][n_in:].T, dh)
             dc = np.where(v, dct * sf, dc)
-    got = dpers.float().cpu().numpy()
-    assert np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
-    # the K-split form of the persistent BPTT (OCRK_LSTM_BWD_KSPLIT=1, opt-in) against
-    # the gather default: same bounds against the oracle and the per-step kernels
-    monkeypatch.setenv("OCRK_LSTM_BWD_KSPLIT", "1")
-    dgat = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H)
+    return dz_ref
+
+
+@pytest.mark.parametrize("T,B,n_in", [(9, 96, 32), (13, 64, 32), (17, 256, 64)])
+def test_bptt_16row_members_match_gather_and_oracle(cuda, monkeypatch, T, B, n_in):
+    """The 16-row / 64-unit BPTT (default at H=512 when co-resident) against the
+    32-row gather form (OCRK_LSTM_BWD_R16=0) and the oracle, with the fused bias
+    partials (B/16 slices) against the column sums of its own dG. B=96 takes the
+    linear workgroup map (grid/8 not a multiple of 8 members), 64 and 256 the
+    XCD-grouped one."""
+    from cnn_lstm_ctc_ocr_amd import _lib
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    H = 512
+    rng = np.random.default_rng(101 + B)
+    bf = lambda a: torch.from_numpy(a.astype(np.float32)).bfloat16().float().numpy()   # noqa: E731
+    x = bf(rng.standard_normal((T, B, n_in)))
+    ks = [bf(rng.standard_normal((n_in + H, 4 * H)) * 0.2) for _ in range(2)]
+    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
+    seq = rng.integers(1, T + 1, B).astype(np.int32)
+    seq[:4] = [T, 1, T - 1, 2]
+    caches = [G.lstm_dir_fwd(x, seq, ks[d], bs[d], d == 1)[1] for d in range(2)]
+    whT = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))).to(cuda).bfloat16()
+    wh = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:] for k in ks]))).to(cuda).bfloat16()
+    wxT = np.ascontiguousarray(np.concatenate([k[:n_in].T for k in ks], 0))
+    gx = K.gemm(torch.from_numpy(x.reshape(T * B, n_in)).to(cuda).bfloat16(),
+                torch.from_numpy(wxT).to(cuda).bfloat16(), trans_b=True,
+                bias=torch.from_numpy(np.concatenate(bs)).to(cuda), out_dtype=torch.bfloat16)
+    seq_d = torch.from_numpy(seq).to(cuda)
+    K._PERSISTENT.clear()
+    assert K.lstm_persistent_ok(B, H, torch.bfloat16)
+    assert _lib.lib().ocrk_lstm_bwd_persistent_slices(B, H) == B // 16
+    K.lstm_error_word(cuda).zero_()
+    _, _, cprev, acts = K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.bfloat16)
+    dout_np = bf(rng.standard_normal((T, B, 2 * H)))
+    dout = torch.from_numpy(dout_np).to(cuda).bfloat16()
+    db16 = torch.zeros(2 * 4 * H, device=cuda)
+    d16 = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H, dbias=db16)
+    monkeypatch.setenv("OCRK_LSTM_BWD_R16", "0")
+    assert _lib.lib().ocrk_lstm_bwd_persistent_slices(B, H) == B // 32
+    db32 = torch.zeros(2 * 4 * H, device=cuda)
+    d32 = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H, dbias=db32)
     torch.cuda.synchronize()
-    monkeypatch.delenv("OCRK_LSTM_BWD_KSPLIT")
+    monkeypatch.delenv("OCRK_LSTM_BWD_R16")
     assert K.lstm_error_word(cuda).item() == 0
-    assert (dstep.float() - dgat.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
-    gg = dgat.float().cpu().numpy()
-    assert np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
-    print(f"dz rel err vs oracle: gather {np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref):.3e} "
-          f"K-split {np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref):.3e}")
+    scale = d32.float().abs().max().item()
+    assert (d16.float() - d32.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
+    dz_ref = _bptt_ref(caches, ks, dout_np, T, B, H, n_in)
+    for got in (d16, d32):
+        g = got.float().cpu().numpy()
+        assert np.linalg.norm(g - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
+    # invalid steps carry exact zeros (row 1 has one step)
+    assert torch.all(d16[1:, 1] == 0)
+    # fused bias partials (f32 sums of the f32 dz) against the column sums of the
+    # kernel's own bf16 dG (bf16 rounding, ~2^-9 per term, over T*B terms) and
+    # against the oracle's dz sums
+    rel = lambda a, b: (torch.linalg.norm(a - b) / torch.linalg.norm(b)).item()   # noqa: E731
+    ref_b = torch.from_numpy(dz_ref.sum(axis=(0, 1)).reshape(-1)).to(cuda)
+    for db, dg in ((db16, d16), (db32, d32)):
+        assert rel(db, dg.float().sum(dim=(0, 1)).reshape(-1)) < 5e-3
+        assert rel(db, ref_b) < 5e-2
+    print(f"bias rel err vs oracle: 16-row {rel(db16, ref_b):.3e} gather {rel(db32, ref_b):.3e}")
 
 
 def test_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
