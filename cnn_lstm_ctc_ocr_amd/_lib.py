@@ -26,6 +26,7 @@ BF16 = 1
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int
+_u32 = ctypes.c_uint
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
 _sz = ctypes.c_size_t
@@ -101,6 +102,7 @@ SIGNATURES = {
     "ocrk_gemm": [_i32, _i32, _i32, _i32, _i32, _f32, _p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64,
                   _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p],
     "ocrk_adam": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p],
+    "ocrk_adam_ex": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _u32, _p],
     "ocrk_cast": [_p, _i32, _p, _i32, _i64, _p],
     "ocrk_permute3": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p],
     "ocrk_strided_copy": [_p, _i64, _i64, _i64, _i64, _p, _i32, _i64, _i64, _p],

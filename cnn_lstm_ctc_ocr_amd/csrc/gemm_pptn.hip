@@ -300,7 +300,12 @@ bool gemm_pptn_enabled() {
 
 // Runs the ping-pong TN engine when it covers the call; -1 otherwise.
 bool gemm_pptn_covers(int amode, int M, int N, int convC) {
-    if (!gemm_pptn_enabled() || M < 256 || N < 256 || M % 8 != 0 || N % 8 != 0) return false;
+#ifdef OCRK_EXPERIMENTS
+    static const int nmin = [] { const char* e = getenv("OCRK_PPTN_NMIN"); return e ? atoi(e) : 256; }();
+#else
+    constexpr int nmin = 256;
+#endif
+    if (!gemm_pptn_enabled() || M < 256 || N < nmin || M % 8 != 0 || N % 8 != 0) return false;
     if (amode == A_COLK) return true;
     return amode == A_IM2COL_T && convC % 64 == 0;        // a 64-column A block = one tap's channels
 }

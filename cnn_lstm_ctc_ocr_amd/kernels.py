@@ -636,10 +636,11 @@ def mean(x):
     return out
 
 
-def adam_(p, g, m, v, lr_t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0):
+def adam_(p, g, m, v, lr_t, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0, zero_grad=False):
+    """zero_grad: g is cleared as it is read (OCRK_ADAM_ZERO_GRAD)."""
     _chk(p, g, m, v)
-    call("ocrk_adam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr_t), float(beta1), float(beta2),
-         float(eps), float(grad_scale), _stream(p))
+    call("ocrk_adam_ex", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr_t), float(beta1), float(beta2),
+         float(eps), float(grad_scale), 1 if zero_grad else 0, _stream(p))
 
 
 # ----------------------------------------------------------------------- CTC

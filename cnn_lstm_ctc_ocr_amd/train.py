@@ -14,6 +14,7 @@ loss is a batch mean (model.py:228). BatchNorm statistics stay per rank.
 """
 import collections
 import math
+import os
 import time
 
 import torch
@@ -23,6 +24,10 @@ from . import _lib
 from . import kernels as K
 from .config import TRAIN
 from .model import check_feasible_host, convnet_layers, ctc_loss_layer, dense_labels, host_labels, rnn_layers
+
+
+# OCRK_ADAM_ZERO=0: keep the separate zero-gradient fill (measurement toggle)
+_ADAM_ZERO = os.environ.get("OCRK_ADAM_ZERO", "1") != "0"
 
 
 class GradBuckets:
@@ -161,8 +166,10 @@ class Trainer:
         self.global_step = global_step
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
+        self._grads_zeroed = False                # flat_grad cleared by the last optimizer pass
         self._status_host = None
         self._status_ev = None
+        self._status_stream = None
         self._status_ring = collections.deque()     # data parallel: (event, pinned copy) per step
         self.status_lag = 2
         self.buckets = GradBuckets(store, process_group)
@@ -195,7 +202,11 @@ class Trainer:
         store = self.store
         if host_labels(label) and not (isinstance(width, torch.Tensor) and width.is_cuda):
             check_feasible_host(label, width)
-        store.zero_grad()
+        if self._grads_zeroed and not (store.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            store.join()             # the last optimizer pass left flat_grad zero (ocrk_adam_ex ZERO_GRAD)
+        else:
+            store.zero_grad()
+        self._grads_zeroed = False
         features, seq_len = convnet_layers(image, width, TRAIN, store)
         if self.overlap_allreduce and features.requires_grad and self.buckets.world() > 1 and \
                 not (features.is_cuda and torch.cuda.is_current_stream_capturing()):
@@ -218,8 +229,11 @@ class Trainer:
         t = self.global_step + 1
         lr = self.learning_rate()
         lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+        # the update clears the gradient as it reads it: the next loss_and_grads skips its fill
+        # (a 4-byte-per-parameter pass at the top of the step)
         K.adam_(store.flat, store.flat_grad, self.m, self.v, lr_t, self.beta1, self.beta2, self.eps,
-                grad_scale=grad_scale)
+                grad_scale=grad_scale, zero_grad=_ADAM_ZERO and store.device.type == "cuda")
+        self._grads_zeroed = _ADAM_ZERO and store.device.type == "cuda"
         store.bump()
         self.global_step += 1
 
@@ -280,9 +294,15 @@ class Trainer:
             return
         if self._status_host is None:
             self._status_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self._status_host.copy_(K.status_word(dev), non_blocking=True)
-        self._status_ev = torch.cuda.Event()
-        self._status_ev.record(torch.cuda.current_stream(dev))
+            self._status_stream = torch.cuda.Stream(dev)
+        # the copy waits for the step on its own stream: the next step's first kernels
+        # do not queue behind it on the main stream
+        cur = torch.cuda.current_stream(dev)
+        self._status_stream.wait_stream(cur)
+        with torch.cuda.stream(self._status_stream):
+            self._status_host.copy_(K.status_word(dev), non_blocking=True)
+            self._status_ev = torch.cuda.Event()
+            self._status_ev.record(self._status_stream)
 
     def poll_status(self):
         """Raise if an earlier step's queued status copy has landed and shows a bit

@@ -360,6 +360,12 @@ int ocrk_gemm(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
  * grad_scale (e.g. 1/world_size after a summing all-reduce). */
 int ocrk_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_t, float beta1,
               float beta2, float eps, float grad_scale, void* stream);
+/* The same update with flags: OCRK_ADAM_ZERO_GRAD clears g as it is read (the
+ * next step's zero-gradient pass folded into the optimizer's; Trainer uses it
+ * and skips its own fill). */
+#define OCRK_ADAM_ZERO_GRAD 1u
+int ocrk_adam_ex(float* p, float* g, float* m, float* v, int64_t n, float lr_t, float beta1,
+                 float beta2, float eps, float grad_scale, unsigned flags, void* stream);
 
 /* Batched weight images: ONE launch for a table of 2-D copies (device array of
  * `njobs` records of 8 x 8 bytes: {const float* src; void* dst; int64 rows, cols,
