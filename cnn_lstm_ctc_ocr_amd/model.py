@@ -70,8 +70,6 @@ class _ConvBlock(torch.autograd.Function):
         else:
             w_nk, _ = store.conv_images(odd, dt)
             y_odd = K.conv3x3_fwd(x, w_nk, P[f"convnet/{odd}/bias"], relu=True)
-        if k == 3:
-            store.prefetch_images()      # the other weight images beside the conv6-conv8 GEMMs
         B, H, W, _ = y_odd.shape
         M = B * H * W
         w_nk, _ = store.conv_images(even, dt)
@@ -122,7 +120,7 @@ class _ConvBlock(torch.autograd.Function):
             _issue(store, late)
             with _conv_side(store, y_odd, dz):             # overlaps the data-gradient GEMM below
                 K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
-        _, w_bwd = store.conv_images(even, dt, bwd=True)
+        _, w_bwd = store.conv_images(even, dt)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
                                     defer=late)
@@ -141,7 +139,7 @@ class _ConvBlock(torch.autograd.Function):
             with _conv_side(store, x, dy_odd):
                 K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
             if ctx.needs_input_grad[0]:
-                _, w_bwd_odd = store.conv_images(odd, dt, bwd=True)
+                _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
         return (dx, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
@@ -298,7 +296,7 @@ class _BiLSTM(torch.autograd.Function):
         dout = dout.contiguous()
         if dout.dtype != dt:
             dout = K.cast(dout, dt)
-        _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt, bwd=True)
+        _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
         # [T,B,2,4H]; the bias gradient (both directions) formed in the BPTT loop
         late = [] if _side_enabled("OCRK_SIDE_STREAM") else None
         dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer),
@@ -370,7 +368,7 @@ class _BiGRU(torch.autograd.Function):
         dout = dout.contiguous()
         if dout.dtype != dt:
             dout = K.cast(dout, dt)
-        _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt, bwd=True)
+        _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt)
         # [T,B,2,3H]; the [gates | candidate] bias gradients formed in the BPTT loop
         late = [] if _side_enabled("OCRK_SIDE_STREAM") else None
         dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=store.gru_bias_cat_grad(layer),

@@ -112,11 +112,6 @@ def reference_init(cfg, seed=0):
     return vals
 
 
-# OCRK_IMG_SPLIT=0: refresh every weight image on the current stream at the
-# first request (measurement toggle for the side-stream refresh)
-_IMG_SPLIT = os.environ.get("OCRK_IMG_SPLIT", "1") != "0"
-
-
 class ParamStore:
     def __init__(self, cfg=None, device="cuda", seed=0, values=None):
         self.cfg = cfg or ModelConfig()
@@ -193,86 +188,24 @@ class ParamStore:
         self.version += 1
         self._images.clear()
         self._plan_fresh = False
-        self._side_issued = False
-        self._img_events = {}
 
     # ---------------------------------------------------- weight images
-    def images(self, key, builder, table="rnn"):
+    def images(self, key, builder):
         """Compute-dtype weight layouts, rebuilt once per parameter version. The
-        model's images in its compute dtype are stable buffers refreshed by three
-        batched launches (ocrk_copy_batch, job tables built once) at the first
-        request of a version: `conv` (the conv forward images) on the current
-        stream, `rnn` (recurrent and logits forward images) and `bwd` (every
-        backward image) on the store's image stream beside the conv forward --
-        a request for a `rnn` / `bwd` image makes the current stream wait for
-        that launch (their events also join `pending`, so the optimizer never
-        overwrites the master values under them). Other keys fall back to
-        `builder`."""
+        model's images in its compute dtype are stable buffers refreshed together
+        by ONE batched launch (ocrk_copy_batch, the job table built once);
+        other keys fall back to `builder`."""
         plan = self._plan_for(key)
         if plan is not None:
-            self._refresh(plan, table)
+            if not self._plan_fresh:
+                K.copy_batch(plan["table"], plan["njobs"], plan["tiles"], self.flat)
+                self._plan_fresh = True
             return plan["images"][key]
         img = self._images.get(key)
         if img is None:
             img = builder()
             self._images[key] = img
         return img
-
-    def _refresh(self, plan, table):
-        cur = torch.cuda.current_stream(self.device)
-        if not self._plan_fresh:
-            conv = plan["tables"]["conv"]
-            if conv[1]:
-                K.copy_batch(*conv, self.flat)
-            self._plan_fresh = True
-            self._side_issued = False
-        if table == "conv":
-            return
-        if not _IMG_SPLIT:                   # measurement toggle: every table on the current stream
-            if not self._side_issued:
-                for name in ("rnn", "bwd"):
-                    if plan["tables"][name][1]:
-                        K.copy_batch(*plan["tables"][name], self.flat)
-                self._side_issued = True
-            return
-        self._issue_side(plan)
-        ev = self._img_events.pop(table, None)
-        if ev is not None:
-            cur.wait_event(ev)
-
-    def _issue_side(self, plan):
-        """The `rnn` and `bwd` tables on the image stream, behind everything the
-        current stream has issued (once per parameter version)."""
-        if self._side_issued:
-            return
-        cur = torch.cuda.current_stream(self.device)
-        side = getattr(self, "_img_stream", None)
-        if side is None:
-            side = self._img_stream = torch.cuda.Stream(device=self.device)
-        side.wait_stream(cur)
-        self._img_events = {}
-        with torch.cuda.stream(side):
-            for name in ("rnn", "bwd"):
-                tab = plan["tables"][name]
-                if not tab[1]:
-                    continue
-                K.copy_batch(*tab, self.flat)
-                ev = torch.cuda.Event()
-                ev.record(side)
-                self._img_events[name] = ev
-                self.pending.append(ev)
-        self._side_issued = True
-
-    def prefetch_images(self):
-        """Start the recurrent / backward image refresh now (model.convnet_layers
-        calls this in front of the MFMA-bound conv6-conv8 GEMMs, where the copy's
-        HBM traffic costs least; a request before it starts it instead)."""
-        plan = getattr(self, "_plan", None)
-        if plan is None or self.device.type != "cuda" or not _IMG_SPLIT:
-            return
-        if not self._plan_fresh:
-            self._refresh(plan, "conv")
-        self._issue_side(plan)
 
     def _plan_for(self, key):
         if self.device.type != "cuda" or os.environ.get("OCRK_BATCHED_IMAGES", "1") == "0":
@@ -292,20 +225,20 @@ class ParamStore:
         dev = self.device
         esz = torch.empty(0, dtype=dtype).element_size()
         code = K.dtype_code(dtype)
-        jobs, images = {"conv": [], "rnn": [], "bwd": []}, {}
+        jobs, images = [], {}
 
-        def job(src, s_off, rows, cols, in_rs, dst, d_off, out_rs, transpose, table):
-            jobs[table].append([src.data_ptr() + 4 * s_off, dst.data_ptr() + esz * d_off, rows, cols, in_rs, out_rs,
-                                0, int(transpose) | (code << 32)])
+        def job(src, s_off, rows, cols, in_rs, dst, d_off, out_rs, transpose):
+            jobs.append([src.data_ptr() + 4 * s_off, dst.data_ptr() + esz * d_off, rows, cols, in_rs, out_rs, 0,
+                         int(transpose) | (code << 32)])
 
         for li in range(2, 9):
             w = self.params[f"convnet/conv{li}/kernel"]                      # [3][3][Cin][Cout]
             kh, kw, cin, cout = w.shape
             w_nk = torch.empty(cout, kh * kw * cin, dtype=dtype, device=dev)
             w_bwd = torch.empty(cin, kh * kw * cout, dtype=dtype, device=dev)
-            job(w, 0, kh * kw * cin, cout, cout, w_nk, 0, kh * kw * cin, True, "conv")
+            job(w, 0, kh * kw * cin, cout, cout, w_nk, 0, kh * kw * cin, True)
             for t in range(kh * kw):
-                job(w, t * cin * cout, cin, cout, cout, w_bwd, t * cout, kh * kw * cout, False, "bwd")
+                job(w, t * cin * cout, cin, cout, cout, w_bwd, t * cout, kh * kw * cout, False)
             images[("conv", f"conv{li}", dtype)] = (w_nk, w_bwd)
         for layer in range(1, len(self.cfg.rnn_sizes) + 1):
             pre = f"rnn/bdrnn{layer}"
@@ -320,10 +253,10 @@ class ParamStore:
                 wh = torch.empty(2, H, G, dtype=dtype, device=dev)
                 for d, dn in enumerate(("fw", "bw")):
                     k = self.params[f"{pre}/{dn}/lstm_cell/kernel"]
-                    job(k, 0, n_in, G, G, wxT, d * G * n_in, n_in, True, "rnn")
-                    job(k, 0, n_in, G, G, wx, d * G, 2 * G, False, "bwd")
-                    job(k, n_in * G, H, G, G, whT, d * G * H, H, True, "rnn")
-                    job(k, n_in * G, H, G, G, wh, d * H * G, G, False, "bwd")
+                    job(k, 0, n_in, G, G, wxT, d * G * n_in, n_in, True)
+                    job(k, 0, n_in, G, G, wx, d * G, 2 * G, False)
+                    job(k, n_in * G, H, G, G, whT, d * G * H, H, True)
+                    job(k, n_in * G, H, G, G, wh, d * H * G, G, False)
                 images[("lstm", layer, dtype)] = (wxT, wx, whT, wh, self.flat_bias_pair(layer))
             else:
                 gk = self.params[f"{pre}/fw/gru_cell/gates/kernel"]
@@ -340,44 +273,40 @@ class ParamStore:
                 for d, dn in enumerate(("fw", "bw")):
                     g = self.params[f"{pre}/{dn}/gru_cell/gates/kernel"]
                     c = self.params[f"{pre}/{dn}/gru_cell/candidate/kernel"]
-                    job(g, 0, n_in, G2, G2, wxT, d * G3 * n_in, n_in, True, "rnn")
-                    job(c, 0, n_in, H, H, wxT, (d * G3 + G2) * n_in, n_in, True, "rnn")
-                    job(g, 0, n_in, G2, G2, wx, d * G3, 2 * G3, False, "bwd")
-                    job(c, 0, n_in, H, H, wx, d * G3 + G2, 2 * G3, False, "bwd")
-                    job(g, n_in * G2, H, G2, G2, whgT, d * G2 * H, H, True, "rnn")
-                    job(c, n_in * H, H, H, H, whcT, d * H * H, H, True, "rnn")
-                    job(g, n_in * G2, H, G2, G2, whg, d * H * G2, G2, False, "bwd")
-                    job(c, n_in * H, H, H, H, whc, d * H * H, H, False, "bwd")
+                    job(g, 0, n_in, G2, G2, wxT, d * G3 * n_in, n_in, True)
+                    job(c, 0, n_in, H, H, wxT, (d * G3 + G2) * n_in, n_in, True)
+                    job(g, 0, n_in, G2, G2, wx, d * G3, 2 * G3, False)
+                    job(c, 0, n_in, H, H, wx, d * G3 + G2, 2 * G3, False)
+                    job(g, n_in * G2, H, G2, G2, whgT, d * G2 * H, H, True)
+                    job(c, n_in * H, H, H, H, whcT, d * H * H, H, True)
+                    job(g, n_in * G2, H, G2, G2, whg, d * H * G2, G2, False)
+                    job(c, n_in * H, H, H, H, whc, d * H * H, H, False)
                 images[("gru", layer, dtype)] = (wxT, wx, whgT, whcT, whg, whc, self.gru_bias_cat(layer))
         lk = self.params["rnn/logits/kernel"]                               # [D][C]
         limg = torch.empty(lk.shape, dtype=dtype, device=dev)
         limgT = torch.empty(lk.shape[1], lk.shape[0], dtype=dtype, device=dev)
-        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limg, 0, lk.shape[1], False, "bwd")
-        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limgT, 0, lk.shape[0], True, "rnn")
+        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limg, 0, lk.shape[1], False)
+        job(lk, 0, lk.shape[0], lk.shape[1], lk.shape[1], limgT, 0, lk.shape[0], True)
         images[("logits", dtype)] = limg
         images[("logitsT", dtype)] = limgT
-        tables = {}
-        for name, js in jobs.items():
-            tiles = 0
-            for j in js:
-                j[6] = tiles
-                tiles += -(-j[2] // 32) * -(-j[3] // 32)
-            table = torch.tensor(js, dtype=torch.int64).to(dev) if js else None
-            tables[name] = (table, len(js), tiles)
-        return {"tables": tables, "images": images}
+        tiles = 0
+        for j in jobs:
+            j[6] = tiles
+            tiles += -(-j[2] // 32) * -(-j[3] // 32)
+        table = torch.tensor(jobs, dtype=torch.int64).to(dev)
+        return {"table": table, "njobs": len(jobs), "tiles": tiles, "images": images}
 
-    def conv_images(self, name, dtype, bwd=False):
-        """conv2..8: w_nk [Cout][3][3][Cin] (forward), w_bwd [Cin][3][3][Cout]
-        (bwd=True: a backward request, which waits for the backward images)."""
+    def conv_images(self, name, dtype):
+        """conv2..8: w_nk [Cout][3][3][Cin] (forward), w_bwd [Cin][3][3][Cout]."""
         def build():
             w = self.params[f"convnet/{name}/kernel"]
             kh, kw, cin, cout = w.shape
             w_nk = K.permute3(w, kh * kw * cin, cout, 1, dtype).view(cout, kh * kw * cin)
             w_bwd = K.permute3(w, kh * kw, cin, cout, dtype).view(cin, kh * kw * cout)
             return w_nk, w_bwd
-        return self.images(("conv", name, dtype), build, "bwd" if bwd else "conv")
+        return self.images(("conv", name, dtype), build)
 
-    def lstm_images(self, layer, dtype, bwd=False):
+    def lstm_images(self, layer, dtype):
         """Recurrent layer `layer` (1-based): WxT_cat [8H][In], Wx_cat [In][8H],
         whT [2][4H][H], wh [2][H][4H] in dtype, bias_cat f32 [8H]."""
         def build():
@@ -399,7 +328,7 @@ class ParamStore:
                 K.strided_copy(k, H, G, G, 1, wh, G, 1, out_offset=d * H * G, in_offset=n_in * G)
             bias = self.flat_bias_pair(layer)
             return wxT, wx, whT, wh, bias
-        return self.images(("lstm", layer, dtype), build, "bwd" if bwd else "rnn")
+        return self.images(("lstm", layer, dtype), build)
 
     def flat_bias_pair(self, layer):
         """[8H] view over the adjacent fw/bw LSTM biases of `layer`."""
@@ -418,7 +347,7 @@ class ParamStore:
         n = self.params[f"{pre}/fw/lstm_cell/bias"].numel()
         return self.flat_grad[off:off + 2 * n]
 
-    def gru_images(self, layer, dtype, bwd=False):
+    def gru_images(self, layer, dtype):
         """GRU layer `layer`: WxT_cat [6H][In] and Wx_cat [In][6H] (per direction
         columns r|u|c), whgT [2][2H][H], whcT [2][H][H] (forward), whg [2][H][2H],
         whc [2][H][H] (backward), all in dtype; bias_cat f32 [6H] (a flat view)."""
@@ -448,7 +377,7 @@ class ParamStore:
                 K.strided_copy(g, H, G2, G2, 1, whg, G2, 1, out_offset=d * H * G2, in_offset=n_in * G2)
                 K.strided_copy(c, H, H, H, 1, whc, H, 1, out_offset=d * H * H, in_offset=n_in * H)
             return wxT, wx, whgT, whcT, whg, whc, self.gru_bias_cat(layer)
-        return self.images(("gru", layer, dtype), build, "bwd" if bwd else "rnn")
+        return self.images(("gru", layer, dtype), build)
 
     def _gru_bias_span(self, layer):
         pre = f"rnn/bdrnn{layer}"
@@ -473,7 +402,7 @@ class ParamStore:
     def logits_image(self, dtype):
         def build():
             return K.cast(self.params["rnn/logits/kernel"].contiguous(), dtype)
-        return self.images(("logits", dtype), build, "bwd")
+        return self.images(("logits", dtype), build)
 
     def logits_image_t(self, dtype):
         """[C][D]: the logits weight transposed (the forward GEMM's B_NK operand)."""
