@@ -434,6 +434,10 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
         case 12: return launch_nt<128, 128, 32, 5, 2, AM>(p, s);
         case 13: return launch_nt<128, 128, 64, 4, 2, AM>(p, s);
         case 14: return launch_nt<128, 64, 64, 3, 2, AM>(p, s);
+        case 15: return launch_nt<64, 96, 64, 3, 2, AM>(p, s);
+        case 16: return launch_nt<64, 128, 32, 4, 2, AM>(p, s);
+        case 17: return launch_nt<128, 96, 64, 3, 2, AM>(p, s);
+        case 18: return launch_nt<64, 128, 64, 3, 2, AM>(p, s);
         default: break;
     }
 #endif
