@@ -291,6 +291,23 @@ def test_adam_matches_oracle(cuda):
     np.testing.assert_allclose(vd.cpu().numpy(), v, rtol=3e-5, atol=1e-9)
 
 
+def test_adam_zero_grad_form(cuda):
+    """ocrk_adam_ex with OCRK_ADAM_ZERO_GRAD (the Trainer's update): the same
+    bits as the plain update, and the gradient cleared as it is read (a length
+    that is not a multiple of 4 exercises the scalar tail)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(3)
+    n = 1003
+    p, g = rng.standard_normal(n).astype(np.float32), rng.standard_normal(n).astype(np.float32)
+    a = [_t(x, cuda) for x in (p, g, np.zeros(n, np.float32), np.zeros(n, np.float32))]
+    b = [_t(x, cuda) for x in (p, g, np.zeros(n, np.float32), np.zeros(n, np.float32))]
+    Kn.adam_(*a, 1e-3, grad_scale=0.5)
+    Kn.adam_(*b, 1e-3, grad_scale=0.5, zero_grad=True)
+    for x, y in zip((a[0], a[2], a[3]), (b[0], b[2], b[3])):
+        assert torch.equal(x, y)
+    assert torch.equal(a[1], _t(g, cuda)) and torch.count_nonzero(b[1]).item() == 0
+
+
 def test_gemm_weight_grad_form_bf16(cuda):
     """dW += x^T . dG as the recurrent backward issues it (bf16 operands, f32
     accumulate into an existing gradient, dG a strided column view, split-K
