@@ -190,11 +190,28 @@ def c1_latency(device, reps=20):
         if i >= 3:
             gpu_ms.append(1e3 * (time.perf_counter() - t0))
     same = [int(v) for v in dense[0].tolist() if v >= 0] == cpu_dec[0]
+    # the same request through the serving path's captured graph (infer.InferGraph):
+    # host crop -> static buffers, one graph launch, the decode read back
+    from cnn_lstm_ctc_ocr_amd.infer import InferGraph
+    g = InferGraph(store, batch=1, width=128, n_classes=95)
+    xh, wh = torch.from_numpy(img), torch.tensor([128], dtype=torch.int32)
+    graph_ms = []
+    for i in range(3 + reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.run(xh, wh)
+        gdec = g.decoded.cpu()
+        if i >= 3:
+            graph_ms.append(1e3 * (time.perf_counter() - t0))
+    same_graph = [int(v) for v in gdec[0].tolist() if v >= 0] == cpu_dec[0]
     return {"workload": "C1: 1 crop 32x128, INFER forward + greedy decode, reference initialisers",
             "cpu_ms": round(float(np.median(cpu_ms)), 3), "cpu_threads": threads, "cpu": cpu,
             "gpu_ms": round(float(np.median(gpu_ms)), 3), "gpu_dtype": "f32",
             "gpu_note": "host wall time incl. launches and the decode's device->host copy",
-            "decode_equal": bool(same)}
+            "gpu_graph_ms": round(float(np.median(graph_ms)), 3),
+            "gpu_graph_note": "the same request as one replay of the captured forward (infer.InferGraph), "
+                              "host crop copied in, decode read back",
+            "decode_equal": bool(same and same_graph)}
 
 
 def cer_vs_ref(device):
