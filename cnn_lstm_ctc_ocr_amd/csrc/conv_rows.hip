@@ -566,10 +566,18 @@ struct RcCfg {
     static constexpr int PART = 9 * CI * CO;
 };
 
+// Wider layers as channel blocks (round 4): blockIdx.y = (ci block, co block) of a
+// CI x CO sub-problem of an XCT -> DCT channel layer (conv5 64 -> 128: two co halves;
+// conv6 128 -> 128: four quadrants), x and dy read with their full channel strides;
+// each workgroup writes its [9][CI][CO] partial as [tap][split] slabs of the block
+// ([y][tap][gridDim.x][CI][CO]), so one ordered split reduce per block lands the
+// taps at their [9][XCT][DCT] rows. Every x / dy byte of the block is read once per
+// workgroup (the 4-wave TN engine re-read the im2col rows per tap: ~700 MB of HBM
+// traffic per conv6 launch).
 template <int CI, int KPX, int CO_>
 __global__ void __launch_bounds__((RcCfg<CI, KPX, CO_>::NT), 1)
 conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
-                             int B, int H, int W) {
+                             int B, int H, int W, int xct, int dct, int nco) {
     using C = RcCfg<CI, KPX, CO_>;
     constexpr int CO = C::CO, TI = CI / 16, NT = C::NT;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -588,14 +596,22 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
         for (int i = 0; i < TI; ++i) acc[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int xq = W * C::XCPR - 1, dq = W * C::DCPR - 1;
+    const int xc0 = (blockIdx.y / nco) * CI, dc0 = (blockIdx.y % nco) * CO;
     u32x4 sx[2][C::XPER], sd[2][C::DPER];
+    // chunk q of a row = pixel q / (CPR) , 8-channel piece q % CPR of the block's channels
     auto load_x = [&](const bf16* base, u32x4 (&v)[C::XPER]) {
 #pragma unroll
-        for (int i = 0; i < C::XPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + NT * i, xq) * 8);
+        for (int i = 0; i < C::XPER; ++i) {
+            const int q = min(tid + NT * i, xq);
+            v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)(q / C::XCPR) * xct + xc0 + (q % C::XCPR) * 8);
+        }
     };
     auto load_d = [&](const bf16* base, u32x4 (&v)[C::DPER]) {
 #pragma unroll
-        for (int i = 0; i < C::DPER; ++i) v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)min(tid + NT * i, dq) * 8);
+        for (int i = 0; i < C::DPER; ++i) {
+            const int q = min(tid + NT * i, dq);
+            v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)(q / C::DCPR) * dct + dc0 + (q % C::DCPR) * 8);
+        }
     };
     auto store_x = [&](int row, const u32x4 (&v)[C::XPER]) {
         char* slot = smem + (row & 3) * C::XSLOT;
@@ -615,10 +631,10 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
     };
 
     for (int b = blockIdx.x; b < B; b += gridDim.x) {
-        const bf16* xb = x + (size_t)b * H * W * CI;
-        const bf16* db = dy + (size_t)b * H * W * CO;
-        auto xrow = [&](int r) { return xb + (size_t)r * W * CI; };
-        auto drow = [&](int r) { return db + (size_t)r * W * CO; };
+        const bf16* xb = x + (size_t)b * H * W * xct;
+        const bf16* db = dy + (size_t)b * H * W * dct;
+        auto xrow = [&](int r) { return xb + (size_t)r * W * xct; };
+        auto drow = [&](int r) { return db + (size_t)r * W * dct; };
         __syncthreads();
         load_x(xrow(0), sx[1]);
         load_d(drow(0), sd[1]);
@@ -669,15 +685,16 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
             if (h + 1 < H) step(h + 1, std::integral_constant<int, 1>{});
         }
     }
-    // this wave's 16 output channels of the [9][CI][64] partial
-    float* out = part + (size_t)blockIdx.x * C::PART;
+    // this wave's 16 output channels of the [9][CI][CO] partial, tap t into slab
+    // [blockIdx.y][t][blockIdx.x]
+    float* out = part + (size_t)blockIdx.y * 9 * gridDim.x * (CI * CO) + (size_t)blockIdx.x * (CI * CO);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                out[(t * CI + 16 * i + 4 * g + e) * CO + 16 * wave + i16] = acc[t][i][e];
+                out[(size_t)t * gridDim.x * (CI * CO) + (16 * i + 4 * g + e) * CO + 16 * wave + i16] = acc[t][i][e];
 }
 
 // Generic forward by rows for the wider layers (conv3-conv6, W <= KPX):
@@ -1057,6 +1074,12 @@ static bool rows_enabled() {
     return !(e && e[0] == '0');
 }
 
+// OCRK_CONV_WGRAD_BLOCKS=0: conv5 / conv6 weight gradients stay on the 4-wave TN engine
+static bool rows_wgrad_blocks() {
+    const char* e = getenv("OCRK_CONV_WGRAD_BLOCKS");
+    return !(e && e[0] == '0');
+}
+
 size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
     return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
 }
@@ -1112,22 +1135,31 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
     return launch_status("conv3x3_dgrad_rows");
 }
 
+// an XCT -> DCT layer as (XCT / CI) x (DCT / CO) channel blocks of CI x CO
 template <int CI, int KPX, int CO = 64>
-static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, float* dw, int accumulate, void* ws,
-                          hipStream_t s) {
+static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, int xct, int dct, float* dw,
+                          int accumulate, void* ws, hipStream_t s) {
     using C = RcCfg<CI, KPX, CO>;
-    const int grid = std::min(B, std::max(cu_count(), 1));
+    const int nci = xct / CI, nco = dct / CO, nb = nci * nco;
+    // one round of workgroups over the blocks (one per CU: ~99 KB of LDS each)
+    const int grid = std::max(1, std::min(B, std::max(cu_count(), 1) / nb));
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX, CO>), C::LDS);
-    conv3x3_wgrad_rows_co_kernel<CI, KPX, CO><<<grid, C::NT, C::LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws,
-                                                                           B, H, W);
+    conv3x3_wgrad_rows_co_kernel<CI, KPX, CO><<<dim3(grid, nb), C::NT, C::LDS, s>>>(
+        (const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W, xct, dct, nco);
     int st = launch_status("conv3x3_wgrad_rows_co");
     if (st) return st;
-    GemmParams p = {};
-    p.M = 9 * CI; p.N = C::CO; p.K = B * H * W; p.batch = 1;
-    p.C = dw; p.ldc = C::CO; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
-    p.splits = grid; p.splitk_ws = (float*)ws;
-    return splitk_finish(p, s);
+    for (int q = 0; q < nb; ++q) {
+        // block q: taps as the batch ([9][grid] slabs of CI x CO), each tap's rows at t * XCT
+        GemmParams p = {};
+        p.M = CI; p.N = CO; p.K = B * H * W; p.batch = 9;
+        p.C = dw + (size_t)(q / nco) * CI * dct + (q % nco) * CO; p.ldc = dct; p.strideC = (int64_t)xct * dct;
+        p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+        p.splits = grid; p.splitk_ws = (float*)ws + (size_t)q * 9 * grid * CI * CO;
+        st = splitk_finish(p, s);
+        if (st) return st;
+    }
+    return OCRK_OK;
 }
 
 // -1 when the shape is not conv2's (Cin = Cout = 32, W <= 254) or the path is off
@@ -1136,12 +1168,14 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
     if (!rows_enabled() || W < 1 || H < 1 || B < 1) return -1;
     if (ws_bytes < conv_rows_wgrad_ws_bytes(B, cin, cout) || (uintptr_t)ws % 16 != 0) return -1;
     if (cout == 64 && W <= 128) {                    // conv3 / conv4
-        if (cin == 32) return launch_rows_co<32, 128>(x, dy, B, H, W, dw, accumulate, ws, s);
-        if (cin == 64) return launch_rows_co<64, 128>(x, dy, B, H, W, dw, accumulate, ws, s);
+        if (cin == 32) return launch_rows_co<32, 128>(x, dy, B, H, W, 32, 64, dw, accumulate, ws, s);
+        if (cin == 64) return launch_rows_co<64, 128>(x, dy, B, H, W, 64, 64, dw, accumulate, ws, s);
         return -1;
     }
-    // conv5 (64 -> 128) would need 8 waves at <= 256 registers: its 144 accumulator
-    // registers spill there, so it stays on the TN engine
+    // conv5 (64 -> 128) and conv6 (128 -> 128) as 64 x 64 channel blocks (one block as
+    // one 8-wave workgroup would spill its 144-288 accumulator registers)
+    if (cout == 128 && W <= 128 && (cin == 64 || cin == 128) && rows_wgrad_blocks())
+        return launch_rows_co<64, 128>(x, dy, B, H, W, cin, 128, dw, accumulate, ws, s);
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;

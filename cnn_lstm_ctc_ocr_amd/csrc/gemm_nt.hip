@@ -445,6 +445,9 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
     // wide N with enough row tiles -> 256 x 256 (8 waves); else 128 x 128 x 64, 2 stages
     if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM>(p, s);
     if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM>(p, s);
+    // N in (64, 96] (the logits, 96 classes): 64 x 96 tiles, three stages -- twice the
+    // workgroups of a 128 x 128 tile with no idle columns (19.9 vs 29.9 us at 32000 x 96 x 1024)
+    if (p.N <= 96) return launch_nt<64, 96, 64, 3, 2, AM>(p, s);
     if (p.N >= 512 && p.M >= 16384) return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
     return launch_nt<128, 128, 64, 2, 2, AM>(p, s);
 }

@@ -326,10 +326,12 @@ def test_gemm_weight_grad_form_bf16(cuda):
     assert _rel(out.cpu().numpy(), ref) < 1e-5
 
 
-# conv2's weight gradient by image rows (conv_rows.hip) against the chunked
-# direct kernel and a float64 reference, at the bench's 30 x 254 rows
+# the weight gradients by image rows (conv_rows.hip) against the chunked direct /
+# TN engines (OCRK_CONV_ROWS=0) and a float64 reference: conv2 at the bench's 30 x 254
+# rows, conv3 / conv4, and conv5 / conv6 as 64 x 64 channel blocks (2 / 4 blocks)
 @pytest.mark.parametrize("B,H,W,C,CO", [(6, 30, 254, 32, 32), (5, 15, 127, 32, 64), (5, 15, 127, 64, 64),
-                                        (3, 4, 9, 64, 64)])
+                                        (3, 4, 9, 64, 64), (3, 7, 126, 64, 128), (3, 7, 126, 128, 128),
+                                        (2, 3, 9, 128, 128)])
 def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(5)
