@@ -432,7 +432,7 @@ extern "C" size_t ocrk_conv3x3_wgrad_workspace_size(int B, int H, int W, int cin
     size_t ws = std::max(ocrk::gemm_splitk_ws_bytes(9 * cin, cout, 1, wgrad_splits(M, cin, cout)),
                          ocrk::conv_direct_wgrad_ws_bytes(B, H, W, cin, cout));
     if ((cin == 32 && cout == 32) || (cout == 64 && (cin == 32 || cin == 64)) ||
-        (cout == 128 && (cin == 64 || cin == 128)))
+        (cout == 128 && (cin == 64 || cin == 128)) || (cout == 256 && (cin == 128 || cin == 256)))
         ws = std::max(ws, ocrk::conv_rows_wgrad_ws_bytes(B, cin, cout));
     return ws;
 }

@@ -1080,6 +1080,12 @@ static bool rows_wgrad_blocks() {
     return !(e && e[0] == '0');
 }
 
+// OCRK_CONV_WGRAD_BLOCKS=2: conv7 / conv8 as channel blocks too (else the ping-pong TN engine)
+static bool rows_wgrad_blocks_wide() {
+    const char* e = getenv("OCRK_CONV_WGRAD_BLOCKS");
+    return e && e[0] == '2';
+}
+
 size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
     return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
 }
@@ -1141,8 +1147,17 @@ static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, in
                           int accumulate, void* ws, hipStream_t s) {
     using C = RcCfg<CI, KPX, CO>;
     const int nci = xct / CI, nco = dct / CO, nb = nci * nco;
-    // one round of workgroups over the blocks (one per CU: ~99 KB of LDS each)
-    const int grid = std::max(1, std::min(B, std::max(cu_count(), 1) / nb));
+    // one round of workgroups over the blocks (one per CU: ~99 KB of LDS each). The
+    // channel-block launches run on the side stream beside the conv backward's main
+    // stream, so they take at most 192 CUs (the other weight-gradient launches' cap):
+    // same box 5.096-5.100 vs 5.097-5.113 ms with all 256, 5.106-5.123 at 128
+    // (OCRK_CONV_WGRAD_CUS overrides; 0 = every CU)
+    static const int cap = [] {
+        const char* e = getenv("OCRK_CONV_WGRAD_CUS");
+        return e ? atoi(e) : 192;
+    }();
+    const int cus = (nb > 1 && cap > 0) ? std::min(cap, cu_count()) : cu_count();
+    const int grid = std::max(1, std::min(B, std::max(cus, 1) / nb));
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX, CO>), C::LDS);
     conv3x3_wgrad_rows_co_kernel<CI, KPX, CO><<<dim3(grid, nb), C::NT, C::LDS, s>>>(
@@ -1176,6 +1191,8 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
     // one 8-wave workgroup would spill its 144-288 accumulator registers)
     if (cout == 128 && W <= 128 && (cin == 64 || cin == 128) && rows_wgrad_blocks())
         return launch_rows_co<64, 128>(x, dy, B, H, W, cin, 128, dw, accumulate, ws, s);
+    if (cout == 256 && W <= 128 && (cin == 128 || cin == 256) && rows_wgrad_blocks_wide())
+        return launch_rows_co<64, 128>(x, dy, B, H, W, cin, 256, dw, accumulate, ws, s);
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;

@@ -331,7 +331,7 @@ def test_gemm_weight_grad_form_bf16(cuda):
 # rows, conv3 / conv4, and conv5 / conv6 as 64 x 64 channel blocks (2 / 4 blocks)
 @pytest.mark.parametrize("B,H,W,C,CO", [(6, 30, 254, 32, 32), (5, 15, 127, 32, 64), (5, 15, 127, 64, 64),
                                         (3, 4, 9, 64, 64), (3, 7, 126, 64, 128), (3, 7, 126, 128, 128),
-                                        (2, 3, 9, 128, 128)])
+                                        (2, 3, 9, 128, 128), (3, 3, 125, 128, 256), (2, 3, 125, 256, 256)])
 def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(5)
@@ -341,6 +341,7 @@ def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
                                      dy.double().permute(0, 3, 1, 2).transpose(0, 1), padding=1)  # [ci][co][3][3]
     ref = ref.permute(2, 3, 0, 1).contiguous()                                                # HWIO
     outs = []
+    monkeypatch.setenv("OCRK_CONV_WGRAD_BLOCKS", "2")           # conv7 / conv8 blocks too (opt-in)
     for mode in ("1", "0"):
         monkeypatch.setenv("OCRK_CONV_ROWS", mode)
         dw = torch.full((3, 3, C, CO), 0.5, device=cuda)
@@ -421,6 +422,7 @@ def test_dgrad_rows_wide_matches(cuda, monkeypatch, CI, CO, H, W, masked):
     w_bwd = (torch.randn(CI, 9 * CO, device=cuda, generator=g) / 20).bfloat16()
     mask = torch.randn(B, H, W, CI, device=cuda, generator=g).bfloat16() if masked else None
     outs = []
+    monkeypatch.setenv("OCRK_CONV_WGRAD_BLOCKS", "2")           # conv7 / conv8 blocks too (opt-in)
     for mode in ("1", "0"):
         monkeypatch.setenv("OCRK_CONV_ROWS", mode)
         db = torch.full((CI,), 0.25, device=cuda) if masked else None
