@@ -421,10 +421,12 @@ class _BiGRU(torch.autograd.Function):
 _TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
 # the lowest layer's weight gradients run beside the conv backward's main-stream
 # kernels (BN backward: 175-212 VGPRs), which cannot share a CU with a 256 x 256
-# TN item (2 waves x 216 VGPRs per SIMD): 192 items leave them 64 CUs. Same-box
+# TN item (2 waves x 216 VGPRs per SIMD): a cap leaves them CUs. Same-box
 # A/B (with the conv weight gradients at 192 too, csrc/conv.hip): 5.215-5.228 vs
-# 5.286-5.288 ms per step; 160: 5.215-5.225, 176: 5.26, 224: 5.25
-_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", "192"))
+# 5.286-5.288 ms per step at 192; 160: 5.215-5.225, 176: 5.26, 224: 5.25. With the
+# 16-row BPTT and the channel-block conv weight gradients (round 4, 7 same-box
+# pairs): 160 5.062-5.091 vs 192 5.081-5.099 ms, 128 5.069-5.094, 224 5.098-5.111
+_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", "160"))
 
 
 # an upper layer's dW_x is queued behind the lower BPTT and meets the lower layer's
