@@ -275,7 +275,7 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
                     unsigned f = base + (unsigned)s;
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(reached(f, base + (unsigned)s))) break;
-                    __builtin_amdgcn_s_sleep(1);
+                    poll_pause();
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_FWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -560,7 +560,7 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
                     unsigned f = base + (unsigned)i;
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(reached(f, base + (unsigned)i))) break;
-                    __builtin_amdgcn_s_sleep(1);
+                    poll_pause();
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -828,7 +828,7 @@ lstm_bwd_r16_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const i
                     unsigned f = base + (unsigned)i;
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(reached(f, base + (unsigned)i))) break;
-                    __builtin_amdgcn_s_sleep(1);
+                    poll_pause();
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
@@ -1064,7 +1064,7 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
                     unsigned f = base + (unsigned)i;
                     if (lane < NU) f = poll_word(gflags + lane, local);
                     if (__all(reached(f, base + (unsigned)i))) break;
-                    __builtin_amdgcn_s_sleep(1);
+                    poll_pause();
                     if (++spins > spin_limit) {
                         if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;

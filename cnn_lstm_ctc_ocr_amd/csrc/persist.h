@@ -99,6 +99,14 @@ __device__ __forceinline__ bool persistent_setup(gu32* flags, int group, int nu,
     return s_setup[2] != 0;
 }
 
+// pause between hand-off polls (s_sleep units of 64 clocks; OCRK_POLL_SLEEP at build time, 0 = spin)
+#ifndef OCRK_POLL_SLEEP
+#define OCRK_POLL_SLEEP 1
+#endif
+__device__ __forceinline__ void poll_pause() {
+    if constexpr (OCRK_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(OCRK_POLL_SLEEP);
+}
+
 // wrap-safe "count has reached target" for the counting flag words
 __device__ __forceinline__ bool reached(unsigned count, unsigned target) { return (int)(count - target) >= 0; }
 
@@ -138,7 +146,7 @@ __device__ __forceinline__ void group_wait(gu32* gflags, int nu, unsigned target
             unsigned f = target;
             if (lane < nu) f = poll_word(gflags + lane, local);
             if (__all(reached(f, target))) break;
-            __builtin_amdgcn_s_sleep(1);
+            poll_pause();
             if (++spins > spin_limit) {
                 if (lane == 0) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 dead = true;
