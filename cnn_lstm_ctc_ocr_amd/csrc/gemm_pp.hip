@@ -376,10 +376,16 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmParams p) {
                     if constexpr (MASK) {
                         const int m = mrow0 + i * 16;
                         if (m < p.M && n < p.N) {
-                            const u16x4 mk = *reinterpret_cast<const u16x4*>(mask + (int64_t)m * p.ldmask + n);
+                            // the 4 mask values as two 32-bit words, each bf16 widened by a shift
+                            // (comparing the u16x4 elements as bf16 kept only element 0's verdict
+                            // for all four: tools/pp_mask_probe.py)
+                            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                            const u32x2 mw = *reinterpret_cast<const u32x2*>(mask + (int64_t)m * p.ldmask + n);
 #pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (!(__builtin_bit_cast(bf16, mk[r]) > (bf16)0.f)) v[r] = 0.f;
+                            for (int r = 0; r < 4; ++r) {
+                                const unsigned bits = (r & 1) ? (mw[r >> 1] & 0xffff0000u) : (mw[r >> 1] << 16);
+                                if (!(__uint_as_float(bits) > 0.f)) v[r] = 0.f;
+                            }
                         }
                     }
                     if (p.relu) {
@@ -503,10 +509,6 @@ int launch_pp_k(const GemmParams& p, hipStream_t stream) {
 
 template <int AM, int BN>
 int launch_pp(const GemmParams& p, hipStream_t stream) {
-    // NOTE (round 4): the MASK epilogue below fails the float64 check at the conv6 /
-    // conv8 data-gradient shapes (tools/pp_conv_check.py: 0.87 relative error with the
-    // mask, 1.7e-3 without) -- the conv modes are routed here only by the experiments
-    // build (OCRK_GEMM_PP=2), never by gemm_pp's product dispatch
     if (AM == A_IM2COL_FLIP && p.mask) {
         if (p.stats) return launch_pp_k<AM, BN, true, true>(p, stream);
         return launch_pp_k<AM, BN, false, true>(p, stream);
@@ -548,6 +550,8 @@ int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
 #else
     constexpr int all = 0;
 #endif
+    // the convolutions stay on the NT / row engines: routed here (N >= 128) they measured
+    // 1.4-2.1x slower per layer and 5.23-5.51 vs 5.08-5.11 ms per step (round 4)
     if (!all && (amode != A_ROWK || p.N < 512)) return -1;         // OCRK_GEMM_PP=2: every shape (make exp)
     if (p.N < 96) return -1;
     // 32-bit buffer offsets
