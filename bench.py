@@ -541,6 +541,8 @@ def main():
                     help="c5: 1 = each bucket's beam search on a second stream beside the next bucket's forward")
     ap.add_argument("--cell", default="lstm", choices=["lstm", "gru"],
                     help="lstm: model_bu.py's BiLSTM 512/512 (BASELINE.json's config); gru: model.py's BiGRU 512/256")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="C3 with N > 1: BatchNorm statistics over all ranks' batches (Trainer(sync_bn=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
@@ -586,7 +588,7 @@ def main():
     T = (W - 2) // 2 - 2
     sizes = RNN_SIZES[args.cell]
     store = ParamStore(ModelConfig(cell=args.cell, rnn_sizes=sizes, dtype=dtype), device=device, seed=0)
-    trainer = Trainer(store)
+    trainer = Trainer(store, sync_bn=args.sync_bn)
     rng = np.random.default_rng(1234 + rank)                # per-rank seed = base + rank
     img, widths, labels = synthetic_batch(rng, B, W, T, device)
 
@@ -717,7 +719,9 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "image": f"32x{W}", "seq_len": T,
                    "parallelism": f"dp{world}",
                    "collective": "one bucketed SUM all-reduce of the flat fp32 gradient per step "
-                                 "(RCCL over xGMI, backend nccl)" if world > 1 else "none"},
+                                 "(RCCL over xGMI, backend nccl)" + (" + SyncBN: 8 small all-reduces"
+                                                                     if args.sync_bn else "")
+                                 if world > 1 else "none"},
         "world_size_seen": dist.get_world_size() if world > 1 else 1,
         "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,

@@ -70,6 +70,12 @@ SIGNATURES = {
     "ocrk_bn_bwd_workspace_size": [_i32, _i32, _i32, _i32],
     "ocrk_bn_relu_pool_bwd": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
                               _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_bn_moments": [_p, _i32, _i32, _i64, _i32, _p, _p, _sz, _p],
+    "ocrk_bn_finalize_moments": [_p, _i32, _f32, _f32, _p, _p, _p, _p, _p],
+    "ocrk_bn_relu_pool_bwd_reduce": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                                     _i32, _p, _p, _i32, _p, _p, _sz, _i32, _p],
+    "ocrk_bn_relu_pool_bwd_apply": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                                    _i32, _p, _p, _p, _p, _i32, _p, _p, _sz, _i32, _p],
     "ocrk_bn_bwd_bias_slab_rows": [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32],
     "ocrk_bn_relu_pool_bwd_slab": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
                                    _i32, _p, _p, _p, _i32, _p, _p, _sz, _i32, _p],

@@ -72,10 +72,34 @@ bn_stats_partial_kernel(const float* __restrict__ stats, int tiles, int64_t M, i
     for (int k = threadIdx.x; k < 3 * C; k += 256) part[(int64_t)blockIdx.x * 3 * C + k] = sacc[k];
 }
 
+// mean / invstd (and the moving averages) of channel c from the merged sums:
+// S = sum x, Q = sum_t s_t^2 / n_t, W2 = sum_t M2_t over nt values
+__device__ __forceinline__ void bn_final_channel(int c, double S, double Q, double W2, double nt, float eps,
+                                                 float momentum, float* __restrict__ mean_out,
+                                                 float* __restrict__ invstd_out, float* __restrict__ moving_mean,
+                                                 float* __restrict__ moving_var) {
+    const double mu = S / nt;
+    const double m2 = fmax(W2 + Q - S * mu, 0.0);
+    const double var = m2 / nt;
+    mean_out[c] = (float)mu;
+    invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (moving_mean) {
+        float dec = 1.f - momentum;
+        double var_u = nt > 1 ? m2 / (nt - 1) : var;
+        moving_mean[c] = moving_mean[c] - (moving_mean[c] - (float)mu) * dec;
+        moving_var[c] = moving_var[c] - (moving_var[c] - (float)var_u) * dec;
+    }
+}
+
+// MOMENTS: write the merged (S, Q, W2) and the count M to moments [3C + 1]
+// instead of finalizing (the cross-rank form: the three sums and the count are
+// additive over ranks, so one SUM all-reduce of the vector then
+// bn_finalize_moments_kernel gives the statistics of the union of the batches)
+template <bool MOMENTS>
 __global__ void __launch_bounds__(256)
 bn_finalize_kernel(const double* __restrict__ part, int nparts, int64_t M, int C, float eps, float momentum,
                    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ moving_mean,
-                   float* __restrict__ moving_var) {
+                   float* __restrict__ moving_var, double* __restrict__ moments) {
     __shared__ double ss[256], sq[256], sw[256];
     const int c = blockIdx.x;
     double S = 0, Q = 0, W2 = 0;
@@ -95,18 +119,34 @@ bn_finalize_kernel(const double* __restrict__ part, int nparts, int64_t M, int C
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const double nt = (double)M, mu = ss[0] / nt;
-        const double m2 = fmax(sw[0] + sq[0] - ss[0] * mu, 0.0);
-        const double var = m2 / nt;
-        mean_out[c] = (float)mu;
-        invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
-        if (moving_mean) {
-            float dec = 1.f - momentum;
-            double var_u = nt > 1 ? m2 / (nt - 1) : var;
-            moving_mean[c] = moving_mean[c] - (moving_mean[c] - (float)mu) * dec;
-            moving_var[c] = moving_var[c] - (moving_var[c] - (float)var_u) * dec;
+        if constexpr (MOMENTS) {
+            moments[c] = ss[0];
+            moments[C + c] = sq[0];
+            moments[2 * C + c] = sw[0];
+            if (c == 0) moments[3 * C] = (double)M;
+        } else {
+            bn_final_channel(c, ss[0], sq[0], sw[0], (double)M, eps, momentum, mean_out, invstd_out, moving_mean,
+                             moving_var);
         }
     }
+}
+
+__global__ void __launch_bounds__(256)
+bn_finalize_moments_kernel(const double* __restrict__ moments, int C, float eps, float momentum,
+                           float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                           float* __restrict__ moving_mean, float* __restrict__ moving_var) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < C)
+        bn_final_channel(c, moments[c], moments[C + c], moments[2 * C + c], moments[3 * C], eps, momentum, mean_out,
+                         invstd_out, moving_mean, moving_var);
+}
+
+// the apply pass's dsum from the cross-rank sums: the kernels scale dsum by
+// 1 / (this launch's pixels), so dsum_ws = dsum * pixels / (all ranks' pixels)
+__global__ void bn_dsum_scale_kernel(const float* __restrict__ dsum, const double* __restrict__ count, int64_t npix,
+                                     int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)((double)dsum[i] * (double)npix / count[0]);
 }
 
 __global__ void bn_infer_params_kernel(const float* mm, const float* mv, int C, float eps,
@@ -546,9 +586,36 @@ extern "C" int ocrk_bn_finalize_tiles(const float* stats, int tiles, int tile_ro
     bn_stats_partial_kernel<<<np, 256, 0, s>>>(stats, tiles, M, tile_rows, C, rpb, (double*)ws);
     int st = ocrk::launch_status("ocrk_bn_finalize partial sums");
     if (st) return st;
-    bn_finalize_kernel<<<C, 256, 0, s>>>((const double*)ws, np, M, C, eps, momentum, mean, invstd, moving_mean,
-                                         moving_var);
+    bn_finalize_kernel<false><<<C, 256, 0, s>>>((const double*)ws, np, M, C, eps, momentum, mean, invstd,
+                                                moving_mean, moving_var, nullptr);
     return ocrk::launch_status("ocrk_bn_finalize");
+}
+
+extern "C" int ocrk_bn_moments(const float* stats, int tiles, int tile_rows, int64_t M, int C, double* moments,
+                               void* ws, size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(tiles >= 1 && C >= 1 && C <= 256 && M >= 1 && tile_rows >= 1 &&
+                 (int64_t)(tiles - 1) * tile_rows < M && (int64_t)tiles * tile_rows >= M,
+                 "ocrk_bn_moments: bad sizes");
+    OCRK_REQUIRE(moments, "ocrk_bn_moments: moments is required");
+    OCRK_REQUIRE(ws && ws_bytes >= ocrk_bn_finalize_workspace_size(tiles, C), "ocrk_bn_moments: workspace too small");
+    hipStream_t s = ocrk::as_stream(stream);
+    const int np0 = std::min(BN_PARTS, tiles);
+    const int rpb = (tiles + np0 - 1) / np0;
+    const int np = (tiles + rpb - 1) / rpb;
+    bn_stats_partial_kernel<<<np, 256, 0, s>>>(stats, tiles, M, tile_rows, C, rpb, (double*)ws);
+    int st = ocrk::launch_status("ocrk_bn_moments partial sums");
+    if (st) return st;
+    bn_finalize_kernel<true><<<C, 256, 0, s>>>((const double*)ws, np, M, C, 0.f, 0.f, nullptr, nullptr, nullptr,
+                                               nullptr, moments);
+    return ocrk::launch_status("ocrk_bn_moments");
+}
+
+extern "C" int ocrk_bn_finalize_moments(const double* moments, int C, float eps, float momentum, float* mean,
+                                        float* invstd, float* moving_mean, float* moving_var, void* stream) {
+    OCRK_REQUIRE(moments && C >= 1 && C <= 256, "ocrk_bn_finalize_moments: bad arguments");
+    bn_finalize_moments_kernel<<<(C + 255) / 256, 256, 0, ocrk::as_stream(stream)>>>(moments, C, eps, momentum, mean,
+                                                                                    invstd, moving_mean, moving_var);
+    return ocrk::launch_status("ocrk_bn_finalize_moments");
 }
 
 extern "C" int ocrk_bn_infer_params(const float* moving_mean, const float* moving_var, int C, float eps,
@@ -631,7 +698,10 @@ extern "C" size_t ocrk_bn_bwd_bias_slab_rows(int B, int H, int W, int C, int kh,
 static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
                        const float* invstd, const float* gamma, const float* beta, int kh, int kw, int sh, int sw,
                        int dp_time_major, void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
-                       float* bias_slab_out, void* ws, size_t ws_bytes, int dtype, void* stream) {
+                       float* bias_slab_out, void* ws, size_t ws_bytes, int dtype, void* stream, int phase = 0,
+                       float* dsum_out = nullptr, const float* dsum_in = nullptr, const double* count = nullptr) {
+    // phase 0: both passes; 1: pass 1 + the ordered sums only (dsum_out gets them); 2: the
+    // apply pass from cross-rank sums dsum_in over count pixels (ws as left by phase 1)
     OCRK_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "ocrk_bn_relu_pool_bwd: C=%d unsupported", C);
     OCRK_REQUIRE(ws_bytes >= ocrk_bn_bwd_workspace_size(B, H, W, C), "ocrk_bn_relu_pool_bwd: workspace too small");
     const int64_t items = (int64_t)B * H * W * (C / 8);
@@ -651,11 +721,21 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
     const int rk = bn_route_variant(kh, kw, sh, sw, H, W);
     if (rk) {
         const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
+        const int64_t tasks = (int64_t)B * Ho * ocrk::cdiv(Wo, BN_ROUTE_SEG) * (C / 8);
+        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
+        nr = (int)ocrk::cdiv(tasks, ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
+    }
+    int st = OCRK_OK;
+    if (phase == 2) {
+        bn_dsum_scale_kernel<<<ocrk::cdiv(2 * C, 256), 256, 0, s>>>(dsum_in, count, npix, 2 * C, dsum);
+        st = ocrk::launch_status("ocrk_bn_relu_pool_bwd_apply scale");
+        if (st) return st;
+    } else if (rk) {
+        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
         const int nseg = (int)ocrk::cdiv(Wo, BN_ROUTE_SEG);
         const int64_t tasks = (int64_t)B * Ho * nseg * (C / 8);
         const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
         const int tpb = (int)(ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
-        nr = (int)ocrk::cdiv(tasks, tpb);
 #define ROUTE_ARGS B, H, W, C, mean, invstd, gamma, beta, dp_time_major, nseg, tpb, slab
         if (dtype == OCRK_BF16) {
             const bf16 *zz = (const bf16*)z, *pp = (const bf16*)dp;
@@ -678,10 +758,12 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
     } else {
         bn_bwd_reduce_kernel<float><<<nb, 256, 0, s>>>((const float*)z, (const float*)dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, (int)ipb, slab, (float*)da);
     }
-    int st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
-    if (st) return st;
-    st = slab_sum(slab, nr, 2 * C, part, dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
-    if (st) return st;
+    if (phase != 2) {
+        st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
+        if (st) return st;
+        st = slab_sum(slab, nr, 2 * C, part, phase == 1 ? dsum_out : dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
+        if (st || phase == 1) return st;
+    }
     if (rk == 1 || rk == 3) {
         // pass 2 repeats the window walk (no staged da image): dz and the conv-bias partial sums
         const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
@@ -737,4 +819,33 @@ extern "C" int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, 
     OCRK_REQUIRE(bias_slab, "ocrk_bn_relu_pool_bwd_slab: bias_slab is required");
     return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
                        dbeta, nullptr, accumulate, bias_slab, ws, ws_bytes, dtype, stream);
+}
+
+// The two passes apart, for BatchNorm statistics over several ranks' batches:
+// _reduce accumulates this batch's dgamma / dbeta and writes its ordered sums
+// dsum [2C] (sum dy | sum dy * xhat, routed through ReLU + pool); the caller
+// SUM-reduces dsum over the ranks; _apply then forms dz with the cross-rank sums
+// over `count` (device double: all ranks' pixels, ocrk_bn_moments' last entry
+// after the same all-reduce). ws is shared by the two calls and must be left
+// untouched between them. One rank with dsum unchanged and count = B*H*W
+// reproduces ocrk_bn_relu_pool_bwd[_slab] up to the rounding of the scale.
+extern "C" int ocrk_bn_relu_pool_bwd_reduce(const void* z, const void* dp, int B, int H, int W, int C,
+                                            const float* mean, const float* invstd, const float* gamma,
+                                            const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                            float* dgamma, float* dbeta, int accumulate, float* dsum, void* ws,
+                                            size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(dsum, "ocrk_bn_relu_pool_bwd_reduce: dsum is required");
+    return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, nullptr, dgamma,
+                       dbeta, nullptr, accumulate, nullptr, ws, ws_bytes, dtype, stream, 1, dsum);
+}
+
+extern "C" int ocrk_bn_relu_pool_bwd_apply(const void* z, const void* dp, int B, int H, int W, int C,
+                                           const float* mean, const float* invstd, const float* gamma,
+                                           const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                           const float* dsum, const double* count, void* dz, float* dbias,
+                                           int accumulate, float* bias_slab, void* ws, size_t ws_bytes, int dtype,
+                                           void* stream) {
+    OCRK_REQUIRE(dsum && count && dz, "ocrk_bn_relu_pool_bwd_apply: dsum, count and dz are required");
+    return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, nullptr,
+                       nullptr, dbias, accumulate, bias_slab, ws, ws_bytes, dtype, stream, 2, nullptr, dsum, count);
 }

@@ -149,6 +149,27 @@ def bn_finalize(stats, M, C, eps, momentum, moving_mean=None, moving_var=None, t
     return mean, invstd
 
 
+def bn_finalize_sync(stats, M, C, eps, momentum, moving_mean, moving_var, tile_rows, group):
+    """bn_finalize over the union of the data-parallel ranks' batches (SyncBN):
+    this rank's moments [3C + 1] (sum, between-tile and within-tile squares,
+    count) SUM-all-reduced over `group`, then finalized; every rank gets the
+    same mean / invstd / moving averages. Returns (mean, invstd, count) with
+    count the all-reduced pixel total (a device f64 [1], for the backward)."""
+    import torch.distributed as dist
+    _chk(stats, moving_mean, moving_var)
+    tiles = stats.shape[0]
+    moments = torch.empty(3 * C + 1, dtype=torch.float64, device=stats.device)
+    nb = _lib.lib().ocrk_bn_finalize_workspace_size(tiles, C)
+    ws = _ws(nb, stats.device)
+    call("ocrk_bn_moments", ptr(stats), tiles, int(tile_rows), M, C, ptr(moments), ptr(ws), nb, _stream(stats))
+    dist.all_reduce(moments, op=dist.ReduceOp.SUM, group=group)
+    mean = torch.empty(C, dtype=torch.float32, device=stats.device)
+    invstd = torch.empty_like(mean)
+    call("ocrk_bn_finalize_moments", ptr(moments), C, float(eps), float(momentum), ptr(mean), ptr(invstd),
+         ptr(moving_mean), ptr(moving_var), _stream(stats))
+    return mean, invstd, moments[3 * C:]
+
+
 def conv3x3_fwd_rowstats_ok(x, cout):
     """Does the conv2 row kernel take this forward (bf16, Cin = Cout = 32, W <= 254)?"""
     if x.dtype != torch.bfloat16 or not x.is_cuda:
@@ -193,17 +214,22 @@ def bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=False):
 
 
 def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True,
-                     dbias=None, defer=None):
+                     dbias=None, defer=None, sync=None):
     """dz of BN + ReLU + max-pool; dgamma, dbeta and (optionally) dbias = column
     sums of dz (the conv bias in front of the BN) accumulate in f32. With a
     `defer` list the dbias reduction is appended to it as (fn, tensors)
-    (ocrk_bn_relu_pool_bwd_slab + ocrk_slab_sum, same bits)."""
+    (ocrk_bn_relu_pool_bwd_slab + ocrk_slab_sum, same bits). sync = (group,
+    count): SyncBN -- the batch statistics were bn_finalize_sync's, so the
+    backward's two sums are SUM-all-reduced over `group` between its passes."""
     _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta, dbias)
     B, H, W, C = z.shape
     kh, kw, sh, sw = pool
     nb = _lib.lib().ocrk_bn_bwd_workspace_size(B, H, W, C)
     ws = _ws(nb, z.device)
     dz = torch.empty_like(z)
+    if sync is not None:
+        return _bn_bwd_sync(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate, dbias,
+                            defer, sync, dz, ws, nb)
     if dbias is not None and defer is not None:
         rows = _lib.lib().ocrk_bn_bwd_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
         slab = torch.empty(rows, C, dtype=torch.float32, device=z.device)
@@ -216,6 +242,29 @@ def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgam
          kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta), ptr(dbias), int(accumulate),
          ptr(ws), nb,
          dtype_code(z.dtype), _stream(z))
+    return dz
+
+
+def _bn_bwd_sync(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate, dbias, defer,
+                 sync, dz, ws, nb):
+    import torch.distributed as dist
+    group, count = sync
+    B, H, W, C = z.shape
+    kh, kw, sh, sw = pool
+    dsum = torch.empty(2 * C, dtype=torch.float32, device=z.device)
+    args = (ptr(z), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), kh, kw, sh, sw,
+            int(dp_time_major))
+    call("ocrk_bn_relu_pool_bwd_reduce", *args, ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dsum), ptr(ws), nb,
+         dtype_code(z.dtype), _stream(z))
+    dist.all_reduce(dsum, op=dist.ReduceOp.SUM, group=group)
+    slab = None
+    if dbias is not None and defer is not None:
+        rows = _lib.lib().ocrk_bn_bwd_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
+        slab = torch.empty(rows, C, dtype=torch.float32, device=z.device)
+    call("ocrk_bn_relu_pool_bwd_apply", *args, ptr(dsum), ptr(count), ptr(dz),
+         ptr(dbias if slab is None else None), int(accumulate), ptr(slab), ptr(ws), nb, dtype_code(z.dtype), _stream(z))
+    if slab is not None:
+        defer.append((lambda: slab_sum(slab, rows, C, C, dbias, accumulate), (slab,)))
     return dz
 
 

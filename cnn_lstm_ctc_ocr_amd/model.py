@@ -25,6 +25,7 @@ import os
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import kernels as K
 from .config import BN_EPS, BN_MOMENTUM, INFER, LAYER_PARAMS, POOLS, TRAIN, ModelConfig, rnn_size  # noqa: F401
@@ -65,6 +66,7 @@ class _ConvBlock(torch.autograd.Function):
         odd, even = f"conv{2 * k - 1}", f"conv{2 * k}"
         P = store.params
         pe = f"convnet/{even}"
+        ctx.bn_sync = None
         if k == 1:
             y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
         else:
@@ -83,9 +85,17 @@ class _ConvBlock(torch.autograd.Function):
                 stats = torch.empty(K.conv_stats_tiles(M), 2, C, dtype=torch.float32, device=x.device)
                 z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False, stats=stats)
                 trows = 128
-            mean, invstd = K.bn_finalize(stats, M, C, BN_EPS, BN_MOMENTUM,
-                                         store.stats[pe + "/batch_norm/moving_mean"],
-                                         store.stats[pe + "/batch_norm/moving_variance"], tile_rows=trows)
+            group = _bn_group(store)
+            if group is not None:                          # SyncBN: statistics of all ranks' batches
+                mean, invstd, count = K.bn_finalize_sync(stats, M, C, BN_EPS, BN_MOMENTUM,
+                                                         store.stats[pe + "/batch_norm/moving_mean"],
+                                                         store.stats[pe + "/batch_norm/moving_variance"], trows,
+                                                         group)
+                ctx.bn_sync = (group, count)
+            else:
+                mean, invstd = K.bn_finalize(stats, M, C, BN_EPS, BN_MOMENTUM,
+                                             store.stats[pe + "/batch_norm/moving_mean"],
+                                             store.stats[pe + "/batch_norm/moving_variance"], tile_rows=trows)
         else:
             z = K.conv3x3_fwd(y_odd, w_nk, P[pe + "/bias"], relu=False)
             mean, invstd = K.bn_infer_params(store.stats[pe + "/batch_norm/moving_mean"],
@@ -114,7 +124,8 @@ class _ConvBlock(torch.autograd.Function):
         dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                 POOLS[even], dp_time_major=(k == 4),
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
-                                dbias=G[pe + "/bias"], defer=late)      # conv bias grad fused
+                                dbias=G[pe + "/bias"], defer=late,      # conv bias grad fused
+                                sync=ctx.bn_sync)
         B, H, W, C = dz.shape
         if k > 1:
             _issue(store, late)
@@ -142,6 +153,15 @@ class _ConvBlock(torch.autograd.Function):
                 _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
         return (dx, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
+
+
+def _bn_group(store):
+    """The process group of SyncBN (store.bn_group, set by Trainer(sync_bn=True))
+    when it spans more than one rank, else None (per-rank statistics)."""
+    g = store.bn_group
+    if g is None or not (dist.is_available() and dist.is_initialized()):
+        return None
+    return g if dist.get_world_size(g) > 1 else None
 
 
 def _block_variables(store, k):

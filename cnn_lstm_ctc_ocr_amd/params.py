@@ -140,6 +140,7 @@ class ParamStore:
         self._images = {}
         self.pending = []          # events of side-stream gradient work not yet joined
         self.deferred = []         # (launch fn, tensors) of gradient work an upper layer deferred
+        self.bn_group = None       # SyncBN: the process group TRAIN-mode BatchNorm statistics span
         self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
 
     # ------------------------------------------------------------ state

@@ -10,7 +10,8 @@ Data parallel: when torch.distributed is initialised with world_size > 1 the
 flat fp32 gradient buffer is summed with ONE all-reduce (RCCL over xGMI on
 MI355X, backend "nccl") and the Adam kernel divides by world_size -- the mean
 of per-rank means, which equals the global mean for equal shards because the
-loss is a batch mean (model.py:228). BatchNorm statistics stay per rank.
+loss is a batch mean (model.py:228). BatchNorm statistics stay per rank
+unless Trainer(sync_bn=True).
 """
 import collections
 import math
@@ -146,12 +147,17 @@ class Trainer:
 
     def __init__(self, store, learning_rate=1e-4, momentum=0.9, decay_rate=0.9, decay_steps=2 ** 16,
                  decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0,
-                 summary=None, summary_every=100):
+                 summary=None, summary_every=100, sync_bn=False):
         """summary: a summary.SummaryWriter; every `summary_every` steps it gets
         learning_rate (train.py:139's tf.summary.scalar), the step's loss and
         the global crops/s since the previous record (no sync: device values
-        are copied asynchronously)."""
+        are copied asynchronously). sync_bn: under data parallelism the
+        TRAIN-mode BatchNorm statistics (and the backward's two sums) span all
+        ranks' batches -- one small SUM all-reduce per BN layer each way -- so N
+        ranks compute the single-device reference's step on the union of their
+        batches; off (the default) they stay per rank."""
         self.store = store
+        store.bn_group = (process_group if process_group is not None else dist.group.WORLD) if sync_bn else None
         self.summary = summary
         self.summary_every = max(1, int(summary_every))
         self._summary_mark = None

@@ -187,6 +187,17 @@ int ocrk_bn_finalize_tiles(const float* stats, int tiles, int tile_rows, int64_t
 int ocrk_bn_finalize(const float* stats, int tiles, int64_t M, int C, float eps, float momentum,
                      float* mean, float* invstd, float* moving_mean, float* moving_var, void* ws, size_t ws_bytes,
                      void* stream);   /* ws: ocrk_bn_finalize_workspace_size bytes (row-range partial sums) */
+/* Batch statistics over several data-parallel ranks' batches (SyncBN; the
+ * reference is one device, so N ranks with these match its statistics over the
+ * union of their batches). ocrk_bn_moments: this rank's merged sums of the same
+ * partials, moments f64 [3C + 1] = (sum x | sum_t s_t^2/n_t | sum_t M2_t | M),
+ * all additive over ranks; SUM-all-reduce the vector, then
+ * ocrk_bn_finalize_moments = ocrk_bn_finalize of the union (the moving averages
+ * with the union's unbiased variance). ws: ocrk_bn_finalize_workspace_size. */
+int ocrk_bn_moments(const float* stats, int tiles, int tile_rows, int64_t M, int C, double* moments, void* ws,
+                    size_t ws_bytes, void* stream);
+int ocrk_bn_finalize_moments(const double* moments, int C, float eps, float momentum, float* mean, float* invstd,
+                             float* moving_mean, float* moving_var, void* stream);
 int ocrk_bn_infer_params(const float* moving_mean, const float* moving_var, int C, float eps,
                          float* mean, float* invstd, void* stream);
 /* out = maxpool(relu(gamma (z-mean) invstd + beta)), window kh x kw, stride
@@ -212,6 +223,21 @@ int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, int H, int 
                                int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
                                int accumulate, float* bias_slab, void* ws, size_t ws_bytes, int dtype,
                                void* stream);
+/* The backward's two passes apart, for SyncBN: _reduce accumulates this rank's
+ * dgamma / dbeta and writes dsum f32 [2C] (sum dy | sum dy*xhat through the ReLU
+ * and pool routing); SUM-all-reduce dsum over the ranks; _apply forms dz from
+ * those sums over `count` (device f64: all ranks' pixels, ocrk_bn_moments' last
+ * entry after its all-reduce), with dbias / bias_slab as above. The same ws
+ * serves both calls and must be left untouched between them. */
+int ocrk_bn_relu_pool_bwd_reduce(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
+                                 const float* invstd, const float* gamma, const float* beta, int kh, int kw,
+                                 int sh, int sw, int dp_time_major, float* dgamma, float* dbeta, int accumulate,
+                                 float* dsum, void* ws, size_t ws_bytes, int dtype, void* stream);
+int ocrk_bn_relu_pool_bwd_apply(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta, int kh, int kw,
+                                int sh, int sw, int dp_time_major, const float* dsum, const double* count,
+                                void* dz, float* dbias, int accumulate, float* bias_slab, void* ws,
+                                size_t ws_bytes, int dtype, void* stream);
 
 /* ------------------------------------------------------------- recurrent
  * a7' -- rnn_layer with LSTMCell (src/weinman/model_bu.py:167-199), both

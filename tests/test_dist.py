@@ -139,3 +139,72 @@ def test_status_word_is_or_reduced_over_ranks():
     out = mgr.dict()
     mp.spawn(_status_worker, args=(2, port, out), nprocs=2, join=True)
     assert out[0] == out[1] == 0x32
+
+
+# ------------------------------------------------------------------ SyncBN
+def _bn_shard(rank):
+    rng = np.random.default_rng(300 + rank)
+    x = rng.standard_normal((2 + rank, 3, 50, 8)) * 1.5 + 0.3     # unequal shards: 300 and 450 pixels
+    dy = rng.standard_normal(x.shape)
+    return x, dy
+
+
+def _moments(x, tile_rows=128):
+    """The additive per-rank summary ocrk_bn_moments leaves (bn.hip): per-tile
+    (sum, M2) merged as S = sum x, Q = sum_t s_t^2 / n_t, W2 = sum_t M2_t, and M."""
+    v = x.reshape(-1, x.shape[-1])
+    S, Q, W2 = (np.zeros(v.shape[1]) for _ in range(3))
+    for t0 in range(0, v.shape[0], tile_rows):
+        blk = v[t0:t0 + tile_rows]
+        s = blk.sum(0)
+        S += s
+        Q += s * s / blk.shape[0]
+        W2 += ((blk - blk.mean(0)) ** 2).sum(0)
+    return np.concatenate([S, Q, W2, [v.shape[0]]])
+
+
+def _syncbn_worker(rank, world, port, out):
+    """Host protocol of Trainer(sync_bn=True) per BN layer: SUM all-reduce of
+    the moments, finalize (bn_final_channel); backward SUM all-reduce of
+    (sum dy, sum dy*xhat), dz over the union's count."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, dy = _bn_shard(rank)
+    C = x.shape[-1]
+    mom = torch.from_numpy(_moments(x))
+    dist.all_reduce(mom, op=dist.ReduceOp.SUM)
+    S, Q, W2, n = mom[:C].numpy(), mom[C:2 * C].numpy(), mom[2 * C:3 * C].numpy(), mom[3 * C].item()
+    mu = S / n
+    var = np.maximum(W2 + Q - S * mu, 0.0) / n
+    inv = 1.0 / np.sqrt(var + G.BN_EPS)
+    xhat = (x - mu) * inv
+    dsum = torch.from_numpy(np.concatenate([dy.sum((0, 1, 2)), (dy * xhat).sum((0, 1, 2))]))
+    dist.all_reduce(dsum, op=dist.ReduceOp.SUM)
+    gamma = np.linspace(0.5, 1.5, C)
+    dx = gamma * inv * (dy - dsum[:C].numpy() / n - xhat * dsum[C:].numpy() / n)
+    out[rank] = (mu, var, dx)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sync_bn_protocol_matches_the_union_batch():
+    """Two ranks with unequal shards: the all-reduced moments give the union's
+    batch mean / variance and the split backward gives the union's dx rows
+    (oracle bn_train / bn_bwd on the concatenated batch, model.py:118-123)."""
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_syncbn_worker, args=(world, port, out), nprocs=world, join=True)
+    xs, dys = zip(*[_bn_shard(r) for r in range(world)])
+    x, dy = np.concatenate(xs), np.concatenate(dys)
+    C = x.shape[-1]
+    gamma = np.linspace(0.5, 1.5, C)
+    _, mean, var, _, cache = G.bn_train(x, gamma, np.zeros(C))
+    dx, _, _ = G.bn_bwd(dy, cache, gamma)
+    rows = np.cumsum([0] + [s.shape[0] for s in xs])
+    for r in range(world):
+        mu_r, var_r, dx_r = out[r]
+        np.testing.assert_allclose(mu_r, mean, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(var_r, var, rtol=1e-12)
+        np.testing.assert_allclose(dx_r, dx[rows[r]:rows[r + 1]], rtol=1e-10, atol=1e-12)
