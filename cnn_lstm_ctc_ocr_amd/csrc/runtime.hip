@@ -2,6 +2,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include "common.h"
 
 namespace ocrk {
@@ -65,6 +66,39 @@ int ocrk_timer_record(void* ev, void* stream) {
     }
     if (e != hipSuccess) {
         ocrk::set_error("ocrk_timer_record: %s", hipGetErrorString(e));
+        return OCRK_ERR_HIP;
+    }
+    return OCRK_OK;
+}
+
+int ocrk_stream_wait(void* waiter, void* signaller, int mode) {
+    OCRK_REQUIRE(mode >= 0 && mode <= 2, "ocrk_stream_wait: mode %d", mode);
+    constexpr int RING = 64, MAXDEV = 64;
+    static std::mutex mu;
+    static hipEvent_t ring[MAXDEV][3][RING] = {};
+    static int next[MAXDEV][3] = {};
+    int dev = 0;
+    // the events live on the signaller's device (a ring per device and mode)
+    if (hipStreamGetDevice(ocrk::as_stream(signaller), &dev) != hipSuccess || dev < 0 || dev >= MAXDEV)
+        return ocrk::launch_status("ocrk_stream_wait");
+    std::lock_guard<std::mutex> lk(mu);
+    const int i = next[dev][mode];
+    hipEvent_t& ev = ring[dev][mode][i];
+    if (!ev) {
+        const unsigned fl = hipEventDisableTiming |
+                            (mode == 1 ? hipEventDisableSystemFence : mode == 2 ? hipEventReleaseToDevice : 0u);
+        int cur = 0;
+        hipGetDevice(&cur);
+        if (cur != dev) hipSetDevice(dev);              // created on the signaller's device
+        const hipError_t ce = hipEventCreateWithFlags(&ev, fl);
+        if (cur != dev) hipSetDevice(cur);
+        if (ce != hipSuccess) return ocrk::launch_status("ocrk_stream_wait create");
+    }
+    next[dev][mode] = (i + 1) % RING;
+    hipError_t e = hipEventRecord(ev, ocrk::as_stream(signaller));
+    if (e == hipSuccess) e = hipStreamWaitEvent(ocrk::as_stream(waiter), ev, 0);
+    if (e != hipSuccess) {
+        ocrk::set_error("ocrk_stream_wait: %s", hipGetErrorString(e));
         return OCRK_ERR_HIP;
     }
     return OCRK_OK;

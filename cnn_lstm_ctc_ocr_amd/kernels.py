@@ -4,6 +4,9 @@ They check shapes/dtypes/devices on the host, allocate outputs and workspaces
 with the torch caching allocator, and launch on torch's current stream. They
 do no math themselves: every call lands in libocrk.so (include/ocrk.h).
 """
+import ctypes
+import os
+
 import torch
 
 from . import _lib
@@ -622,6 +625,48 @@ def permute3(x, d0, d1, d2, dtype, out=None):
     return out
 
 
+def stream_wait(waiter, signaller, mode=1):
+    """`waiter` (a torch.cuda.Stream) waits for the work issued so far on
+    `signaller` (ocrk_stream_wait: an event without the system-scope release)."""
+    call("ocrk_stream_wait", ctypes.c_void_p(waiter.cuda_stream), ctypes.c_void_p(signaller.cuda_stream), int(mode))
+
+
+# cross-stream ordering inside a step (the side-stream forks and joins, the status
+# copy's fork): 0 default torch events, 1 / 2 ocrk_stream_wait's modes (OCRK_FORK_EVENTS)
+FORK_MODE = int(os.environ.get("OCRK_FORK_EVENTS", "0"))
+
+
+def fork(waiter, signaller):
+    """waiter.wait_stream(signaller), through ocrk_stream_wait when FORK_MODE is
+    set and the signaller is not being captured into a graph."""
+    if FORK_MODE and not torch.cuda.is_current_stream_capturing():
+        stream_wait(waiter, signaller, FORK_MODE)
+    else:
+        waiter.wait_stream(signaller)
+
+
+class StreamMark:
+    """A side stream as a wait target (the store's pending list): wait_on(waiter)
+    orders `waiter` after everything issued on the stream up to that call --
+    a superset of the work up to the mark, which is what the joins need (they
+    wait for all of it) -- through ocrk_stream_wait, without the system-scope
+    release a default event record costs the recording stream."""
+
+    def __init__(self, stream, mode):
+        self.stream, self.mode = stream, mode
+
+    def wait_on(self, waiter):
+        stream_wait(waiter, self.stream, self.mode)
+
+
+def wait_mark(waiter, mark):
+    """waiter waits for a pending entry: a StreamMark or a torch.cuda.Event."""
+    if isinstance(mark, StreamMark):
+        mark.wait_on(waiter)
+    else:
+        waiter.wait_event(mark)
+
+
 def copy_batch(table, njobs, total_tiles, stream_of):
     """One launch of the 2-D copy jobs in `table` (int64 device tensor [njobs, 8],
     include/ocrk.h ocrk_copy_batch): the weight images of a parameter version."""
@@ -638,7 +683,6 @@ def strided_copy(src, rows, cols, in_rs, in_cs, out, out_rs, out_cs, out_offset=
 
 
 def ctypes_offset(t, elems):
-    import ctypes
     return ctypes.c_void_p(t.data_ptr() + elems * t.element_size())
 
 

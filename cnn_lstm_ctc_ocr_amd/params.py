@@ -181,7 +181,7 @@ class ParamStore:
         if self.pending:
             cur = torch.cuda.current_stream(self.device)
             for ev in self.pending:
-                cur.wait_event(ev)
+                K.wait_mark(cur, ev)
             self.pending.clear()
 
     def bump(self):

@@ -66,9 +66,9 @@ class GradBuckets:
         if g.is_cuda:
             if self._stream is None:
                 self._stream = torch.cuda.Stream(g.device)
-            self._stream.wait_stream(torch.cuda.current_stream(g.device))
+            K.fork(self._stream, torch.cuda.current_stream(g.device))
             for ev in self.store.pending:                   # the side-stream weight gradients
-                self._stream.wait_event(ev)
+                K.wait_mark(self._stream, ev)
             with torch.cuda.stream(self._stream):
                 self.work = dist.all_reduce(g[self.split:], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                 g.record_stream(self._stream)
@@ -304,7 +304,7 @@ class Trainer:
         # the copy waits for the step on its own stream: the next step's first kernels
         # do not queue behind it on the main stream
         cur = torch.cuda.current_stream(dev)
-        self._status_stream.wait_stream(cur)
+        K.fork(self._status_stream, cur)
         with torch.cuda.stream(self._status_stream):
             self._status_host.copy_(K.status_word(dev), non_blocking=True)
             self._status_ev = torch.cuda.Event()

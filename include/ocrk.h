@@ -434,6 +434,14 @@ int ocrk_timer_record(void* ev, void* stream);
 int ocrk_timer_elapsed(void* ev0, void* ev1, float* ms);
 int ocrk_timer_destroy(void* ev);
 
+/* Stream ordering on one device: `waiter` waits for everything issued so far on
+ * `signaller` (the weight-gradient side streams' fork from the main stream).
+ * mode 1: a ring of events created with hipEventDisableSystemFence; mode 2: with
+ * hipEventReleaseToDevice -- both skip the system-scope release a default event
+ * record makes (a ~6 us bubble on the recording stream); mode 0: a default
+ * event. Not for streams being captured (the caller uses a graph-aware event). */
+int ocrk_stream_wait(void* waiter, void* signaller, int mode);
+
 /* Host-side CRC32C (Castagnoli) of n bytes continuing from `crc` (0 to start):
  * TFRecord framing and TensorBundle checksums for the input pipeline and the
  * checkpoint reader/writer (src/weinman/mjsynth.py:148-172, train.py:152-165). */

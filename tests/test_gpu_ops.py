@@ -205,6 +205,22 @@ def test_slab_sum_matches_colsum_order(cuda):
     np.testing.assert_allclose(out2.cpu().numpy(), strided[:, :40].double().sum(0).cpu().numpy(), rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("nslab,nc", [(2085, 512), (777, 64), (2048, 256), (31, 128)])
+def test_slab_sum_fixed_order_bits(cuda, nslab, nc):
+    """The one-launch form's order (tensor_ops.hip slab_sum_fused): row group rg
+    of 16 adds rows rg, rg + 16, ... in sequence (double), then the 16 groups in
+    order; the 32- / 8- / 1-row load batches must not change it."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    g = torch.Generator(device="cpu").manual_seed(nslab)
+    x = torch.randn(nslab, nc, generator=g) * torch.rand(nslab, 1, generator=g) * 10
+    out = torch.zeros(nc, device=cuda)
+    Kn.slab_sum(x.to(cuda), nslab, nc, nc, out, accumulate=False)
+    xd = x.double().numpy()
+    groups = [np.cumsum(xd[rg::16], axis=0)[-1] if rg < nslab else np.zeros(nc) for rg in range(16)]
+    want = np.cumsum(np.stack(groups), axis=0)[-1].astype(np.float32)
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
 # column sums (bias gradients of the odd convs, recurrent and logits layers)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N", [(37, 64), (5000, 24), (3001, 4096), (20000, 256)])
