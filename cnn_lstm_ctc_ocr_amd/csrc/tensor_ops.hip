@@ -282,131 +282,101 @@ struct CopyJob {
 };
 static_assert(sizeof(CopyJob) == 8 * 8, "job layout (include/ocrk.h)");
 
-// A workgroup moves COPY_TPW consecutive tiles (jobs may change between them):
-// the job search runs over the table's first tiles staged in LDS, every tile's
-// reads are issued before any is staged (the ~21k one-tile workgroups of a
-// parameter version were latency-bound on the dependent search loads and one
-// read round trip each). Jobs whose sizes, strides and addresses are 4-element
-// aligned (all but the 95-column logits) move a float4 read and a 4-element
-// packed write per thread and tile; the rest keep the scalar 32 x 8 form.
-constexpr int COPY_JOBS_LDS = 256, COPY_TPW = 4;
-__global__ void __launch_bounds__(256) copy_batch_kernel(const CopyJob* __restrict__ jobs, int njobs,
-                                                         int64_t total_tiles) {
-    __shared__ float tile[COPY_TPW][32][33];
+// The job search runs over the tables' first tiles staged in LDS (one load
+// round trip instead of a chain of dependent global loads per workgroup: the
+// ~21k single-tile workgroups of a parameter version were latency-bound on it).
+// Jobs whose sizes, strides and addresses are 4-element aligned (all but the
+// 95-column logits) move 16-B float4 reads and 4-element packed writes (one
+// each per thread); the rest keep the scalar form.
+constexpr int COPY_JOBS_LDS = 256;
+__global__ void __launch_bounds__(256) copy_batch_kernel(const CopyJob* __restrict__ jobs, int njobs) {
+    __shared__ float tile[32][33];
     __shared__ int64_t first[COPY_JOBS_LDS];
-    const bool lds_search = njobs <= COPY_JOBS_LDS;
-    if (lds_search) {
+    const int64_t t = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    if (njobs <= COPY_JOBS_LDS) {
         if ((int)threadIdx.x < njobs) first[threadIdx.x] = jobs[threadIdx.x].tile0;
         __syncthreads();
-    }
-    const int q = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;         // vector form: tile row, 4 columns
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;             // scalar form: 32 x 8
-    int jk[COPY_TPW];
-    float4 v[COPY_TPW];
-    float sv[COPY_TPW][4];
-#pragma unroll
-    for (int k = 0; k < COPY_TPW; ++k) {
-        const int64_t t = (int64_t)blockIdx.x * COPY_TPW + k;
-        jk[k] = -1;
-        if (t >= total_tiles) continue;
-        int lo = 0, hi = njobs - 1;
         while (lo < hi) {                               // last job with tile0 <= t
             const int mid = (lo + hi + 1) >> 1;
-            if ((lds_search ? first[mid] : jobs[mid].tile0) <= t) lo = mid; else hi = mid - 1;
+            if (first[mid] <= t) lo = mid; else hi = mid - 1;
         }
-        jk[k] = lo;
-        const CopyJob& j = jobs[lo];
-        const int64_t lt = t - j.tile0, tc = (j.cols + 31) / 32;
-        const int64_t r0 = (lt / tc) * 32, c0 = (lt % tc) * 32;
-        const bool vec = ((j.rows | j.cols | j.in_rs | j.out_rs) & 3) == 0 && ((uintptr_t)j.src & 15) == 0 &&
-                         ((uintptr_t)j.dst & (j.dtype == OCRK_BF16 ? 7 : 15)) == 0;
-        if (vec) {
-            v[k] = (r0 + q < j.rows && c0 + c4 < j.cols)
-                       ? *reinterpret_cast<const float4*>(j.src + (r0 + q) * j.in_rs + c0 + c4)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {
-            jk[k] = -2 - lo;                            // scalar form
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int64_t r = r0 + ty + 8 * m, c = c0 + tx;
-                sv[k][m] = (r < j.rows && c < j.cols) ? j.src[r * j.in_rs + c] : 0.f;
-            }
+    } else {
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (jobs[mid].tile0 <= t) lo = mid; else hi = mid - 1;
         }
     }
-#pragma unroll
-    for (int k = 0; k < COPY_TPW; ++k) {
-        if (jk[k] >= 0) {
-            tile[k][q][c4] = v[k].x; tile[k][q][c4 + 1] = v[k].y;
-            tile[k][q][c4 + 2] = v[k].z; tile[k][q][c4 + 3] = v[k].w;
-        } else if (jk[k] <= -2) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m) tile[k][ty + 8 * m][tx] = sv[k][m];
+    const CopyJob j = jobs[lo];
+    const int64_t lt = t - j.tile0, tc = (j.cols + 31) / 32;
+    const int64_t r0 = (lt / tc) * 32, c0 = (lt % tc) * 32;
+    const bool bf = j.dtype == OCRK_BF16;
+    const bool vec = ((j.rows | j.cols | j.in_rs | j.out_rs) & 3) == 0 && ((uintptr_t)j.src & 15) == 0 &&
+                     ((uintptr_t)j.dst & (bf ? 7 : 15)) == 0;
+    if (vec) {
+        const int q = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;      // tile row / first of 4 columns
+        if (r0 + q < j.rows && c0 + c4 < j.cols) {
+            const float4 v = *reinterpret_cast<const float4*>(j.src + (r0 + q) * j.in_rs + c0 + c4);
+            tile[q][c4] = v.x; tile[q][c4 + 1] = v.y; tile[q][c4 + 2] = v.z; tile[q][c4 + 3] = v.w;
         }
+        __syncthreads();
+        float o[4];
+        int64_t orow, ocol;
+        if (j.transpose) {                              // out row = input column q, 4 input rows
+            orow = c0 + q; ocol = r0 + c4;
+            if (orow >= j.cols || ocol >= j.rows) return;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = tile[c4 + e][q];
+        } else {
+            orow = r0 + q; ocol = c0 + c4;
+            if (orow >= j.rows || ocol >= j.cols) return;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = tile[q][c4 + e];
+        }
+        const int64_t off = orow * j.out_rs + ocol;
+        if (bf) {
+            typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+            u32x2_t w;
+            w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)o[0]) |
+                   ((unsigned)__builtin_bit_cast(unsigned short, (bf16)o[1]) << 16);
+            w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)o[2]) |
+                   ((unsigned)__builtin_bit_cast(unsigned short, (bf16)o[3]) << 16);
+            *reinterpret_cast<u32x2_t*>(reinterpret_cast<bf16*>(j.dst) + off) = w;
+        } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(j.dst) + off) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        return;
+    }
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;      // 32 x 8
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t r = r0 + ty + 8 * k, c = c0 + tx;
+        tile[ty + 8 * k][tx] = (r < j.rows && c < j.cols) ? j.src[r * j.in_rs + c] : 0.f;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < COPY_TPW; ++k) {
-        if (jk[k] == -1) continue;
-        const bool scalar = jk[k] <= -2;
-        const CopyJob& j = jobs[scalar ? -2 - jk[k] : jk[k]];
-        const int64_t t = (int64_t)blockIdx.x * COPY_TPW + k;
-        const int64_t lt = t - j.tile0, tc = (j.cols + 31) / 32;
-        const int64_t r0 = (lt / tc) * 32, c0 = (lt % tc) * 32;
-        const bool bf = j.dtype == OCRK_BF16;
-        if (!scalar) {
-            float o[4];
-            int64_t orow, ocol;
-            if (j.transpose) {                          // out row = input column q, 4 input rows
-                orow = c0 + q; ocol = r0 + c4;
-                if (orow >= j.cols || ocol >= j.rows) continue;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = tile[k][c4 + e][q];
-            } else {
-                orow = r0 + q; ocol = c0 + c4;
-                if (orow >= j.rows || ocol >= j.cols) continue;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = tile[k][q][c4 + e];
-            }
-            const int64_t off = orow * j.out_rs + ocol;
-            if (bf) {
-                typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-                u32x2_t w;
-                w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)o[0]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)o[1]) << 16);
-                w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)o[2]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)o[3]) << 16);
-                *reinterpret_cast<u32x2_t*>(reinterpret_cast<bf16*>(j.dst) + off) = w;
-            } else {
-                *reinterpret_cast<float4*>(reinterpret_cast<float*>(j.dst) + off) =
-                    make_float4(o[0], o[1], o[2], o[3]);
-            }
-            continue;
+    for (int k = 0; k < 4; ++k) {
+        int64_t orow, ocol;
+        float v;
+        if (j.transpose) {                              // out row = input column
+            orow = c0 + ty + 8 * k; ocol = r0 + tx;
+            v = tile[tx][ty + 8 * k];
+            if (orow >= j.cols || ocol >= j.rows) continue;
+        } else {
+            orow = r0 + ty + 8 * k; ocol = c0 + tx;
+            v = tile[ty + 8 * k][tx];
+            if (orow >= j.rows || ocol >= j.cols) continue;
         }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            int64_t orow, ocol;
-            float x;
-            if (j.transpose) {                          // out row = input column
-                orow = c0 + ty + 8 * m; ocol = r0 + tx;
-                x = tile[k][tx][ty + 8 * m];
-                if (orow >= j.cols || ocol >= j.rows) continue;
-            } else {
-                orow = r0 + ty + 8 * m; ocol = c0 + tx;
-                x = tile[k][ty + 8 * m][tx];
-                if (orow >= j.rows || ocol >= j.cols) continue;
-            }
-            const int64_t o = orow * j.out_rs + ocol;
-            if (bf) reinterpret_cast<bf16*>(j.dst)[o] = (bf16)x;
-            else reinterpret_cast<float*>(j.dst)[o] = x;
-        }
+        const int64_t o = orow * j.out_rs + ocol;
+        if (bf) reinterpret_cast<bf16*>(j.dst)[o] = (bf16)v;
+        else reinterpret_cast<float*>(j.dst)[o] = v;
     }
 }
 
 extern "C" int ocrk_copy_batch(const void* jobs, int njobs, int64_t total_tiles, void* stream) {
     OCRK_REQUIRE(njobs >= 1 && total_tiles >= 1 && total_tiles < (1ll << 31), "ocrk_copy_batch: njobs=%d tiles=%lld",
                  njobs, (long long)total_tiles);
-    copy_batch_kernel<<<(unsigned)((total_tiles + COPY_TPW - 1) / COPY_TPW), 256, 0, ocrk::as_stream(stream)>>>(
-        (const CopyJob*)jobs, njobs, total_tiles);
+    copy_batch_kernel<<<(unsigned)total_tiles, 256, 0, ocrk::as_stream(stream)>>>((const CopyJob*)jobs, njobs);
     return ocrk::launch_status("ocrk_copy_batch");
 }
 

@@ -173,6 +173,7 @@ class Trainer:
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
         self._grads_zeroed = False                # flat_grad cleared by the last optimizer pass
+        self._unit = None
         self._status_host = None
         self._status_ev = None
         self._status_stream = None
@@ -219,7 +220,11 @@ class Trainer:
             features.register_hook(self.buckets.rnn_ready)
         logits = rnn_layers(features, seq_len, store.cfg.num_classes, store)
         loss = ctc_loss_layer(logits, label, seq_len)
-        loss.backward()
+        # d loss / d loss = 1 from a resident scalar (no fill launch per step)
+        unit = self._unit
+        if unit is None or unit.device != loss.device or unit.dtype != loss.dtype:
+            unit = self._unit = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(unit)
         return loss
 
     def reduce_gradients(self):
