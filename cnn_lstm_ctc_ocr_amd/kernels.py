@@ -632,9 +632,10 @@ def stream_wait(waiter, signaller, mode=1):
 
 
 # cross-stream ordering inside a step (the side-stream forks and joins, the status
-# copy's fork): 0 default torch events, 1 / 2 ocrk_stream_wait's modes (OCRK_FORK_EVENTS;
-# same box, 3 x 30 steps: 1 5.077-5.087, 2 5.098-5.120, 0 5.109-5.135 ms)
-FORK_MODE = int(os.environ.get("OCRK_FORK_EVENTS", "1"))
+# copy's fork): 0 default torch events, 1 / 2 ocrk_stream_wait's modes (OCRK_FORK_EVENTS).
+# Box-dependent: mode 1 5.077-5.087 vs 5.109-5.135 ms on one box, 5.038-5.054 vs
+# 5.019-5.028 (4 x 30 steps) on another -- the default stays 0
+FORK_MODE = int(os.environ.get("OCRK_FORK_EVENTS", "0"))
 
 
 def fork(waiter, signaller):
