@@ -373,6 +373,9 @@ class GraphedStep:
     def __init__(self, trainer, image, width, label, max_label_len=None, before_capture=None):
         store = trainer.store
         dev = store.device
+        if store.bn_group is not None and trainer.world_size() > 1:
+            # SyncBN's collectives sit inside the forward and backward: not captured here
+            raise NotImplementedError("GraphedStep with Trainer(sync_bn=True): run eager steps")
         self.trainer = trainer
         self.B = int(image.shape[0])
         self.image = image.detach().to(dev).clone()
