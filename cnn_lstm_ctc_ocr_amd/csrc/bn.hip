@@ -643,7 +643,16 @@ extern "C" int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, 
     return ocrk::launch_status("ocrk_bn_relu_pool_fwd");
 }
 
-static int64_t bn_bwd_blocks(int64_t items) { return std::max<int64_t>(1, std::min<int64_t>(2048, ocrk::cdiv(items, 256 * 8))); }
+// pass-1 blocks (= rows of the partial-sum slab the ordered column sums walk on the
+// critical path): at most OCRK_BN_BWD_BLOCKS (default 2048)
+static int64_t bn_bwd_blocks(int64_t items) {
+    static const int64_t cap = [] {              // thread-safe once
+        const char* e = getenv("OCRK_BN_BWD_BLOCKS");
+        const long v = e ? atol(e) : 2048;
+        return (int64_t)(v >= 64 && v <= 8192 ? v : 2048);
+    }();
+    return std::max<int64_t>(1, std::min<int64_t>(cap, ocrk::cdiv(items, 256 * 8)));
+}
 static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::cdiv(items, nb), 256) * 256; }
 
 // Window-centric pass 1 covers the path's pools (2x2/[2,2], 2x2/[2,1],
