@@ -23,12 +23,15 @@ import torch.distributed as dist
 
 from . import _lib
 from . import kernels as K
+from . import model as _model
 from .config import TRAIN
 from .model import check_feasible_host, convnet_layers, ctc_loss_layer, dense_labels, host_labels, rnn_layers
 
 
 # OCRK_ADAM_ZERO=0: keep the separate zero-gradient fill (measurement toggle)
 _ADAM_ZERO = os.environ.get("OCRK_ADAM_ZERO", "1") != "0"
+# OCRK_UNIT_SEED=0: seed the backward with torch's own ones (measurement toggle)
+_UNIT_SEED = os.environ.get("OCRK_UNIT_SEED", "1") != "0"
 
 
 class GradBuckets:
@@ -173,7 +176,6 @@ class Trainer:
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
         self._grads_zeroed = False                # flat_grad cleared by the last optimizer pass
-        self._unit = None
         self._status_host = None
         self._status_ev = None
         self._status_stream = None
@@ -220,11 +222,9 @@ class Trainer:
             features.register_hook(self.buckets.rnn_ready)
         logits = rnn_layers(features, seq_len, store.cfg.num_classes, store)
         loss = ctc_loss_layer(logits, label, seq_len)
-        # d loss / d loss = 1 from a resident scalar (no fill launch per step)
-        unit = self._unit
-        if unit is None or unit.device != loss.device or unit.dtype != loss.dtype:
-            unit = self._unit = torch.ones((), dtype=loss.dtype, device=loss.device)
-        loss.backward(unit)
+        # d loss / d loss = 1 from a resident scalar: no fill launch per step, and the
+        # CTC backward skips its x 1 pass over the logits gradient
+        loss.backward(_model.unit_seed(loss.device) if loss.dtype == torch.float32 and _UNIT_SEED else None)
         return loss
 
     def reduce_gradients(self):
