@@ -467,44 +467,90 @@ def launch_ranks(n, argv, timeout=None):
     return rc
 
 
+def _stand_in_grad(rng_seed, n):
+    """A rank's stand-in gradient: a fixed function of its seed (every rank can
+    recompute every other rank's)."""
+    return torch.from_numpy(np.random.default_rng(rng_seed).standard_normal(n).astype(np.float32))
+
+
 def selftest(args, world, rank):
-    """--selftest: the multi-rank launch / barrier / max-over-ranks / one-line
-    protocol of this script on the CPU under gloo, with a stand-in host
-    workload instead of the GPU step (tests/test_bench_launcher.py). It is not
-    a benchmark and its line says so."""
+    """--selftest: the C4 data-parallel protocol of this script on the CPU
+    under gloo (no GPU): the launch, then per step the C4 partition -- each
+    rank draws its own `--batch` crops from seed base + rank exactly as the GPU
+    step does (synthetic_batch) -- the gradient exchange of train.GradBuckets
+    over the real LSTM 512/512 ParamStore layout (the recurrent + logits bucket
+    started from the mid-backward hook, then the conv bucket), the device
+    status word OR-reduced over the ranks, and the barrier / max-over-ranks
+    timing / one-line protocol. The forward + backward is a stand-in (a
+    gradient that is a fixed function of the rank's batch), so the exchange is
+    checked exactly: every rank must hold the sum of all ranks' gradients and
+    the OR of their status bits (tests/test_bench_launcher.py). It is not a
+    benchmark and its line says so."""
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import GradBuckets, or_allreduce_status
     if world > 1:
         dist.init_process_group("gloo")
-    g = torch.ones(1 << 16)
-    x = torch.randn(128, 128)
+    B, W = args.batch, args.width
+    T = (W - 2) // 2 - 2
+    store = ParamStore(ModelConfig(cell=args.cell, rnn_sizes=RNN_SIZES[args.cell], dtype=torch.float32),
+                       device="cpu", seed=0)
+    buckets = GradBuckets(store)
+    n = store.flat_grad.numel()
+    checks = {"partition": True, "allreduce": True, "status_or": True}
+    seen = []
 
-    def step():
-        for _ in range(4):
-            torch.mm(x, x)
+    def step(i):
+        rng = np.random.default_rng(1234 + rank)                 # per-rank seed = base + rank (the GPU step's)
+        img, widths, (lab, ln) = synthetic_batch(rng, B, W, T, "cpu")
+        digest = int(img[:, 0, :8, 0].to(torch.int64).sum()) + int(ln.sum())
+        seen.append(digest)
+        g = store.flat_grad
+        g.copy_(_stand_in_grad(1234 + rank + 7919 * i, n))     # the stand-in backward's gradient
+        buckets.rnn_ready()                                      # the hook: recurrent + logits bucket
+        scale = buckets.finish() if world > 1 else 1.0           # conv bucket, then wait for both
+        word = torch.tensor([1 << (1 + rank % 6)], dtype=torch.int32)
         if world > 1:
-            dist.all_reduce(g)
-    for _ in range(args.warmup):
-        step()
+            or_allreduce_status(word)
+        return scale, word, digest
+    for i in range(args.warmup):
+        step(args.steps + i)                                     # its own stand-in gradients
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        scale, word, digest = step(i)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # exactness: the reduced gradient of the last step is the sum over ranks, the word the OR of their bits
+    want = sum(_stand_in_grad(1234 + r + 7919 * (args.steps - 1), n).double() for r in range(world))
+    checks["allreduce"] = bool(torch.allclose(store.flat_grad.double(), want, rtol=1e-5, atol=1e-5)) and \
+        abs(scale - 1.0 / world) < 1e-12
+    checks["status_or"] = int(word[0]) == int(np.bitwise_or.reduce([1 << (1 + r % 6) for r in range(world)]))
     ranks_seen = world
+    digests = [digest]
     if world > 1:
         t = torch.tensor([elapsed, 1.0], dtype=torch.float64)
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, ranks_seen = float(t[0]), int(t[1])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, digest)
+        digests = gathered
+        ok = torch.tensor([int(all(checks.values()))], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        checks = {k: bool(v) and bool(ok[0]) for k, v in checks.items()}
+    # C4's partition: distinct batches per rank, each the one its seed gives
+    checks["partition"] = len(set(digests)) == world and len(set(seen)) == 1
     if rank == 0:
         print(json.dumps({"metric": "launcher self-test (CPU stand-in step, not a benchmark)",
-                          "value": round(world * args.batch * args.steps / elapsed, 2), "unit": "items/sec",
+                          "value": round(world * B * args.steps / elapsed, 2), "unit": "items/sec",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(1e3 * elapsed / args.steps, 3), "world_size_seen": ranks_seen,
-                          "backend": "gloo", "config": {"global_batch": args.batch * world,
-                                                        "parallelism": f"dp{world}"}}), flush=True)
+                          "backend": "gloo", "checks": checks, "grad_values": n,
+                          "config": {"global_batch": B * world, "per_gpu_batch": B,
+                                     "parallelism": f"dp{world}", "seeds": f"1234 + rank (0..{world - 1})"}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 

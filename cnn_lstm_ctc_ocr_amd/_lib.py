@@ -35,6 +35,8 @@ _sz = ctypes.c_size_t
 SIGNATURES = {
     "ocrk_version": [],
     "ocrk_last_error": [],
+    "ocrk_set_option": [ctypes.c_char_p, _i64, _p],
+    "ocrk_get_option": [ctypes.c_char_p, _p],
     "ocrk_preprocess": [_p, _i64, _p, _i32, _p],
     "ocrk_status_clear": [_p, ctypes.c_uint32, _p],
     "ocrk_set_f32_gemm_mode": [_i32],

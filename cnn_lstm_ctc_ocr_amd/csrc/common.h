@@ -56,9 +56,29 @@ inline void set_dyn_lds(DeviceOnce& o, const void* kern, int bytes) {
     });
 }
 
+// Engine options (route and schedule switches kept for A/B measurement and for
+// the parity tests of alternative routes). Each starts from its OCRK_<NAME>
+// environment variable, read ONCE for the process (the first opt() call);
+// afterwards only ocrk_set_option changes it. A lookup is one relaxed atomic
+// load: no getenv on a launch path.
+enum Option : int {
+    OPT_CONV_DIRECT = 0,      // 0 implicit GEMM only, 1 (default) the Cin 32 shapes, 2 every covered shape
+    OPT_CONV_ROWS,            // 1 (default) row-walking conv kernels, 0 the chunked direct / TN engines
+    OPT_CONV_ROWS_WIDE,       // 1 (default) conv3-conv6 on the row kernels too, 0 GEMM / direct engines
+    OPT_CONV_WGRAD_BLOCKS,    // 1 (default) conv5/6 weight gradients as channel blocks, 2 conv7/8 too, 0 TN
+    OPT_LSTM_SPIN_LIMIT,      // polls before a persistent hand-off wait gives up (<= 0: 1 << 22)
+    OPT_PERSIST_LATE,         // 1 (default) late epilogue loads behind the staging DMA, 0 at the step top
+    OPT_LSTM_BWD_KSPLIT,      // 1: the K-split persistent BPTT (opt-in)
+    OPT_LSTM_BWD_PB16,        // 1: K-split partial products exchanged in bf16
+    OPT_LSTM_BWD_R16,         // 1 (default) 16-row / 64-unit BPTT members at H = 512, 0 the 32-row gather
+    OPT_CTC_LDS,              // 1 (default) CTC lattices in LDS when they fit, 0 in the global workspace
+    OPT_COUNT
+};
+int64_t opt(Option o);
+
 }  // namespace ocrk
 
-#define OCRK_REQUIRE(cond, ...)                         \
+#define OCRK_REQUIRE(cond, ...)                       \
     do {                                                \
         if (!(cond)) {                                  \
             ocrk::set_error(__VA_ARGS__);               \

@@ -551,10 +551,7 @@ int launch_direct(const bf16* x, const bf16* w, const float* bias, const bf16* m
 // OCRK_CONV_DIRECT=0: implicit GEMM only; 2: every shape the kernel covers
 // (default: the Cin = 32 / Cout = 32 shapes it was measured faster on,
 // tools/bench_conv.py -> profiles/r2_conv_layers.txt)
-int conv_direct_mode() {
-    const char* e = getenv("OCRK_CONV_DIRECT");           // read per call: tests switch it
-    return e ? atoi(e) : 1;
-}
+int conv_direct_mode() { return (int)opt(OPT_CONV_DIRECT); }
 
 // forward: y = conv(x) + bias (ReLU if relu), optional per-128-pixel-tile (sum, M2)
 int conv_direct_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,

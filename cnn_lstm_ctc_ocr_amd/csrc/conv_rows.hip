@@ -1068,33 +1068,21 @@ static int launch_dgrad_co(const void* dy, int B, int H, int W, const void* w_bw
 
 }  // namespace
 
-// OCRK_CONV_ROWS=0: the chunked direct kernel instead (read per call)
-static bool rows_enabled() {
-    const char* e = getenv("OCRK_CONV_ROWS");
-    return !(e && e[0] == '0');
-}
+// OCRK_CONV_ROWS=0: the chunked direct kernel instead
+static bool rows_enabled() { return opt(OPT_CONV_ROWS) != 0; }
 
 // OCRK_CONV_WGRAD_BLOCKS=0: conv5 / conv6 weight gradients stay on the 4-wave TN engine
-static bool rows_wgrad_blocks() {
-    const char* e = getenv("OCRK_CONV_WGRAD_BLOCKS");
-    return !(e && e[0] == '0');
-}
+static bool rows_wgrad_blocks() { return opt(OPT_CONV_WGRAD_BLOCKS) != 0; }
 
 // OCRK_CONV_WGRAD_BLOCKS=2: conv7 / conv8 as channel blocks too (else the ping-pong TN engine)
-static bool rows_wgrad_blocks_wide() {
-    const char* e = getenv("OCRK_CONV_WGRAD_BLOCKS");
-    return e && e[0] == '2';
-}
+static bool rows_wgrad_blocks_wide() { return opt(OPT_CONV_WGRAD_BLOCKS) == 2; }
 
 size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
     return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
 }
 
 // OCRK_CONV_ROWS_WIDE=0: the wider layers (conv3-conv6) stay on the GEMM / direct engines
-static bool rows_wide_enabled() {
-    const char* e = getenv("OCRK_CONV_ROWS_WIDE");
-    return !(e && e[0] == '0');
-}
+static bool rows_wide_enabled() { return opt(OPT_CONV_ROWS_WIDE) != 0; }
 
 static bool rows_fwd_wide(int cin, int cout) {
     // conv6's 128 -> 128 stays on the GEMM engine: one 8-wave workgroup spills

@@ -482,8 +482,7 @@ extern "C" int ocrk_ctc_loss(const float* logits, const int* labels, const int* 
     int R = (2 * max_label_len + 1 + 63) / 64;
     hipStream_t s = ocrk::as_stream(stream);
     const size_t lat = 3 * (size_t)T * (2 * (size_t)max_label_len + 1) * sizeof(float);
-    const char* lds_env = getenv("OCRK_CTC_LDS");         // OCRK_CTC_LDS=0: lattices in the global workspace
-    const bool in_lds = lat <= CTC_LAT_MAX && !(lds_env && lds_env[0] == '0');
+    const bool in_lds = lat <= CTC_LAT_MAX && ocrk::opt(ocrk::OPT_CTC_LDS) != 0;   // 0: lattices in the workspace
     // the softmax cache behind the lattices when it fits as well
     const size_t pbytes = (size_t)T * C * sizeof(float);
     const int pcache = in_lds && grad && lat + pbytes <= CTC_LAT_MAX;

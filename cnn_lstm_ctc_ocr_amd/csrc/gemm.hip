@@ -543,7 +543,9 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
 }
 
 // fp32 GEMMs on the bf16x3 split (mode 0, the default) or the exact f32 MFMA
-// (mode 1: ocrk_set_f32_gemm_mode, or OCRK_F32_MFMA=1 for the whole process)
+// (mode 1: ocrk_set_f32_gemm_mode, or OCRK_F32_MFMA=1 for the whole process).
+// Process-wide, not per thread: torch's autograd runs a backward's launches on
+// its own device thread, which must see the mode the training step set.
 static std::atomic<int> g_f32_mode{0};
 
 bool f32_exact_mfma() {

@@ -1203,12 +1203,9 @@ lstm_bwd_ksplit_kernel(const bf16* __restrict__ wh, void* __restrict__ px, const
     }
 }
 
-// The late-load forms (OCRK_PERSIST_LATE=0 disables them, read per launch); their
-// buffer loads address the largest operand (`bytes`) with 32-bit offsets.
-static bool persist_late(int64_t bytes) {
-    const char* e = getenv("OCRK_PERSIST_LATE");
-    return !(e && e[0] == '0') && bytes < 0x7fffffffll;
-}
+// The late-load forms (option PERSIST_LATE=0 disables them); their buffer loads
+// address the largest operand (`bytes`) with 32-bit offsets.
+static bool persist_late(int64_t bytes) { return opt(OPT_PERSIST_LATE) != 0 && bytes < 0x7fffffffll; }
 
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H) {
@@ -1300,10 +1297,7 @@ extern "C" int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* w
 // measured 5.2 (bf16 partials) / 7.0 (f32) against 4.2 us per step for the
 // gather form at B=256, H=512 -- its exchange buffer (NU x NU blocks per group,
 // 2-4 MB per XCD) does not stay in the XCD's L2 between steps.
-static bool lstm_bwd_ksplit() {
-    const char* e = getenv("OCRK_LSTM_BWD_KSPLIT");
-    return e && e[0] == '1';
-}
+static bool lstm_bwd_ksplit() { return opt(OPT_LSTM_BWD_KSPLIT) == 1; }
 
 extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
     // flag word + XCC word per workgroup (128-B aligned block), then the exchange buffer:
@@ -1316,15 +1310,17 @@ extern "C" size_t ocrk_lstm_bwd_persistent_workspace_size(int B, int H) {
 }
 
 // the 16-row / 64-unit BPTT (H = 512): default where its grid (B workgroups) is co-resident;
-// OCRK_LSTM_BWD_R16=0 keeps the 32-row gather kernel (read per call: A/B and tests)
+// option LSTM_BWD_R16=0 keeps the 32-row gather kernel (A/B and tests)
 static bool lstm_bwd_r16(int B, int H) {
-    const char* e = getenv("OCRK_LSTM_BWD_R16");
-    if ((e && e[0] == '0') || H != 512 || B % PBR || lstm_bwd_ksplit()) return false;   // flag words as the gather form
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_r16_kernel, 512, 0) != hipSuccess) return false;
-    return 2L * (B / R16_ROWS) * (H / R16_UNITS) <= (long)cus * per_cu;
+    if (opt(OPT_LSTM_BWD_R16) == 0 || H != 512 || B % PBR || lstm_bwd_ksplit()) return false;   // flag words as the gather form
+    static ocrk::DeviceOnce once;
+    static int per_cu[ocrk::kMaxDevices];
+    const int dev = ocrk::current_device();
+    ocrk::once_per_device(once, [dev] {
+        int n = 0;
+        per_cu[dev] = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lstm_bwd_r16_kernel, 512, 0) == hipSuccess ? n : 0;
+    });
+    return 2L * (B / R16_ROWS) * (H / R16_UNITS) <= (long)ocrk::cu_count() * per_cu[dev];
 }
 
 extern "C" int ocrk_lstm_bwd_persistent_slices(int B, int H) {
@@ -1368,8 +1364,7 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
     }
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (lstm_bwd_ksplit()) {
-        const char* pe = getenv("OCRK_LSTM_BWD_PB16");            // partial products exchanged in bf16
-        const bool pb16 = pe && pe[0] == '1';
+        const bool pb16 = opt(OPT_LSTM_BWD_PB16) == 1;            // partial products exchanged in bf16
 #define KSPLIT_LAUNCH(KSV, PB)                                                                                   \
         lstm_bwd_ksplit_kernel<KSV, PB><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout,  \
                                                              cprev_t, (const bf16*)acts_t, (bf16*)dG_t, cnt, err,     \

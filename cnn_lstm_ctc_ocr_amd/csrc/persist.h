@@ -164,12 +164,11 @@ __device__ __forceinline__ void group_post(gu32* flag, unsigned v, bool local) {
     if (threadIdx.x == 0) raise_flag(flag, v, local);
 }
 
-// polls before a hand-off wait gives up: OCRK_LSTM_SPIN_LIMIT (read per launch:
-// tests force tiny limits; it bounds every persistent recurrence), default 1 << 22
+// polls before a hand-off wait gives up: option LSTM_SPIN_LIMIT (tests force tiny
+// limits; it bounds every persistent recurrence), default 1 << 22
 inline unsigned recur_spin_limit() {
-    const char* e = getenv("OCRK_LSTM_SPIN_LIMIT");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (unsigned)v : (1u << 22);
+    const int64_t v = ocrk::opt(ocrk::OPT_LSTM_SPIN_LIMIT);
+    return v > 0 && v < (1ll << 32) ? (unsigned)v : (1u << 22);
 }
 
 // flag word + XCC word per workgroup, rounded to a 128-B block (the size of a

@@ -1,5 +1,7 @@
 // libocrk runtime plumbing: version, thread-local error string, launch status.
+#include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -25,11 +27,64 @@ int launch_status(const char* what) {
     return OCRK_OK;
 }
 
+// ---------------------------------------------------------------- options
+namespace {
+struct OptDef {
+    const char* name;
+    int64_t def;
+};
+constexpr OptDef kOptDefs[OPT_COUNT] = {
+    {"CONV_DIRECT", 1}, {"CONV_ROWS", 1}, {"CONV_ROWS_WIDE", 1}, {"CONV_WGRAD_BLOCKS", 1},
+    {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0}, {"LSTM_BWD_PB16", 0},
+    {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1},
+};
+std::atomic<int64_t> g_opts[OPT_COUNT];
+std::once_flag g_opts_once;
+
+void init_opts() {
+    for (int i = 0; i < OPT_COUNT; ++i) {
+        char env[64];
+        snprintf(env, sizeof(env), "OCRK_%s", kOptDefs[i].name);
+        const char* e = getenv(env);
+        g_opts[i].store(e && *e ? atoll(e) : kOptDefs[i].def, std::memory_order_relaxed);
+    }
+}
+
+int find_opt(const char* name) {
+    if (!name) return -1;
+    if (!strncmp(name, "OCRK_", 5)) name += 5;
+    for (int i = 0; i < OPT_COUNT; ++i)
+        if (!strcmp(name, kOptDefs[i].name)) return i;
+    return -1;
+}
+}  // namespace
+
+int64_t opt(Option o) {
+    std::call_once(g_opts_once, init_opts);
+    return g_opts[o].load(std::memory_order_relaxed);
+}
+
 }  // namespace ocrk
 
 extern "C" {
 
 int ocrk_version(void) { return OCRK_ABI_VERSION; }
+
+int ocrk_set_option(const char* name, int64_t value, int64_t* prev) {
+    const int i = ocrk::find_opt(name);
+    OCRK_REQUIRE(i >= 0, "ocrk_set_option: unknown option '%s'", name ? name : "(null)");
+    ocrk::opt((ocrk::Option)i);                         // defaults from the environment first
+    const int64_t old = ocrk::g_opts[i].exchange(value, std::memory_order_relaxed);
+    if (prev) *prev = old;
+    return OCRK_OK;
+}
+
+int ocrk_get_option(const char* name, int64_t* value) {
+    const int i = ocrk::find_opt(name);
+    OCRK_REQUIRE(i >= 0 && value, "ocrk_get_option: unknown option '%s' or null slot", name ? name : "(null)");
+    *value = ocrk::opt((ocrk::Option)i);
+    return OCRK_OK;
+}
 
 const char* ocrk_last_error(void) { return ocrk::g_err; }
 
@@ -88,11 +143,17 @@ int ocrk_stream_wait(void* waiter, void* signaller, int mode) {
         const unsigned fl = hipEventDisableTiming |
                             (mode == 1 ? hipEventDisableSystemFence : mode == 2 ? hipEventReleaseToDevice : 0u);
         int cur = 0;
-        hipGetDevice(&cur);
-        if (cur != dev) hipSetDevice(dev);              // created on the signaller's device
-        const hipError_t ce = hipEventCreateWithFlags(&ev, fl);
-        if (cur != dev) hipSetDevice(cur);
-        if (ce != hipSuccess) return ocrk::launch_status("ocrk_stream_wait create");
+        hipError_t ce = hipGetDevice(&cur);
+        if (ce == hipSuccess && cur != dev) ce = hipSetDevice(dev);   // created on the signaller's device
+        if (ce == hipSuccess) ce = hipEventCreateWithFlags(&ev, fl);
+        if (cur != dev) {
+            const hipError_t re = hipSetDevice(cur);
+            if (ce == hipSuccess) ce = re;
+        }
+        if (ce != hipSuccess) {
+            ocrk::set_error("ocrk_stream_wait create: %s", hipGetErrorString(ce));
+            return OCRK_ERR_HIP;
+        }
     }
     next[dev][mode] = (i + 1) % RING;
     hipError_t e = hipEventRecord(ev, ocrk::as_stream(signaller));

@@ -5,11 +5,10 @@ with the torch caching allocator, and launch on torch's current stream. They
 do no math themselves: every call lands in libocrk.so (include/ocrk.h).
 """
 import ctypes
-import os
 
 import torch
 
-from . import _lib
+from . import _lib, options
 from ._lib import ptr, call
 
 F32, BF16 = _lib.F32, _lib.BF16
@@ -310,7 +309,7 @@ def lstm_persistent_ok(B, H, dtype):
     On by default where the grid fits co-resident (B % 32 == 0, H in {256,
     512}); OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
     import os
-    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
+    if dtype != torch.bfloat16 or not options.get("LSTM_PERSISTENT"):
         return False
     key = (B, H)
     if key not in _PERSISTENT:
@@ -394,7 +393,10 @@ class f32_exact:
     """Context manager: fp32 GEMMs / convs with exact f32 MFMA products while
     inside (ocrk_set_f32_gemm_mode(1)), and the fp32 recurrence on the per-step
     f32 kernels; the default outside is the bf16x3 split (include/ocrk.h).
-    Process-wide: not for concurrent threads with different needs."""
+    Process-wide (the autograd engine runs a backward's launches on its own
+    device thread, which must see the mode): serving launched from another
+    thread while a training step is inside runs exact fp32 products as well
+    (still fp32-correct, slower); INTEGRATION.md "precision"."""
 
     def __init__(self, on=True):
         self.on = on
@@ -419,7 +421,7 @@ def lstm_f32_persistent_ok(B, H):
     in exact fp32 mode (f32_exact); OCRK_LSTM_PERSISTENT=0 selects the per-step
     fp32 kernels."""
     import os
-    if os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0" or f32_mode_exact():
+    if not options.get("LSTM_PERSISTENT") or f32_mode_exact():
         return False
     key = ("f32", B, H)
     if key not in _PERSISTENT:
@@ -479,7 +481,7 @@ def lstm_fused_x_ok(B, H, n_in, dtype, force=False):
     step's critical path), 480 vs 490 us for GEMM + loop alone and 5.865 vs
     5.847 ms for the train step (profiles/r3_fused_projection.txt)."""
     import os
-    if not force and os.environ.get("OCRK_LSTM_FUSE_X", "0") != "1":
+    if not force and options.get("LSTM_FUSE_X") != 1:
         return False
     if not lstm_persistent_ok(B, H, dtype):
         return False
@@ -542,7 +544,7 @@ def gru_persistent_ok(B, H, dtype):
     Same rule and switch as the LSTM: B % 32 == 0, H in {256, 512}, the grid
     co-resident; OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
     import os
-    if dtype != torch.bfloat16 or os.environ.get("OCRK_LSTM_PERSISTENT", "1") == "0":
+    if dtype != torch.bfloat16 or not options.get("LSTM_PERSISTENT"):
         return False
     key = (B, H)
     if key not in _GRU_PERSISTENT:
@@ -635,14 +637,20 @@ def stream_wait(waiter, signaller, mode=1):
 # copy's fork): 0 default torch events, 1 / 2 ocrk_stream_wait's modes (OCRK_FORK_EVENTS).
 # Box-dependent: mode 1 5.077-5.087 vs 5.109-5.135 ms on one box, 5.038-5.054 vs
 # 5.019-5.028 (4 x 30 steps) on another -- the default stays 0
-FORK_MODE = int(os.environ.get("OCRK_FORK_EVENTS", "0"))
+
+
+
+def fork_mode():
+    """0: torch events for stream forks; 1 / 2: ocrk_stream_wait's fence-less events (option FORK_EVENTS)."""
+    return options.get("FORK_EVENTS")
 
 
 def fork(waiter, signaller):
-    """waiter.wait_stream(signaller), through ocrk_stream_wait when FORK_MODE is
+    """waiter.wait_stream(signaller), through ocrk_stream_wait when fork_mode() is
     set and the signaller is not being captured into a graph."""
-    if FORK_MODE and not torch.cuda.is_current_stream_capturing():
-        stream_wait(waiter, signaller, FORK_MODE)
+    mode = fork_mode()
+    if mode and not torch.cuda.is_current_stream_capturing():
+        stream_wait(waiter, signaller, mode)
     else:
         waiter.wait_stream(signaller)
 

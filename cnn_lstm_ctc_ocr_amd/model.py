@@ -21,13 +21,13 @@ Structure of the launches (NHWC activations, compute dtype = store.cfg.dtype):
   then the CTC lattice.
 """
 import contextlib
-import os
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import kernels as K
+from . import options
 from .config import BN_EPS, BN_MOMENTUM, INFER, LAYER_PARAMS, POOLS, TRAIN, ModelConfig, rnn_size  # noqa: F401
 from .params import ParamStore
 
@@ -120,7 +120,7 @@ class _ConvBlock(torch.autograd.Function):
         # bias-gradient reductions (conv bias in front of the BN, and the odd conv's
         # bias from the data-gradient GEMM's tile column sums) go to the side stream
         # with the weight gradients, off the main stream's dependent chain
-        late = [] if _side_enabled("OCRK_CONV_SIDE") else None
+        late = [] if _side_enabled("CONV_SIDE") else None
         dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                 POOLS[even], dp_time_major=(k == 4),
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
@@ -220,14 +220,14 @@ class side_work:
 
     def __enter__(self):
         dev = self.store.device
-        if os.environ.get("OCRK_SIDE_STREAM", "1") == "0":        # measurement toggle
+        if not options.get("SIDE_STREAM"):                          # measurement toggle
             self.side = None
             return self
         side = _SIDE_STREAMS.get((dev, self.lane))
         if side is None:
             side = _SIDE_STREAMS[(dev, self.lane)] = torch.cuda.Stream(device=dev)
         self.side = side
-        # with K.FORK_MODE: the fork without the system-scope release of a default
+        # with K.fork_mode(): the fork without the system-scope release of a default
         # event record (a ~6 us bubble on the main stream per fork)
         K.fork(side, torch.cuda.current_stream(dev))
         self.ctx = torch.cuda.stream(side)
@@ -237,8 +237,9 @@ class side_work:
     def __exit__(self, *exc):
         if self.side is None:
             return False
-        if K.FORK_MODE and not torch.cuda.is_current_stream_capturing():
-            done = K.StreamMark(self.side, K.FORK_MODE)
+        mode = K.fork_mode()
+        if mode and not torch.cuda.is_current_stream_capturing():
+            done = K.StreamMark(self.side, mode)
         else:
             done = torch.cuda.Event()
             done.record(self.side)
@@ -247,10 +248,6 @@ class side_work:
             t.record_stream(self.side)
         self.store.pending.append(done)
         return False
-
-
-_DEFER_DWX = os.environ.get("OCRK_DEFER_DWX", "0") == "1"
-_DX_FIRST = os.environ.get("OCRK_DX_FIRST", "0") == "1"
 
 
 def _run_deferred(store):
@@ -265,10 +262,9 @@ def _run_deferred(store):
 
 def _side_enabled(var):
     """Deferred bias reductions go to the side stream unless it is off
-    (OCRK_SIDE_STREAM=0 / `var`=0); opt-in OCRK_DEFER_BIAS=1 (measured slower: 5.95 vs
+    (options SIDE_STREAM=0 / `var`=0); opt-in DEFER_BIAS=1 (measured slower: 5.95 vs
     5.80-5.90 ms per step, the side stream being the busier one in the conv backward)."""
-    return os.environ.get("OCRK_SIDE_STREAM", "1") != "0" and os.environ.get(var, "1") != "0" and \
-        os.environ.get("OCRK_DEFER_BIAS", "0") == "1"
+    return bool(options.get("SIDE_STREAM") and options.get(var) and options.get("DEFER_BIAS") == 1)
 
 
 def _issue(store, late):
@@ -284,8 +280,8 @@ def _issue(store, late):
 
 def _conv_side(store, *tensors):
     """Conv weight gradients on the side stream, overlapping the main stream's
-    data-gradient GEMMs and BN backward (OCRK_CONV_SIDE=0: issue them inline)."""
-    if os.environ.get("OCRK_CONV_SIDE", "1") == "0":
+    data-gradient GEMMs and BN backward (option CONV_SIDE=0: issue them inline)."""
+    if not options.get("CONV_SIDE"):
         return contextlib.nullcontext()
     return side_work(store, *tensors)
 
@@ -321,15 +317,15 @@ class _BiLSTM(torch.autograd.Function):
             dout = K.cast(dout, dt)
         _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
         # [T,B,2,4H]; the bias gradient (both directions) formed in the BPTT loop
-        late = [] if _side_enabled("OCRK_SIDE_STREAM") else None
+        late = [] if _side_enabled("SIDE_STREAM") else None
         dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer),
                         defer=late)
         R = T * B
         dx = None
-        # the lowest layer's data gradient first (OCRK_DX_FIRST=1): the side stream's
+        # the lowest layer's data gradient first (option DX_FIRST=1): the side stream's
         # weight-gradient GEMMs start behind it instead of taking the CUs it needs
         # (it gates the whole conv-tower backward); upper layers keep dx beside dW_h
-        dx_first = _DX_FIRST and layer == 1 and ctx.needs_input_grad[0]
+        dx_first = options.get("DX_FIRST") == 1 and layer == 1 and ctx.needs_input_grad[0]
         if dx_first:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
         _run_deferred(store)                                 # an upper layer's dW_x, now behind this BPTT
@@ -350,7 +346,7 @@ class _BiLSTM(torch.autograd.Function):
                 K.gemm(hprev.view(R, 2 * H), dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G4, K=R,
                        lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4, stride_c=sk,
                        splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
-                if layer > 1 and _DEFER_DWX and ctx.needs_input_grad[0]:
+                if layer > 1 and options.get("DEFER_DWX") == 1 and ctx.needs_input_grad[0]:
                     store.deferred.append((dw_x, (x, dG)))   # issued behind the next BPTT (fewer CUs held)
                 else:
                     dw_x()
@@ -393,7 +389,7 @@ class _BiGRU(torch.autograd.Function):
             dout = K.cast(dout, dt)
         _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt)
         # [T,B,2,3H]; the [gates | candidate] bias gradients formed in the BPTT loop
-        late = [] if _side_enabled("OCRK_SIDE_STREAM") else None
+        late = [] if _side_enabled("SIDE_STREAM") else None
         dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=store.gru_bias_cat_grad(layer),
                        defer=late)
         pre = f"rnn/bdrnn{layer}"
@@ -441,7 +437,6 @@ class _BiGRU(torch.autograd.Function):
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
 
-_TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
 # the lowest layer's weight gradients run beside the conv backward's main-stream
 # kernels (BN backward: 175-212 VGPRs), which cannot share a CU with a 256 x 256
 # TN item (2 waves x 216 VGPRs per SIMD): a cap leaves them CUs. Same-box
@@ -449,19 +444,16 @@ _TN_ITEMS = int(os.environ.get("OCRK_TN_ITEMS", "256"))
 # 5.286-5.288 ms per step at 192; 160: 5.215-5.225, 176: 5.26, 224: 5.25. With the
 # 16-row BPTT and the channel-block conv weight gradients (round 4, 7 same-box
 # pairs): 160 5.062-5.091 vs 192 5.081-5.099 ms, 128 5.069-5.094, 224 5.098-5.111
-_TN_ITEMS_L1 = int(os.environ.get("OCRK_TN_ITEMS_L1", "160"))
 
 
 # an upper layer's dW_x is queued behind the lower BPTT and meets the lower layer's
 # data gradient when that BPTT ends (OCRK_TN_ITEMS_LATE: its own cap; 192: 5.28,
 # 128: 5.34 vs 5.27-5.30 ms at 256)
-_TN_ITEMS_LATE = int(os.environ.get("OCRK_TN_ITEMS_LATE", str(_TN_ITEMS)))
-
-
+# (options TN_ITEMS_L1 = 160, TN_ITEMS = 256, TN_ITEMS_LATE = TN_ITEMS)
 def _tn_items(layer, late=False):
     if layer == 1:
-        return _TN_ITEMS_L1
-    return _TN_ITEMS_LATE if late else _TN_ITEMS
+        return options.get("TN_ITEMS_L1")
+    return options.get("TN_ITEMS_LATE" if late else "TN_ITEMS")
 
 
 def _splits(M, N, Kdim, batch=1, items=None):
@@ -475,7 +467,7 @@ def _splits(M, N, Kdim, batch=1, items=None):
     5.374-5.402 vs 5.416-5.426 ms, 320 / 384 / 512 5.45 / 5.44-5.48 / 5.56-5.58)."""
     if M >= 256 and N >= 256:
         tiles = -(-M // 256) * -(-N // 256) * batch
-        return int(max(1, min((items or _TN_ITEMS) // tiles, Kdim // 1024)))      # <= 256 items: one round on the chip
+        return int(max(1, min((items or options.get("TN_ITEMS")) // tiles, Kdim // 1024)))      # <= 256 items: one round on the chip
     tiles = -(-M // 128) * -(-N // 128) * batch
     return int(max(1, min(-(-512 // tiles), Kdim // 2048)))
 
@@ -563,24 +555,42 @@ class _CTCLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
-        if g.data_ptr() in _UNIT_SEEDS and g.dtype == torch.float32:
+        if _UNIT_ARMED[0] and g.data_ptr() in _UNIT_SEEDS and g.dtype == torch.float32:
             return grad, None, None, None          # d loss / d loss = 1 (Trainer's resident seed): x 1 is exact
         return K.mul_scalar_(grad, g.to(torch.float32).contiguous()), None, None, None
 
 
 # resident scalar 1.0 tensors (one per device, held here for the process so their
-# addresses stay theirs) that a training loop seeds loss.backward with
+# addresses stay theirs) that the Trainer seeds loss.backward with; private, and
+# trusted by _CTCLoss.backward only while unit_backward() is armed
 _UNIT_SEEDS = {}
 _UNIT_BY_DEVICE = {}
+_UNIT_ARMED = [False]
 
 
-def unit_seed(device):
-    """The resident f32 scalar 1.0 of `device` (never written): loss.backward(unit_seed(dev))."""
+def _unit_seed(device):
     t = _UNIT_BY_DEVICE.get(device)
     if t is None:
         t = _UNIT_BY_DEVICE[device] = torch.ones((), dtype=torch.float32, device=device)
         _UNIT_SEEDS[t.data_ptr()] = t
     return t
+
+
+def unit_backward(loss):
+    """loss.backward() seeded from the device's resident f32 1.0: no fill launch,
+    and the CTC backward skips its x 1 pass over the logits gradient. The skip is
+    armed only for this call (backward is synchronous), and only for that tensor."""
+    seed = _unit_seed(loss.device)
+    if _UNIT_CHECK and seed.item() != 1.0:
+        raise RuntimeError("the resident backward seed was overwritten")
+    _UNIT_ARMED[0] = True
+    try:
+        loss.backward(seed)
+    finally:
+        _UNIT_ARMED[0] = False
+
+
+_UNIT_CHECK = False          # tests: verify the seed (a device sync) before every use
 
 
 def dense_labels(sequence_labels, batch, device):

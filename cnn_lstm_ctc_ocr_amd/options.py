@@ -1,0 +1,94 @@
+"""Engine options: the route and schedule switches kept for A/B measurement and
+for the parity tests of alternative routes (no reference counterpart).
+
+Every option starts from its ``OCRK_<NAME>`` environment variable, read ONCE:
+the host-side ones here at import, the kernel-side ones by libocrk at its first
+launch (``ocrk_get_option`` / ``ocrk_set_option``, include/ocrk.h). After that
+only ``set()`` / ``override()`` change them, so no op reads the environment on
+its launch path. ``override`` is what tests use to run an alternative route:
+
+    with options.override(LSTM_BWD_R16=0):
+        ...                                  # the 32-row gather BPTT
+"""
+import contextlib
+import os
+
+# host-side options (this package) -> default
+_HOST_DEFAULTS = {
+    "LSTM_PERSISTENT": 1,     # 0: per-step recurrent kernels instead of the persistent loops
+    "LSTM_FUSE_X": 0,         # 1: first-layer projection inside the persistent forward (opt-in)
+    "BATCHED_IMAGES": 1,      # 0: weight images rebuilt by per-layout copies instead of one batched launch
+    "SIDE_STREAM": 1,         # 0: weight gradients inline on the main stream
+    "CONV_SIDE": 1,           # 0: conv weight gradients inline
+    "DEFER_BIAS": 0,          # 1: bias reductions on their own stream (measured slower)
+    "DEFER_DWX": 0,           # 1: an upper layer's dW_x behind the lower BPTT (measured no gain)
+    "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
+    "TN_ITEMS": 256,          # workgroup cap of the recurrent weight-gradient launches
+    "TN_ITEMS_L1": 160,       # the same for the first layer (beside the conv backward)
+    "TN_ITEMS_LATE": 0,       # deferred dW_x cap (0: TN_ITEMS)
+    "ADAM_ZERO": 1,           # 0: separate gradient fill instead of the in-Adam zeroing
+    "UNIT_SEED": 1,           # 0: backward seeded with torch's ones instead of the resident 1.0
+    "FORK_EVENTS": 0,         # 1 / 2: stream forks through ocrk_stream_wait's fence-less events
+    "SIDE_CU_MASK": 0,        # > 0: the weight-gradient side stream restricted to this many CUs
+}
+# kernel-side options (libocrk's registry, csrc/common.h)
+KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOCKS", "LSTM_SPIN_LIMIT",
+                  "PERSIST_LATE", "LSTM_BWD_KSPLIT", "LSTM_BWD_PB16", "LSTM_BWD_R16", "CTC_LDS")
+
+
+def _env_int(name, default):
+    v = os.environ.get("OCRK_" + name)
+    if v is None or v == "":
+        return default
+    try:
+        return int(v)
+    except ValueError:
+        raise ValueError(f"OCRK_{name}={v!r}: an integer is expected") from None
+
+
+_HOST = {k: _env_int(k, d) for k, d in _HOST_DEFAULTS.items()}
+if not _HOST["TN_ITEMS_LATE"]:
+    _HOST["TN_ITEMS_LATE"] = _HOST["TN_ITEMS"]
+
+
+def get(name):
+    """Current value of an option (host-side or kernel-side)."""
+    if name in _HOST:
+        return _HOST[name]
+    if name in KERNEL_OPTIONS:
+        import ctypes
+
+        from . import _lib
+        v = ctypes.c_int64()
+        _lib.call("ocrk_get_option", name.encode(), ctypes.byref(v))
+        return v.value
+    raise KeyError(f"unknown option {name!r}")
+
+
+def set(name, value):  # noqa: A001  (module-level setter, options.set)
+    """Set an option; returns the previous value."""
+    value = int(value)
+    if name in _HOST:
+        prev, _HOST[name] = _HOST[name], value
+        return prev
+    if name in KERNEL_OPTIONS:
+        import ctypes
+
+        from . import _lib
+        prev = ctypes.c_int64()
+        _lib.call("ocrk_set_option", name.encode(), value, ctypes.byref(prev))
+        return prev.value
+    raise KeyError(f"unknown option {name!r}")
+
+
+@contextlib.contextmanager
+def override(**values):
+    """Temporarily set options (restored on exit, in reverse order)."""
+    prev = []
+    try:
+        for k, v in values.items():
+            prev.append((k, set(k, v)))
+        yield
+    finally:
+        for k, v in reversed(prev):
+            set(k, v)

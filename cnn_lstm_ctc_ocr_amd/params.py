@@ -9,12 +9,12 @@ tensors are views. The compute-dtype weight images the kernels read (GEMM
 layouts, bf16 casts) are derived from the master copy once per parameter
 version (see `images()`).
 """
-import os
 
 import numpy as np
 import torch
 
 from . import kernels as K
+from . import options
 from .config import LAYER_PARAMS, ModelConfig
 
 _ALIGN = 64  # elements (256 B): every view starts 16-B aligned for vector loads
@@ -209,7 +209,7 @@ class ParamStore:
         return img
 
     def _plan_for(self, key):
-        if self.device.type != "cuda" or os.environ.get("OCRK_BATCHED_IMAGES", "1") == "0":
+        if self.device.type != "cuda" or not options.get("BATCHED_IMAGES"):
             return None
         dtype = key[-1]
         if dtype != self.cfg.dtype:

@@ -15,7 +15,6 @@ unless Trainer(sync_bn=True).
 """
 import collections
 import math
-import os
 import time
 
 import torch
@@ -23,15 +22,12 @@ import torch.distributed as dist
 
 from . import _lib
 from . import kernels as K
+from . import options
 from . import model as _model
 from .config import TRAIN
 from .model import check_feasible_host, convnet_layers, ctc_loss_layer, dense_labels, host_labels, rnn_layers
 
 
-# OCRK_ADAM_ZERO=0: keep the separate zero-gradient fill (measurement toggle)
-_ADAM_ZERO = os.environ.get("OCRK_ADAM_ZERO", "1") != "0"
-# OCRK_UNIT_SEED=0: seed the backward with torch's own ones (measurement toggle)
-_UNIT_SEED = os.environ.get("OCRK_UNIT_SEED", "1") != "0"
 
 
 class GradBuckets:
@@ -160,7 +156,7 @@ class Trainer:
         ranks compute the single-device reference's step on the union of their
         batches; off (the default) they stay per rank."""
         self.store = store
-        store.bn_group = (process_group if process_group is not None else dist.group.WORLD) if sync_bn else None
+        self.sync_bn = bool(sync_bn)               # the group is resolved at each step (_bn_group)
         self.summary = summary
         self.summary_every = max(1, int(summary_every))
         self._summary_mark = None
@@ -192,6 +188,14 @@ class Trainer:
             e = math.floor(e)
         return self.base_lr * self.decay_rate ** e
 
+    def _bn_group(self):
+        """SyncBN's process group, resolved when a step runs (so a Trainer built
+        before init_process_group still synchronises): None without sync_bn or
+        outside data parallelism (one process: its statistics are the global ones)."""
+        if not self.sync_bn or not (dist.is_available() and dist.is_initialized()):
+            return None
+        return self.group if self.group is not None else dist.group.WORLD
+
     def world_size(self):
         if dist.is_available() and dist.is_initialized():
             return dist.get_world_size(self.group)
@@ -209,6 +213,16 @@ class Trainer:
 
     def _loss_and_grads(self, image, width, label):
         store = self.store
+        # the store is shared (serving, other trainers): this Trainer's SyncBN
+        # setting holds for its own forward + backward only
+        prev_group, store.bn_group = store.bn_group, self._bn_group()
+        try:
+            return self._forward_backward(image, width, label)
+        finally:
+            store.bn_group = prev_group
+
+    def _forward_backward(self, image, width, label):
+        store = self.store
         if host_labels(label) and not (isinstance(width, torch.Tensor) and width.is_cuda):
             check_feasible_host(label, width)
         if self._grads_zeroed and not (store.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
@@ -224,7 +238,10 @@ class Trainer:
         loss = ctc_loss_layer(logits, label, seq_len)
         # d loss / d loss = 1 from a resident scalar: no fill launch per step, and the
         # CTC backward skips its x 1 pass over the logits gradient
-        loss.backward(_model.unit_seed(loss.device) if loss.dtype == torch.float32 and _UNIT_SEED else None)
+        if loss.dtype == torch.float32 and options.get("UNIT_SEED"):
+            _model.unit_backward(loss)
+        else:
+            loss.backward()
         return loss
 
     def reduce_gradients(self):
@@ -240,11 +257,12 @@ class Trainer:
         t = self.global_step + 1
         lr = self.learning_rate()
         lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+        zero = bool(options.get("ADAM_ZERO")) and store.device.type == "cuda"
         # the update clears the gradient as it reads it: the next loss_and_grads skips its fill
         # (a 4-byte-per-parameter pass at the top of the step)
         K.adam_(store.flat, store.flat_grad, self.m, self.v, lr_t, self.beta1, self.beta2, self.eps,
-                grad_scale=grad_scale, zero_grad=_ADAM_ZERO and store.device.type == "cuda")
-        self._grads_zeroed = _ADAM_ZERO and store.device.type == "cuda"
+                grad_scale=grad_scale, zero_grad=zero)
+        self._grads_zeroed = zero
         store.bump()
         self.global_step += 1
 
@@ -269,6 +287,8 @@ class Trainer:
         time once the writer's copies have landed (no sync in the loop)."""
         if self.summary is None:
             return
+        if self._summary_mark is not None and self.global_step % self.summary_every:
+            return                                # events only at the marks (a record costs ~6 us)
         dev = self.store.device
         if dev.type == "cuda":
             now = torch.cuda.Event(enable_timing=True)
@@ -373,7 +393,7 @@ class GraphedStep:
     def __init__(self, trainer, image, width, label, max_label_len=None, before_capture=None):
         store = trainer.store
         dev = store.device
-        if store.bn_group is not None and trainer.world_size() > 1:
+        if trainer._bn_group() is not None and trainer.world_size() > 1:
             # SyncBN's collectives sit inside the forward and backward: not captured here
             raise NotImplementedError("GraphedStep with Trainer(sync_bn=True): run eager steps")
         self.trainer = trainer

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 4
+#define OCRK_ABI_VERSION 5
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -43,7 +43,10 @@ enum ocrk_status {
 enum ocrk_dtype { OCRK_F32 = 0, OCRK_BF16 = 1 };
 
 /* How OCRK_F32 operands are multiplied by every GEMM / implicit-GEMM conv entry point
- * (process-wide; returns the previous mode or an error code):
+ * (process-wide -- torch's autograd issues a backward's launches from its own device
+ * thread, so a per-thread mode would miss them; a process that trains in fp32 and
+ * serves at the same time must serialise the two; returns the previous
+ * mode or an error code):
  *   0 (default) "bf16x3": each fp32 operand split into bf16 hi + lo and a product taken
  *     as ah.bh + ah.bl + al.bh on the bf16 MFMA, f32 accumulation (~2^-16 relative per
  *     product): the fp32 serving path (server.py:78-145 runs float32), logits within
@@ -79,6 +82,17 @@ int ocrk_status_clear(unsigned* status_word, uint32_t bits, void* stream);
 
 int ocrk_version(void);
 const char* ocrk_last_error(void);
+
+/* Engine options: route / schedule switches kept for A/B measurement and for the
+ * parity tests of alternative routes (no reference counterpart). Each starts from
+ * its OCRK_<NAME> environment variable, read once per process; afterwards only
+ * ocrk_set_option changes it (process-wide, takes effect at the next launch; the
+ * "OCRK_" prefix is optional in `name`). Names: CONV_DIRECT, CONV_ROWS,
+ * CONV_ROWS_WIDE, CONV_WGRAD_BLOCKS, LSTM_SPIN_LIMIT, PERSIST_LATE,
+ * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS (meanings in
+ * csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
+int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
+int ocrk_get_option(const char* name, int64_t* value);
 
 /* a1 -- validate._preprocess_image (src/weinman/validate.py:56-68):
  * out[i] = float32(in[i]) * float32(1/255) - 0.5, n elements. */

@@ -73,11 +73,17 @@ class TorchRef:
         self.seq_len = None
 
     def forward(self, img_u8, training=True, widths=None):
-        """img_u8 uint8 [B, 32, W, 1] -> logits [T, B, 96]. widths ([B] true
-        crop widths): the recurrence is masked by seq_len_from_width(widths)
-        (self.seq_len holds it afterwards), else every row runs all T steps."""
+        """img_u8 uint8 [B, 32, W, 1] -> logits [T, B, 96]; a floating-point
+        image is taken as already preprocessed (the training input pipeline's
+        float32 batches, mjsynth.py:185-194: first row duplicated, 0.0 dynamic
+        padding). widths ([B] true crop widths): the recurrence is masked by
+        seq_len_from_width(widths) (self.seq_len holds it afterwards), else every
+        row runs all T steps."""
         p = self.p
-        x = img_u8.permute(0, 3, 1, 2).float() * (1.0 / 255.0) - 0.5          # NCHW, float32 as TF
+        if img_u8.dtype == torch.uint8:
+            x = img_u8.permute(0, 3, 1, 2).float() * (1.0 / 255.0) - 0.5      # NCHW, float32 as TF
+        else:
+            x = img_u8.permute(0, 3, 1, 2).float()
         x = x.to(self.dtype)
         q = self.q
         for name, cin, cout, pad, bn in LAYERS:

@@ -27,6 +27,24 @@ def test_gpus_2_spawns_two_ranks_and_one_line():
     assert res["n_gpus"] == 2 and res["world_size_seen"] == 2
     assert res["config"]["global_batch"] == 512 and res["config"]["parallelism"] == "dp2"
     assert res["steps"] == 3
+    assert res["checks"] == {"partition": True, "allreduce": True, "status_or": True}, res["checks"]
+
+
+def test_c4_partition_world_8():
+    """C4 (BASELINE configs[3]: 8 ranks x 256 crops) rehearsed on the CPU: the
+    launcher starts 8 gloo ranks, each draws its 256 crops from seed 1234 +
+    rank, the GradBuckets exchange over the LSTM 512/512 ParamStore layout
+    leaves every rank the sum of all 8 gradients (Adam's scale 1/8), the status
+    word is OR-reduced, and rank 0 prints one line with the max-over-ranks time."""
+    r = _run("--gpus", "8", "--selftest", "--steps", "2", "--warmup", "1", "--batch", "256")
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 8 and res["world_size_seen"] == 8
+    assert res["config"]["global_batch"] == 2048 and res["config"]["parallelism"] == "dp8"
+    assert res["checks"] == {"partition": True, "allreduce": True, "status_or": True}, res["checks"]
+    assert res["grad_values"] > 10_000_000                  # the whole LSTM 512/512 flat gradient
 
 
 def test_single_rank_default_is_unchanged():

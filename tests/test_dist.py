@@ -208,3 +208,32 @@ def test_sync_bn_protocol_matches_the_union_batch():
         np.testing.assert_allclose(mu_r, mean, rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(var_r, var, rtol=1e-12)
         np.testing.assert_allclose(dx_r, dx[rows[r]:rows[r + 1]], rtol=1e-10, atol=1e-12)
+
+
+def _syncbn_group_worker(rank, world, port, out):
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(32, 32), dtype=torch.float32), device="cpu", seed=1)
+    tr = Trainer(store, sync_bn=True)           # built BEFORE the process group exists
+    before = tr._bn_group()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    after = tr._bn_group()
+    other = Trainer(store)                      # a second trainer on the same (shared) store
+    out[rank] = (before is None, after is dist.group.WORLD, other._bn_group() is None,
+                 tr._bn_group() is dist.group.WORLD, store.bn_group is None)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sync_bn_group_resolved_when_the_step_runs():
+    """Trainer(sync_bn=True) built before init_process_group must
+    still synchronise once the group exists (the group is resolved per step,
+    not captured at construction), and a later Trainer on the same ParamStore
+    must not switch it off (the setting lives on the Trainer; the store only
+    carries it for the duration of that Trainer's own forward + backward)."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_syncbn_group_worker, args=(2, port, out), nprocs=2, join=True)
+    assert out[0] == out[1] == (True, True, True, True, True)

@@ -42,13 +42,13 @@ BF16_OUT = 4e-3
 @pytest.mark.parametrize("B,H,W,cin,cout", [(4, 30, 254, 32, 32), (4, 15, 127, 32, 64), (4, 15, 127, 64, 64),
                                              (4, 7, 126, 64, 128), (8, 3, 125, 128, 256), (16, 3, 125, 256, 256)])
 @pytest.mark.parametrize("direct", ["1", "2"])
-def test_bf16_conv_engines_at_layer_shapes(cuda, monkeypatch, B, H, W, cin, cout, direct):
+def test_bf16_conv_engines_at_layer_shapes(cuda, ocrk_opts, B, H, W, cin, cout, direct):
     """conv2..conv5 shapes run the direct kernel (conv_direct.hip) forward and
     backward-data where it is routed (OCRK_CONV_DIRECT=1, the default: Cin 32
     or dgrad output 32) or wherever it covers the shape (=2), conv8 the
     implicit GEMM; ragged tails (B*H*W not a multiple of the 128-pixel tile)."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    monkeypatch.setenv("OCRK_CONV_DIRECT", direct)
+    ocrk_opts("CONV_DIRECT", int(direct))
     rng = np.random.default_rng(cin * 7 + W)
     x = _bf(rng.standard_normal((B, H, W, cin)))
     w = _bf(rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin))

@@ -15,10 +15,10 @@ from oracle import ref_graph as G
 pytestmark = pytest.mark.gpu
 
 
-def _both(monkeypatch, fn):
-    monkeypatch.setenv("OCRK_LSTM_PERSISTENT", "0")
+def _both(ocrk_opts, fn):
+    ocrk_opts("LSTM_PERSISTENT", 0)
     step = fn()
-    monkeypatch.setenv("OCRK_LSTM_PERSISTENT", "1")
+    ocrk_opts("LSTM_PERSISTENT", 1)
     pers = fn()
     torch.cuda.synchronize()
     return step, pers
@@ -29,7 +29,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("T,B,n_in,H", [(11, 64, 32, 256), (125, 256, 256, 512), (125, 256, 1024, 256)])
-def test_gru_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch, T, B, n_in, H):
+def test_gru_persistent_matches_step_kernels_and_oracle(cuda, ocrk_opts, T, B, n_in, H):
     from cnn_lstm_ctc_ocr_amd import kernels as K
     rng = np.random.default_rng(11 + H + n_in)
     bf = lambda a: torch.from_numpy(np.asarray(a, np.float32)).bfloat16().float().numpy()   # noqa: E731
@@ -58,7 +58,7 @@ def test_gru_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch, T, B,
     seq_d = dev(seq)
     assert K.gru_persistent_ok(B, H, torch.bfloat16)
     K.status_word(cuda).zero_()
-    step, pers = _both(monkeypatch, lambda: K.gru_fwd(gx, whgT, whcT, seq_d, T, B, H, torch.bfloat16))
+    step, pers = _both(ocrk_opts, lambda: K.gru_fwd(gx, whgT, whcT, seq_d, T, B, H, torch.bfloat16))
     assert K.read_status(cuda) == 0
     # both orders feed h back in bf16 and drift apart by a few bf16 ulps per step; the oracle bounds both
     for a, b in zip(step, pers):
@@ -71,7 +71,7 @@ def test_gru_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch, T, B,
     dout_np = bf(rng.standard_normal(ref.shape))
     dout = dev(dout_np).bfloat16()
     _, hprev, _rh, acts = pers
-    dstep, dpers = _both(monkeypatch, lambda: K.gru_bwd(whg, whc, seq_d, dout, hprev, acts, T, B, H))
+    dstep, dpers = _both(ocrk_opts, lambda: K.gru_bwd(whg, whc, seq_d, dout, hprev, acts, T, B, H))
     assert K.read_status(cuda) == 0
     scale = dstep.float().abs().max().item()
     assert (dstep.float() - dpers.float()).abs().max().item() < 3e-2 * max(scale, 1e-6)
@@ -93,7 +93,7 @@ def test_gru_persistent_matches_step_kernels_and_oracle(cuda, monkeypatch, T, B,
     assert max(errs.values()) < 2e-2, errs
 
 
-def test_gru_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
+def test_gru_persistent_timeout_sets_status_and_raises(cuda, ocrk_opts):
     """A hand-off wait that gives up (spin limit forced to 1 poll) ORs its bit
     into the status word, the launch still completes, the host raises."""
     from cnn_lstm_ctc_ocr_amd import _lib
@@ -106,10 +106,10 @@ def test_gru_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
     seq = torch.full((B,), T, dtype=torch.int32, device=cuda)
     assert K.gru_persistent_ok(B, H, torch.bfloat16)
     K.status_word(cuda).zero_()
-    monkeypatch.setenv("OCRK_LSTM_SPIN_LIMIT", "1")
+    ocrk_opts("LSTM_SPIN_LIMIT", 1)
     K.gru_fwd(gx, whgT, whcT, seq, T, B, H, torch.bfloat16)
     torch.cuda.synchronize()
-    monkeypatch.delenv("OCRK_LSTM_SPIN_LIMIT")
+    ocrk_opts.reset("LSTM_SPIN_LIMIT")
     with pytest.raises(_lib.DeviceError):
         K.check_status(cuda)
     K.gru_fwd(gx, whgT, whcT, seq, T, B, H, torch.bfloat16)

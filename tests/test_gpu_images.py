@@ -22,14 +22,14 @@ def _all_images(store, dtype):
 
 @pytest.mark.parametrize("cell,sizes", [("lstm", (512, 512)), ("gru", (512, 256))])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_batched_images_equal_the_per_image_builders(cuda, monkeypatch, cell, sizes, dtype):
+def test_batched_images_equal_the_per_image_builders(cuda, ocrk_opts, cell, sizes, dtype):
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
     store = ParamStore(ModelConfig(cell=cell, rnn_sizes=sizes, dtype=dtype), device=cuda, seed=7)
     for rnd in range(2):
-        monkeypatch.setenv("OCRK_BATCHED_IMAGES", "1")
+        ocrk_opts("BATCHED_IMAGES", 1)
         batched = _all_images(store, dtype)
         assert store._plan_fresh                          # the batched launch made them
-        monkeypatch.setenv("OCRK_BATCHED_IMAGES", "0")
+        ocrk_opts("BATCHED_IMAGES", 0)
         store._images.clear()
         built = _all_images(store, dtype)
         torch.cuda.synchronize()
@@ -42,7 +42,7 @@ def test_batched_images_equal_the_per_image_builders(cuda, monkeypatch, cell, si
 
 
 @pytest.mark.parametrize("mode", [1, 2])
-def test_side_stream_fork_modes_give_the_same_step(cuda, monkeypatch, mode):
+def test_side_stream_fork_modes_give_the_same_step(cuda, ocrk_opts, mode):
     """The side-stream fork through ocrk_stream_wait (events without the
     system-scope release) orders the weight-gradient work exactly as the
     default torch event: the same gradient bits (every kernel reduces in a
@@ -55,7 +55,7 @@ def test_side_stream_fork_modes_give_the_same_step(cuda, monkeypatch, mode):
     labels = [list(rng.integers(0, 95, int(rng.integers(2, 9)))) for _ in range(64)]
     grads = []
     for m in (0, mode):
-        monkeypatch.setattr(K, "FORK_MODE", m)
+        ocrk_opts("FORK_EVENTS", m)
         store = ParamStore(ModelConfig(dtype=torch.bfloat16), device=cuda, seed=2)
         tr = Trainer(store)
         tr.loss_and_grads(img, np.full(64, 128, np.int32), labels)

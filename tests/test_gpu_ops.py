@@ -348,7 +348,7 @@ def test_gemm_weight_grad_form_bf16(cuda):
 @pytest.mark.parametrize("B,H,W,C,CO", [(6, 30, 254, 32, 32), (5, 15, 127, 32, 64), (5, 15, 127, 64, 64),
                                         (3, 4, 9, 64, 64), (3, 7, 126, 64, 128), (3, 7, 126, 128, 128),
                                         (2, 3, 9, 128, 128), (3, 3, 125, 128, 256), (2, 3, 125, 256, 256)])
-def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
+def test_conv2_wgrad_rows_matches(cuda, ocrk_opts, B, H, W, C, CO):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(5)
     x = torch.randn(B, H, W, C, device=cuda, generator=g).bfloat16()
@@ -357,9 +357,9 @@ def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
                                      dy.double().permute(0, 3, 1, 2).transpose(0, 1), padding=1)  # [ci][co][3][3]
     ref = ref.permute(2, 3, 0, 1).contiguous()                                                # HWIO
     outs = []
-    monkeypatch.setenv("OCRK_CONV_WGRAD_BLOCKS", "2")           # conv7 / conv8 blocks too (opt-in)
+    ocrk_opts("CONV_WGRAD_BLOCKS", 2)           # conv7 / conv8 blocks too (opt-in)
     for mode in ("1", "0"):
-        monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+        ocrk_opts("CONV_ROWS", int(mode))
         dw = torch.full((3, 3, C, CO), 0.5, device=cuda)
         Kn.conv3x3_bwd_weight(x, dy, dw, accumulate=True)
         outs.append(dw.double() - 0.5)
@@ -370,7 +370,7 @@ def test_conv2_wgrad_rows_matches(cuda, monkeypatch, B, H, W, C, CO):
 
 # conv2's data gradient by image rows (conv_rows.hip) against the chunked direct
 # kernel (same bits: same products, same k order per output) and float64
-def test_conv2_dgrad_rows_matches(cuda, monkeypatch):
+def test_conv2_dgrad_rows_matches(cuda, ocrk_opts):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(7)
     for B, H, W in [(4, 30, 254), (3, 7, 37), (2, 1, 5)]:
@@ -384,7 +384,7 @@ def test_conv2_dgrad_rows_matches(cuda, monkeypatch):
         ref = ref.permute(0, 2, 3, 1) * (mask.double() > 0)
         outs = []
         for mode in ("1", "0"):
-            monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+            ocrk_opts("CONV_ROWS", int(mode))
             outs.append(Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask))
         torch.testing.assert_close(outs[0].double(), ref, rtol=2e-2, atol=2e-2)
         assert torch.equal(outs[0], outs[1]), (B, H, W)
@@ -396,7 +396,7 @@ def test_conv2_dgrad_rows_matches(cuda, monkeypatch):
                                           (32, 64, [(4, 15, 127), (2, 3, 20)]),
                                           (64, 64, [(4, 15, 127), (2, 2, 9)]),
                                           (64, 128, [(4, 7, 126), (2, 5, 17)])])
-def test_conv2_fwd_rowstats_matches(cuda, monkeypatch, CI, CO, shapes):
+def test_conv2_fwd_rowstats_matches(cuda, ocrk_opts, CI, CO, shapes):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(9)
     for B, H, W in shapes:
@@ -407,10 +407,10 @@ def test_conv2_fwd_rowstats_matches(cuda, monkeypatch, CI, CO, shapes):
         assert Kn.conv3x3_fwd_rowstats_ok(x, C)
         z, st = Kn.conv3x3_fwd_rowstats(x, w_nk, bias)
         M = B * H * W
-        monkeypatch.setenv("OCRK_CONV_ROWS", "0")
+        ocrk_opts("CONV_ROWS", 0)
         st_ref = torch.empty(Kn.conv_stats_tiles(M), 2, C, device=cuda)
         z_ref = Kn.conv3x3_fwd(x, w_nk, bias, relu=False, stats=st_ref)
-        monkeypatch.delenv("OCRK_CONV_ROWS")
+        ocrk_opts.reset("CONV_ROWS")
         assert torch.equal(z, z_ref), (B, H, W)
         m1, i1 = Kn.bn_finalize(st, M, C, 1e-3, 0.99, tile_rows=W)
         m2, i2 = Kn.bn_finalize(st_ref, M, C, 1e-3, 0.99)
@@ -430,7 +430,7 @@ def test_conv2_fwd_rowstats_matches(cuda, monkeypatch, CI, CO, shapes):
 # the producer's bias sums, conv5: 64 <- 128 plain) against the GEMM path
 @pytest.mark.parametrize("CI,CO,H,W,masked", [(64, 64, 15, 127, True), (64, 64, 15, 127, False),
                                               (64, 64, 3, 20, True)])
-def test_dgrad_rows_wide_matches(cuda, monkeypatch, CI, CO, H, W, masked):
+def test_dgrad_rows_wide_matches(cuda, ocrk_opts, CI, CO, H, W, masked):
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     g = torch.Generator(device=cuda).manual_seed(CI + CO + W)
     B = 5
@@ -438,9 +438,9 @@ def test_dgrad_rows_wide_matches(cuda, monkeypatch, CI, CO, H, W, masked):
     w_bwd = (torch.randn(CI, 9 * CO, device=cuda, generator=g) / 20).bfloat16()
     mask = torch.randn(B, H, W, CI, device=cuda, generator=g).bfloat16() if masked else None
     outs = []
-    monkeypatch.setenv("OCRK_CONV_WGRAD_BLOCKS", "2")           # conv7 / conv8 blocks too (opt-in)
+    ocrk_opts("CONV_WGRAD_BLOCKS", 2)           # conv7 / conv8 blocks too (opt-in)
     for mode in ("1", "0"):
-        monkeypatch.setenv("OCRK_CONV_ROWS", mode)
+        ocrk_opts("CONV_ROWS", int(mode))
         db = torch.full((CI,), 0.25, device=cuda) if masked else None
         dx = Kn.conv3x3_bwd_data(dy, w_bwd, relu_mask=mask, dbias=db)
         outs.append((dx, db))

@@ -13,11 +13,11 @@ from oracle import ref_graph as G
 pytestmark = pytest.mark.gpu
 
 
-def _both(K, monkeypatch, fn):
-    monkeypatch.setenv("OCRK_LSTM_PERSISTENT", "0")
+def _both(K, ocrk_opts, fn):
+    ocrk_opts("LSTM_PERSISTENT", 0)
     K._PERSISTENT.clear()
     step = fn()
-    monkeypatch.setenv("OCRK_LSTM_PERSISTENT", "1")
+    ocrk_opts("LSTM_PERSISTENT", 1)
     K._PERSISTENT.clear()
     pers = fn()
     torch.cuda.synchronize()
@@ -26,7 +26,7 @@ def _both(K, monkeypatch, fn):
 
 
 @pytest.mark.parametrize("T,B,n_in,H", [(11, 64, 32, 256), (17, 256, 64, 512)])
-def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, B, n_in, H):
+def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, ocrk_opts, T, B, n_in, H):
     from cnn_lstm_ctc_ocr_amd import kernels as K
     rng = np.random.default_rng(7 + B)
     bf = lambda a: torch.from_numpy(a.astype(np.float32)).bfloat16().float().numpy()   # noqa: E731
@@ -46,7 +46,7 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
     seq_d = torch.from_numpy(seq).to(cuda)
     assert K.lstm_persistent_ok(B, H, torch.bfloat16)
     K.lstm_error_word(cuda).zero_()
-    step, pers = _both(K, monkeypatch, lambda: K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.bfloat16))
+    step, pers = _both(K, ocrk_opts, lambda: K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.bfloat16))
     assert K.lstm_error_word(cuda).item() == 0
     # h is fed back in bf16: the two summation orders drift apart by a few bf16
     # ulps over the steps (max 0.02 seen at T=17, K=512); the oracle bounds both
@@ -59,7 +59,7 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
     dout_np = bf(rng.standard_normal(ref.shape))
     dout = torch.from_numpy(dout_np).to(cuda).bfloat16()
     _, _, cprev, acts = pers
-    dstep, dpers = _both(K, monkeypatch, lambda: K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H))
+    dstep, dpers = _both(K, ocrk_opts, lambda: K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H))
     assert K.lstm_error_word(cuda).item() == 0
     scale = dstep.float().abs().max().item()
     assert (dstep.float() - dpers.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
@@ -69,10 +69,10 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, monkeypatch, T, 
     assert np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
     # the K-split form of the persistent BPTT (OCRK_LSTM_BWD_KSPLIT=1, opt-in) against
     # the gather default: same bounds against the oracle and the per-step kernels
-    monkeypatch.setenv("OCRK_LSTM_BWD_KSPLIT", "1")
+    ocrk_opts("LSTM_BWD_KSPLIT", 1)
     dgat = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H)
     torch.cuda.synchronize()
-    monkeypatch.delenv("OCRK_LSTM_BWD_KSPLIT")
+    ocrk_opts.reset("LSTM_BWD_KSPLIT")
     assert K.lstm_error_word(cuda).item() == 0
     assert (dstep.float() - dgat.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
     gg = dgat.float().cpu().numpy()
@@ -103,7 +103,7 @@ def _bptt_ref(caches, ks, dout_np, T, B, H, n_in):
 
 
 @pytest.mark.parametrize("T,B,n_in", [(9, 96, 32), (13, 64, 32), (17, 256, 64)])
-def test_bptt_16row_members_match_gather_and_oracle(cuda, monkeypatch, T, B, n_in):
+def test_bptt_16row_members_match_gather_and_oracle(cuda, ocrk_opts, T, B, n_in):
     """The 16-row / 64-unit BPTT (default at H=512 when co-resident) against the
     32-row gather form (OCRK_LSTM_BWD_R16=0) and the oracle, with the fused bias
     partials (B/16 slices) against the column sums of its own dG. B=96 takes the
@@ -136,12 +136,12 @@ def test_bptt_16row_members_match_gather_and_oracle(cuda, monkeypatch, T, B, n_i
     dout = torch.from_numpy(dout_np).to(cuda).bfloat16()
     db16 = torch.zeros(2 * 4 * H, device=cuda)
     d16 = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H, dbias=db16)
-    monkeypatch.setenv("OCRK_LSTM_BWD_R16", "0")
+    ocrk_opts("LSTM_BWD_R16", 0)
     assert _lib.lib().ocrk_lstm_bwd_persistent_slices(B, H) == B // 32
     db32 = torch.zeros(2 * 4 * H, device=cuda)
     d32 = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H, dbias=db32)
     torch.cuda.synchronize()
-    monkeypatch.delenv("OCRK_LSTM_BWD_R16")
+    ocrk_opts.reset("LSTM_BWD_R16")
     assert K.lstm_error_word(cuda).item() == 0
     scale = d32.float().abs().max().item()
     assert (d16.float() - d32.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
@@ -162,7 +162,7 @@ def test_bptt_16row_members_match_gather_and_oracle(cuda, monkeypatch, T, B, n_i
     print(f"bias rel err vs oracle: 16-row {rel(db16, ref_b):.3e} gather {rel(db32, ref_b):.3e}")
 
 
-def test_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
+def test_persistent_timeout_sets_status_and_raises(cuda, ocrk_opts):
     """A hand-off wait that gives up (forced here with a spin limit of 1 poll)
     must surface: the kernels OR their bit into the device status word, run to
     completion (no hang), and the host raises DeviceError at its next check
@@ -177,10 +177,10 @@ def test_persistent_timeout_sets_status_and_raises(cuda, monkeypatch):
     K._PERSISTENT.clear()
     assert K.lstm_persistent_ok(B, H, torch.bfloat16)
     K.status_word(cuda).zero_()
-    monkeypatch.setenv("OCRK_LSTM_SPIN_LIMIT", "1")
+    ocrk_opts("LSTM_SPIN_LIMIT", 1)
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
     torch.cuda.synchronize()
-    monkeypatch.delenv("OCRK_LSTM_SPIN_LIMIT")
+    ocrk_opts.reset("LSTM_SPIN_LIMIT")
     with pytest.raises(_lib.DeviceError):
         K.check_status(cuda)
     assert K.read_status(cuda) == 0
@@ -228,7 +228,7 @@ def test_fused_input_projection_forward(cuda, B):
 
 
 @pytest.mark.parametrize("T,B,n_in", [(19, 64, 64), (23, 160, 256)])
-def test_f32_persistent_fwd_matches_oracle_and_step_kernels(cuda, monkeypatch, T, B, n_in):
+def test_f32_persistent_fwd_matches_oracle_and_step_kernels(cuda, ocrk_opts, T, B, n_in):
     """The fp32 forward loop (csrc/lstm_f32x3.hip: one persistent launch, h.W_h on
     the bf16x3 split) against the float64 oracle (lstm_dir_fwd, ragged lengths,
     reverse direction) and the per-step fp32 kernels (exact f32 MFMA): outputs
@@ -252,7 +252,7 @@ def test_f32_persistent_fwd_matches_oracle_and_step_kernels(cuda, monkeypatch, T
     seq_d = torch.from_numpy(seq).to(cuda)
     assert K.lstm_f32_persistent_ok(B, H)
     K.lstm_error_word(cuda).zero_()
-    step, pers = _both(K, monkeypatch, lambda: K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.float32))
+    step, pers = _both(K, ocrk_opts, lambda: K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.float32))
     assert K.lstm_error_word(cuda).item() == 0
     out = pers[0].cpu().numpy()
     assert np.linalg.norm(out - ref) / np.linalg.norm(ref) < 5e-5

@@ -1,5 +1,4 @@
-"""Longer bf16-vs-fp32 training evidence than tests/test_gpu_train_curves.py
-(300 steps at the reference's lr leave both models on the blank plateau, CER 1):
+"""Training-curve sweeps beside tests/test_gpu_trained.py (any step count / lr):
 the same fixture (the reference's data/val/words-000.tfrecord crops), the same
 width-sorted batches of 32 and seeded epoch shuffle, both precisions from the
 same seed, `--steps` steps at `--lr`, the loss of every step and the greedy CER
@@ -30,9 +29,9 @@ def main():
     args = ap.parse_args()
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
     from cnn_lstm_ctc_ocr_amd.train import Trainer
-    from test_gpu_train_curves import _batches
+    from test_gpu_trained import shard_batches
     dev = torch.device("cuda:0")
-    batches = _batches(dev)
+    batches = shard_batches()
     res = {"steps": args.steps, "lr": args.lr, "batches": len(batches), "batch": 32,
            "data": "tests/golden/mjsynth_val_words000.npz (reference data/val/words-000.tfrecord, 803 crops)"}
     for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
