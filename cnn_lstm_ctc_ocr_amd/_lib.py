@@ -84,6 +84,8 @@ SIGNATURES = {
     "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_stream_wait": [_p, _p, _i32],
+    "ocrk_stream_create_cu_limited": [_i32, _p],
+    "ocrk_stream_destroy": [_p],
     "ocrk_copy_batch": [_p, _i32, _i64, _p],
     "ocrk_gru_fwd_persistent_supported": [_i32, _i32],
     "ocrk_gru_fwd_persistent_workspace_size": [_i32, _i32],

@@ -24,6 +24,7 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // set up thread-safely: one process may drive several GPUs, one thread each
 // ("a per-device kernel-module cache (thread-safe)").
 constexpr int kMaxDevices = 64;
+constexpr int kMaxCuWords = 32;                       // CU-mask words (1024 CUs)
 inline int current_device() {
     int d = 0;
     (void)hipGetDevice(&d);
@@ -72,6 +73,8 @@ enum Option : int {
     OPT_LSTM_BWD_PB16,        // 1: K-split partial products exchanged in bf16
     OPT_LSTM_BWD_R16,         // 1 (default) 16-row / 64-unit BPTT members at H = 512, 0 the 32-row gather
     OPT_CTC_LDS,              // 1 (default) CTC lattices in LDS when they fit, 0 in the global workspace
+    OPT_PP_PERSIST_NK,        // ping-pong GEMM: persistent workgroups when K-tiles per item <= this (8)
+    OPT_PP_DEEP,              // 1: the deep-lead ping-pong schedule for the plain (A_ROWK) GEMMs
     OPT_COUNT
 };
 int64_t opt(Option o);

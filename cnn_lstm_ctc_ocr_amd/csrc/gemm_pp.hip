@@ -489,6 +489,347 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmParams p) {
     }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime count (the in-flight VMEM ops a
+// schedule allows): a scalar jump table over the immediate forms; n > 63 waits
+// for vmcnt(63), which is stricter and so still correct.
+__device__ __forceinline__ void vm_wait_n(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    n = n > 63 ? 63 : n;
+    switch (n) {
+#define VW1(i) case i: vm_wait<i>(); break;
+#define VW8(b) VW1(b) VW1(b + 1) VW1(b + 2) VW1(b + 3) VW1(b + 4) VW1(b + 5) VW1(b + 6) VW1(b + 7)
+        VW8(0) VW8(8) VW8(16) VW8(24) VW8(32) VW8(40) VW8(48) VW8(56)
+#undef VW8
+#undef VW1
+    default: vm_wait<0>();
+    }
+}
+
+// vm_wait_n with the schedule's steady-state count as a one-compare fast path
+template <int FAST>
+__device__ __forceinline__ void vm_wait_fast(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n == FAST) vm_wait<FAST>();
+    else vm_wait_n(n);
+}
+
+// ---------------------------------------------------------------------------
+// Deep-lead form of the ping-pong engine (A_ROWK, bf16 C, bias / ReLU
+// epilogue): the same 256 x BN x 64 tile, 8 waves, 4 phases per K-tile and
+// the same two 64-KB LDS buffers, but each DMA unit is issued as soon as the
+// slot it overwrites is free, not a whole K-tile ahead into the other buffer,
+// so a unit lands 5-6 phases (1.25-1.5 K-tiles) after its issue instead of 3.
+// What frees the slots early: the B q0 fragments are kept in registers from
+// phase 0 to phase 3 (phase 3 reads no LDS), so in step s (buffer s & 1):
+//     last reads  U0, U1: phase 0   U2: phase 1   U3: phase 2
+// and a slot may be re-filled two phases after its last read (the stagger:
+// G1 reads one barrier behind G0). The unit stream, one unit per phase:
+//     phase 0: U2(s+1)   phase 1: U3(s+1)   phase 2: U0(s+2)   phase 3: U1(s+2)
+// into the buffer of the step it belongs to. Waits (counted from a uniform
+// tally of the VMEM ops this wave issued, so item boundaries, epilogue stores
+// and the end of the stream need no special cases), each two phases before
+// the read they protect:
+//     phase 0: U3(s)        phase 2: U0 + U1(s+1)        phase 3: U2(s+1)
+// Item epilogue (persistent workgroups, items prefetched across): when item i
+// ends in step s, U3(s+1) and U0, U1(s+2) are in flight, but the U2 and U3
+// slots of step s's buffer are free until phase 0 of step s+1, so each wave
+// stages its C rows there, 16 rows at a time (per-wave areas of 2.3 / 1.3 KB:
+// waves 0-3 in the four U2 pieces, waves 4-7 in the two U3 row blocks), and
+// the next item's first step starts only after a barrier behind those reads.
+// The bias (projections only) is loaded at the top of the epilogue, which
+// drains the three units then in flight (in-order vmcnt) -- at most ~1 us per
+// item; holding it in registers through the last step instead costs 16 VGPRs
+// the schedule does not have (256 with spills).
+template <int BN>
+__global__ void __launch_bounds__(512) gemm_pp_deep_kernel(const GemmParams p) {
+    constexpr int BM = 256, BK = 64, ROWB = 128;
+    constexpr int WCOLS = BN / 4;
+    constexpr int QN = WCOLS / 32;
+    constexpr int A_BYTES = BM * ROWB, BUF = (BM + BN) * ROWB;
+    constexpr int NUA = 2, NUB = BN / 128;
+    constexpr int HBLK = WCOLS / 16;
+    constexpr int PITCH = WCOLS * 2 + 16, CPRW = WCOLS / 8;
+    constexpr int CR = 16;                                // staged rows per round
+    constexpr int NST = 128 * CPRW / 64;                  // 16-B C stores per lane per item
+    static_assert(BN == 256 || BN == 128, "BN");
+    static_assert(CR * PITCH <= (BN == 256 ? 4096 : 2048), "a wave's staging fits its slot piece");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int i16 = lane & 15, g = lane >> 4, sw = lane & 7;
+
+    const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
+    const int nitems = tm * tn * p.batch * p.splits;
+    const int per = (nitems + 7) >> 3;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, sp = gridDim.x >> 3;
+    const int wend = min(nitems, (xcd + 1) * per);
+    int w_issue = xcd * per + slot;
+    if (w_issue >= wend) return;
+
+    const int lrow = lane >> 3;
+    const int cs = (lane & 7) ^ lrow;
+    int arow[4];
+    arow[0] = wave * 8;
+    arow[1] = 128 + wave * 8;
+    arow[2] = 64 + wave * 8;
+    arow[3] = 192 + wave * 8;
+    int bcol[2 * NUB];
+#pragma unroll
+    for (int i = 0; i < NUB; ++i) {
+        const int b = i * 8 + wave;
+        bcol[i] = (b / HBLK) * WCOLS + (b % HBLK) * 8;
+        bcol[NUB + i] = bcol[i] + WCOLS / 2;
+    }
+
+    i32x4_t ra, rb;
+    int i_m0 = 0, i_n0 = 0, i_kbeg = 0, i_kend = 0, i_nk = 0, i_kt = 0;
+    const unsigned a_lane = (unsigned)(lrow * p.lda * 2), b_lane = (unsigned)(lrow * p.ldb * 2);
+    auto setup_issue = [&](int w) {
+        const PPItem it = pp_item(w, tm, tn, p.splits, BM, BN);
+        const bf16* A = reinterpret_cast<const bf16*>(p.A) + it.zb * p.strideA;
+        const bf16* B = reinterpret_cast<const bf16*>(p.B) + it.zb * p.strideB;
+        ra = uniform_rsrc_words(A, (int64_t)p.M * p.lda * 2);
+        rb = uniform_rsrc_words(B, (int64_t)p.N * p.ldb * 2);
+        i_m0 = it.m0;
+        i_n0 = it.n0;
+        i_kbeg = it.zs * p.k_chunk;
+        i_kend = min(p.K, i_kbeg + p.k_chunk);
+        i_nk = max(1, (i_kend - i_kbeg + BK - 1) / BK);
+        i_kt = 0;
+    };
+    int ops = 0;                                          // VMEM ops this wave has issued (uniform)
+    // unit U of the issue side's current K-tile into `buf` (inline asm: the
+    // compiler's waitcnt pass does not see these, the counted waits order them)
+    auto issue = [&](auto U_, char* buf) {
+        constexpr int U = decltype(U_)::value;
+        const int k = i_kbeg + i_kt * BK + 8 * cs;
+        const bool kok = k < i_kend;
+        if constexpr (U == 0 || U == 3) {
+#pragma unroll
+            for (int i = 0; i < NUA; ++i) {
+                const int s = (U == 0 ? 0 : 2) + i;
+                const int mrow = i_m0 + arow[s];
+                const bool ok = kok && lrow < p.M - mrow;
+                const unsigned voff = a_lane + (unsigned)(mrow * p.lda * 2) + (unsigned)(k * 2);
+                lds_dma16_asm(ra, buf + arow[s] * ROWB, ok ? voff : PP_OOB);
+            }
+            ops += NUA;
+        } else {
+#pragma unroll
+            for (int i = 0; i < NUB; ++i) {
+                const int s = (U == 1 ? 0 : NUB) + i;
+                const int ncol = i_n0 + bcol[s];
+                const bool ok = kok && lrow < p.N - ncol;
+                const unsigned voff = b_lane + (unsigned)(ncol * p.ldb * 2) + (unsigned)(k * 2);
+                lds_dma16_asm(rb, buf + A_BYTES + bcol[s] * ROWB, ok ? voff : PP_OOB);
+            }
+            ops += NUB;
+        }
+    };
+    int is = 0;                                           // step the issue side is on
+    auto advance_issue = [&]() -> bool {
+        ++is;
+        if (++i_kt < i_nk) return true;
+        w_issue += sp;
+        if (w_issue >= wend) return false;
+        setup_issue(w_issue);
+        return true;
+    };
+    auto ibuf = [&]() { return smem + (is & 1) * BUF; };
+
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+
+    int w_comp = w_issue;
+    PPItem cur_it = pp_item(w_comp, tm, tn, p.splits, BM, BN);
+    int c_nk, c_kt = 0;
+
+    // prologue: step 0 whole, then U0 / U1 of step 1
+    int m3_cur = 0, m3_next = 0, m2_next = 0, m1_next = 0, m1_next2 = 0;
+    setup_issue(w_issue);
+    c_nk = i_nk;
+    issue(I0{}, ibuf());
+    issue(I1{}, ibuf());
+    issue(I2{}, ibuf());
+    issue(I3{}, ibuf());
+    m3_cur = ops;
+    bool more = advance_issue();
+    if (more) {
+        issue(I0{}, ibuf());
+        issue(I1{}, ibuf());
+        m1_next = ops;
+    }
+    vm_wait_n(ops - m3_cur);
+    pp_barrier();
+    if (wm == 1) pp_barrier();
+
+    floatx4 acc[8][2 * QN];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2 * QN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 afr[4][2], bq0[QN][2], bq1[QN][2];
+    const int a_base = (wm * 128 + i16) * ROWB, b_base = A_BYTES + (wn * WCOLS + i16) * ROWB;
+    auto read_a = [&](const char* cur, int qa) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                afr[i][kk] = *reinterpret_cast<const bf16x8*>(
+                    cur + a_base + (qa * 64 + i * 16) * ROWB + (((kk * 4 + g) ^ sw) << 4));
+    };
+    auto read_b = [&](const char* cur, int qb, bf16x8 (&bf)[QN][2]) {
+#pragma unroll
+        for (int j = 0; j < QN; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                bf[j][kk] = *reinterpret_cast<const bf16x8*>(
+                    cur + b_base + (qb * (WCOLS / 2) + j * 16) * ROWB + (((kk * 4 + g) ^ sw) << 4));
+    };
+    auto mfma_q = [&](auto QA_, auto QB_, const bf16x8 (&bf)[QN][2]) {
+        constexpr int QA = decltype(QA_)::value, QB = decltype(QB_)::value;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < QN; ++j)
+                    acc[QA * 4 + i][QB * QN + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        bf[j][kk], afr[i][kk], acc[QA * 4 + i][QB * QN + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    int s = 0;
+    for (;;) {
+        const char* cur = smem + (s & 1) * BUF;
+        // ---- phase 0: A q0 + B q0 (B q0 kept to phase 3); U2(s+1); retire U3(s)
+        read_a(cur, 0);
+        read_b(cur, 0, bq0);
+        if (more) { issue(I2{}, ibuf()); m2_next = ops; }
+        vm_wait_fast<NUA + 2 * NUB>(ops - m3_cur);                 // U0, U1, U2(s+1) stay in flight
+        pp_barrier();
+        mfma_q(I0{}, I0{}, bq0);
+        pp_barrier();
+        // ---- phase 1: B q1; U3(s+1)
+        read_b(cur, 1, bq1);
+        if (more) {
+            issue(I3{}, ibuf());
+            m3_next = ops;
+            more = advance_issue();
+        }
+        pp_barrier();
+        mfma_q(I0{}, I1{}, bq1);
+        pp_barrier();
+        // ---- phase 2: A q1 (B q1 kept); U0(s+2); retire U0 + U1(s+1)
+        read_a(cur, 1);
+        if (more) issue(I0{}, ibuf());
+        vm_wait_fast<NUB + 2 * NUA>(ops - m1_next);                // U2, U3(s+1), U0(s+2) stay
+        pp_barrier();
+        mfma_q(I1{}, I1{}, bq1);
+        pp_barrier();
+        // ---- phase 3: no LDS reads (B q0 from phase 0); U1(s+2); retire U2(s+1)
+        if (more) { issue(I1{}, ibuf()); m1_next2 = ops; }
+        vm_wait_fast<2 * NUA + NUB>(ops - m2_next);                // U3(s+1), U0, U1(s+2) stay
+        pp_barrier();
+        mfma_q(I1{}, I0{}, bq0);
+        pp_barrier();
+        m3_cur = m3_next;
+        m1_next = m1_next2;
+        ++s;
+        if (++c_kt < c_nk) continue;
+
+        // ================================================= item epilogue
+        if (wm == 0) pp_barrier();                        // groups meet: step s's reads are done
+        // staging: the U2 (waves 0-3) / U3 (waves 4-7) slots of step s's buffer
+        char* stg = const_cast<char*>(cur) +
+                    (wm == 0 ? A_BYTES + (wn * WCOLS + WCOLS / 2) * ROWB : (wn < 2 ? 64 : 192) * ROWB + (wn & 1) * 4096);
+        floatx4 bv[2 * QN];
+        if (p.bias) {
+            const __amdgpu_buffer_rsrc_t rbias = uniform_rsrc(p.bias + cur_it.zb * p.strideBias, (int64_t)p.N * 4);
+            const int ncol0 = cur_it.n0 + wn * WCOLS + 4 * g;
+#pragma unroll
+            for (int j = 0; j < 2 * QN; ++j) {
+                const int n = ncol0 + j * 16;
+                bv[j] = __builtin_bit_cast(
+                    floatx4, __builtin_amdgcn_raw_buffer_load_b128(rbias, n < p.N ? (unsigned)(n * 4) : PP_OOB, 0, 0));
+            }
+            ops += 2 * QN;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 2 * QN; ++j) bv[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * QN; ++j) {
+            const floatx4 b = bv[j];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                floatx4 v = acc[i][j] * p.alpha + b;
+                if (p.relu) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+                }
+                acc[i][j] = v;
+            }
+        }
+        bf16* Cb = reinterpret_cast<bf16*>(p.C) + cur_it.zb * p.strideC;
+        const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(Cb, ((int64_t)(p.M - 1) * p.ldc + p.N) * 2);
+        const int c8 = lane % CPRW, r0 = lane / CPRW;
+        const int n = cur_it.n0 + wn * WCOLS + 8 * c8;
+#pragma unroll
+        for (int h = 0; h < 128 / CR; ++h) {
+#pragma unroll
+            for (int j = 0; j < 2 * QN; ++j) {
+                u16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = __builtin_bit_cast(unsigned short, (bf16)acc[h][j][r]);
+                *reinterpret_cast<u16x4*>(stg + i16 * PITCH + (j * 16 + 4 * g) * 2) = o;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int q = 0; q < CR * CPRW / 64; ++q) {
+                const int r = r0 + q * (64 / CPRW);
+                const int m = cur_it.m0 + wm * 128 + h * CR + r;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(stg + r * PITCH + c8 * 16);
+                const unsigned off = (m < p.M && n < p.N) ? (unsigned)(((int64_t)m * p.ldc + n) * 2) : PP_OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rc, off, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        ops += NST;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();                                     // staging reads done before U2 / U3(s+1) refill them
+        w_comp += sp;
+        if (w_comp >= wend) break;
+        cur_it = pp_item(w_comp, tm, tn, p.splits, BM, BN);
+        c_nk = max(1, (min(p.K, cur_it.zs * p.k_chunk + p.k_chunk) - cur_it.zs * p.k_chunk + BK - 1) / BK);
+        c_kt = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 2 * QN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (wm == 1) pp_barrier();                        // re-stagger
+    }
+}
+
+template <int BN>
+int launch_pp_deep(const GemmParams& p, hipStream_t stream) {
+    constexpr int LDS = 2 * (256 + BN) * 128;
+    static DeviceOnce configured;
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_pp_deep_kernel<BN>), LDS);
+    const int ncu = cu_count();
+    const int64_t items = cdiv(p.M, 256) * cdiv(p.N, BN) * (int64_t)p.batch * p.splits;
+    // persistent: one workgroup per CU, items prefetched across
+    const int64_t grid = std::min<int64_t>(cdiv(items, 8) * 8, (int64_t)(ncu / 8) * 8);
+    gemm_pp_deep_kernel<BN><<<dim3((unsigned)grid), 512, LDS, stream>>>(p);
+    return launch_status("gemm_pp_deep");
+}
+
 template <int AM, int BN, bool STATS, bool MASK>
 int launch_pp_k(const GemmParams& p, hipStream_t stream) {
     constexpr int LDS = 2 * (256 + BN) * 128;
@@ -501,7 +842,7 @@ int launch_pp_k(const GemmParams& p, hipStream_t stream) {
     // item per workgroup -- the epilogue's stores then never sit in front of
     // the next item's DMA waits (vmcnt is in order), measured faster for K >= 1024.
     const int64_t nk = cdiv(p.K, 64);
-    const int64_t grid = nk <= 8 ? std::min<int64_t>(cdiv(items, 8) * 8, (int64_t)(ncu / 8) * 8)
+    const int64_t grid = nk <= opt(OPT_PP_PERSIST_NK) ? std::min<int64_t>(cdiv(items, 8) * 8, (int64_t)(ncu / 8) * 8)
                                  : cdiv(items, 8) * 8;
     gemm_pp_kernel<AM, BN, STATS, MASK><<<dim3((unsigned)grid), 512, LDS, stream>>>(p);
     return launch_status("gemm_pp");
@@ -514,6 +855,7 @@ int launch_pp(const GemmParams& p, hipStream_t stream) {
         return launch_pp_k<AM, BN, false, true>(p, stream);
     }
     if (p.mask) return -1;
+    if (AM == A_ROWK && !p.stats && opt(OPT_PP_DEEP)) return launch_pp_deep<BN>(p, stream);
     if (p.stats) return launch_pp_k<AM, BN, true, false>(p, stream);
     return launch_pp_k<AM, BN, false, false>(p, stream);
 }

@@ -36,7 +36,7 @@ struct OptDef {
 constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"CONV_DIRECT", 1}, {"CONV_ROWS", 1}, {"CONV_ROWS_WIDE", 1}, {"CONV_WGRAD_BLOCKS", 1},
     {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0}, {"LSTM_BWD_PB16", 0},
-    {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1},
+    {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1}, {"PP_PERSIST_NK", 8}, {"PP_DEEP", 0},
 };
 std::atomic<int64_t> g_opts[OPT_COUNT];
 std::once_flag g_opts_once;
@@ -162,6 +162,33 @@ int ocrk_stream_wait(void* waiter, void* signaller, int mode) {
         ocrk::set_error("ocrk_stream_wait: %s", hipGetErrorString(e));
         return OCRK_ERR_HIP;
     }
+    return OCRK_OK;
+}
+
+int ocrk_stream_create_cu_limited(int n_cus, void** stream) {
+    OCRK_REQUIRE(stream != nullptr && n_cus > 0, "ocrk_stream_create_cu_limited: n_cus %d / null slot", n_cus);
+    const int total = ocrk::cu_count();
+    uint32_t mask[ocrk::kMaxCuWords] = {};
+    OCRK_REQUIRE(total <= 32 * ocrk::kMaxCuWords, "ocrk_stream_create_cu_limited: %d CUs", total);
+    // keep n of every `total` CUs, the left-out ones evenly spaced over the CU
+    // order (so every XCD / shader engine keeps some for other streams)
+    const int keep = n_cus < total ? n_cus : total;
+    for (int i = 0; i < total; ++i) {
+        const bool on = (int64_t)(i + 1) * keep / total != (int64_t)i * keep / total;
+        if (on) mask[i / 32] |= 1u << (i % 32);
+    }
+    hipStream_t s = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)((total + 31) / 32), mask);
+    if (e != hipSuccess) {
+        ocrk::set_error("ocrk_stream_create_cu_limited: %s", hipGetErrorString(e));
+        return OCRK_ERR_HIP;
+    }
+    *stream = s;
+    return OCRK_OK;
+}
+
+int ocrk_stream_destroy(void* stream) {
+    if (stream) (void)hipStreamDestroy(ocrk::as_stream(stream));
     return OCRK_OK;
 }
 

@@ -640,6 +640,19 @@ def stream_wait(waiter, signaller, mode=1):
 
 
 
+_CU_STREAMS = []        # (handle, ExternalStream): kept for the process
+
+
+def cu_limited_stream(device, n_cus):
+    """torch.cuda.ExternalStream over ocrk_stream_create_cu_limited(n_cus) on `device`."""
+    with torch.cuda.device(device):
+        h = ctypes.c_void_p()
+        call("ocrk_stream_create_cu_limited", int(n_cus), ctypes.byref(h))
+        st = torch.cuda.ExternalStream(h.value, device=device)
+    _CU_STREAMS.append((h, st))
+    return st
+
+
 def fork_mode():
     """0: torch events for stream forks; 1 / 2: ocrk_stream_wait's fence-less events (option FORK_EVENTS)."""
     return options.get("FORK_EVENTS")

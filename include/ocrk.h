@@ -89,9 +89,17 @@ const char* ocrk_last_error(void);
  * ocrk_set_option changes it (process-wide, takes effect at the next launch; the
  * "OCRK_" prefix is optional in `name`). Names: CONV_DIRECT, CONV_ROWS,
  * CONV_ROWS_WIDE, CONV_WGRAD_BLOCKS, LSTM_SPIN_LIMIT, PERSIST_LATE,
- * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS (meanings in
+ * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP (meanings in
  * csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
+
+/* A stream on the current device whose kernels run on only n_cus of its CUs
+ * (hipExtStreamCreateWithCUMask; the CUs left out are evenly spaced over the CU
+ * order, so every XCD keeps some), for side work that must leave CUs to the
+ * main stream (the weight gradients beside the data gradients; option
+ * SIDE_CU_MASK). Released with ocrk_stream_destroy. No reference counterpart. */
+int ocrk_stream_create_cu_limited(int n_cus, void** stream);
+int ocrk_stream_destroy(void* stream);
 int ocrk_get_option(const char* name, int64_t* value);
 
 /* a1 -- validate._preprocess_image (src/weinman/validate.py:56-68):

@@ -111,6 +111,33 @@ def test_bf16_plain_gemms_bias_bf16_out(cuda, M_, N, K, tag):
     assert np.all(err <= 2 ** -8 * np.abs(ref) + 1e-3 * np.abs(ref).max()), tag
 
 
+@pytest.mark.parametrize("M_,N,K,relu,with_bias", [(32000, 4096, 1024, False, True), (8000, 4096, 256, False, True),
+                                                   (8000, 1024, 4096, False, False), (7777, 1032, 96, True, True),
+                                                   (4100, 520, 200, False, True)])
+def test_pp_deep_schedule_bit_identical(cuda, ocrk_opts, M_, N, K, relu, with_bias):
+    """The deep-lead ping-pong schedule (option PP_DEEP, csrc/gemm_pp.hip:
+    units issued into slots as they free, persistent workgroups with items
+    prefetched across, C staged in the U2 / U3 slots) multiplies in the same
+    order as the one-tile-lead form, so its output is the same bits -- on the
+    bench shapes (32,000 rows: ~8 items per workgroup), BN = 128 tiles, ragged
+    M / N / K tails, with and without bias, with ReLU."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(M_ + N + K)
+    a = torch.from_numpy(_bf(rng.standard_normal((M_, K)))).to(cuda).bfloat16()
+    w = torch.from_numpy(_bf(rng.standard_normal((N, K)) / np.sqrt(K))).to(cuda).bfloat16()
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).to(cuda) if with_bias else None
+    outs = []
+    for deep in (0, 1):
+        ocrk_opts("PP_DEEP", deep)
+        outs.append(Kn.gemm(a, w, trans_b=True, bias=bias, relu=relu, out_dtype=torch.bfloat16))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), (M_, N, K)
+    ref = a[:2048].double() @ w.double().t() + (bias.double() if with_bias else 0)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert _rel(outs[1][:2048].double().cpu().numpy(), ref.cpu().numpy()) < BF16_OUT
+
+
 @pytest.mark.parametrize("R,n_in,G4,splits,col", [(8000, 1024, 2048, 4, 0), (8000, 512, 2048, 8, 2048),
                                                    (8000, 256, 2048, 1, 0), (8000, 1024, 96, 3, 0),
                                                    (1000, 264, 296, 2, 8)])
