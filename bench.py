@@ -120,13 +120,14 @@ def _cpu_batch(rng, B, W):
 RNN_SIZES = {"lstm": (512, 512), "gru": (512, 256)}     # model_bu.py (bench default) / model.py
 
 
-def cpu_baseline(sample, warmup=3, steps=10, cell="lstm"):
+def cpu_baseline(sample, warmup=1, steps=2, cell="lstm"):
     """BASELINE.md CPU-baseline plan: the reference graph's train step (conv ->
     BiLSTM 512/512 -> CTC -> TF1 Adam) as the PyTorch-CPU restatement
     (oracle/torch_ref.py, checked against the NumPy oracle in
     tests/test_oracle.py; TensorFlow 1.x is unavailable), with every host
-    thread this process may use, 3 warm-up + 10 timed steps on `sample`
-    synthetic 32x256 crops (bounded so the default run stays within minutes)."""
+    thread this process may use, on `sample` synthetic 32x256 crops -- by
+    default the GPU step's own shape (B = 256), 1 warm-up + 2 timed steps
+    (~15 s of host time, bounded so the default run stays within minutes)."""
     from oracle import ref_model as M
     from oracle.torch_ref import TorchRef
     threads, model = host_cpu()
@@ -579,7 +580,9 @@ def main():
     ap.add_argument("--probe-every", type=int, default=4,
                     help="eager mode: the roofline kernel's HIP-event probes bracket its launches in every "
                          "Nth timed step (each probe event costs ~6 us of queue idle; 1 = every step)")
-    ap.add_argument("--cpu-sample", type=int, default=32, help="crops per CPU-baseline train step")
+    ap.add_argument("--cpu-sample", type=int, default=256,
+                    help="crops per CPU-baseline train step (default: the GPU step's B = 256)")
+    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline train steps (after 1 warm-up)")
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
                     help="c3: the headline train step (default); c2: B=64 fp32 fwd+CTC+greedy; "
                          "c5: bucketed 32x{64..512} crops, beam-16 decode")
@@ -808,7 +811,7 @@ def main():
     if rank == 0 and not args.no_cer and args.cell == "lstm":      # the golden decodes are of the LSTM model
         result["cer_vs_ref"] = cer_vs_ref(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, cell=args.cell)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, steps=args.cpu_steps, cell=args.cell)
         if args.cell == "lstm":
             result["c1_latency"] = c1_latency(device)
     if rank == 0:

@@ -308,7 +308,6 @@ def lstm_persistent_ok(B, H, dtype):
     """Run the bf16 time loops as persistent launches (csrc/lstm_persistent.hip)?
     On by default where the grid fits co-resident (B % 32 == 0, H in {256,
     512}); OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
-    import os
     if dtype != torch.bfloat16 or not options.get("LSTM_PERSISTENT"):
         return False
     key = (B, H)
@@ -420,7 +419,6 @@ def lstm_f32_persistent_ok(B, H):
     (csrc/lstm_f32x3.hip)? H = 512, B % 16 == 0 and the grid co-resident; not
     in exact fp32 mode (f32_exact); OCRK_LSTM_PERSISTENT=0 selects the per-step
     fp32 kernels."""
-    import os
     if not options.get("LSTM_PERSISTENT") or f32_mode_exact():
         return False
     key = ("f32", B, H)
@@ -480,7 +478,6 @@ def lstm_fused_x_ok(B, H, n_in, dtype, force=False):
     longer (3.40 vs 2.68 us: the x.W_x MFMAs and the x-row DMA land on the
     step's critical path), 480 vs 490 us for GEMM + loop alone and 5.865 vs
     5.847 ms for the train step (profiles/r3_fused_projection.txt)."""
-    import os
     if not force and options.get("LSTM_FUSE_X") != 1:
         return False
     if not lstm_persistent_ok(B, H, dtype):
@@ -543,7 +540,6 @@ def gru_persistent_ok(B, H, dtype):
     """Run the bf16 GRU time loops as persistent launches (csrc/gru_persistent.hip)?
     Same rule and switch as the LSTM: B % 32 == 0, H in {256, 512}, the grid
     co-resident; OCRK_LSTM_PERSISTENT=0 selects the per-step kernels."""
-    import os
     if dtype != torch.bfloat16 or not options.get("LSTM_PERSISTENT"):
         return False
     key = (B, H)

@@ -57,11 +57,24 @@ def _grad_enabled(*ts):
 
 
 # ------------------------------------------------------------------ convnet
+def _conv_precision(exact):
+    """fp32 training's conv tower runs exact f32 MFMA products (store.f32_conv_exact,
+    set by the Trainer): the BN backward amplifies the bf16x3 split's ~2^-16 product
+    error ~200x into the tower's gradients; everything else keeps the split."""
+    return K.f32_exact() if exact else contextlib.nullcontext()
+
+
 class _ConvBlock(torch.autograd.Function):
     """conv_{2k-1} -> conv_{2k} -> BN -> ReLU -> pool (model.py:134-146)."""
 
     @staticmethod
     def forward(ctx, x, store, k, training, *variables):
+        ctx.exact = store.cfg.dtype == torch.float32 and store.f32_conv_exact
+        with _conv_precision(ctx.exact):
+            return _ConvBlock._forward(ctx, x, store, k, training)
+
+    @staticmethod
+    def _forward(ctx, x, store, k, training):
         dt = store.cfg.dtype
         odd, even = f"conv{2 * k - 1}", f"conv{2 * k}"
         P = store.params
@@ -108,6 +121,11 @@ class _ConvBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dp):
+        with _conv_precision(ctx.exact):
+            return _ConvBlock._backward(ctx, dp)
+
+    @staticmethod
+    def _backward(ctx, dp):
         store, k = ctx.store, ctx.k
         x, y_odd, z, mean, invstd = ctx.saved_tensors
         dt = store.cfg.dtype

@@ -30,6 +30,7 @@ _HOST_DEFAULTS = {
     "UNIT_SEED": 1,           # 0: backward seeded with torch's ones instead of the resident 1.0
     "FORK_EVENTS": 0,         # 1 / 2: stream forks through ocrk_stream_wait's fence-less events
     "SIDE_CU_MASK": 0,        # > 0: the weight-gradient side stream restricted to this many CUs
+    "F32_TRAIN_EXACT": 0,     # 1: fp32 training with exact f32 products everywhere (else conv tower only)
 }
 # kernel-side options (libocrk's registry, csrc/common.h)
 KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOCKS", "LSTM_SPIN_LIMIT",

@@ -141,6 +141,7 @@ class ParamStore:
         self.pending = []          # events of side-stream gradient work not yet joined
         self.deferred = []         # (launch fn, tensors) of gradient work an upper layer deferred
         self.bn_group = None       # SyncBN: the process group TRAIN-mode BatchNorm statistics span
+        self.f32_conv_exact = False    # fp32 training: the conv tower on exact f32 products (Trainer)
         self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
 
     # ------------------------------------------------------------ state

@@ -203,13 +203,23 @@ class Trainer:
 
     def loss_and_grads(self, image, width, label):
         """Forward + backward only; gradients land in store.flat_grad. A float32
-        store trains with exact fp32 products (kernels.f32_exact; the fp32 serving
+        store trains its conv tower with exact fp32 products (the fp32 serving
         path's bf16x3 split is within 1e-4 on logits but its ~2^-16 per-product
-        error is amplified ~200x into the conv-tower gradients by the BN backward)."""
-        if self.store.cfg.dtype == torch.float32:
+        error is amplified ~200x into the conv-tower gradients by the BN
+        backward) and the recurrent layers and logits on the split (5e-5 on their
+        gradients): the persistent fp32 loops and the bf16-rate GEMMs. Option
+        F32_TRAIN_EXACT=1: exact products everywhere (the per-step fp32 loops)."""
+        store = self.store
+        if store.cfg.dtype != torch.float32:
+            return self._loss_and_grads(image, width, label)
+        if options.get("F32_TRAIN_EXACT"):
             with K.f32_exact():
                 return self._loss_and_grads(image, width, label)
-        return self._loss_and_grads(image, width, label)
+        prev, store.f32_conv_exact = store.f32_conv_exact, True
+        try:
+            return self._loss_and_grads(image, width, label)
+        finally:
+            store.f32_conv_exact = prev
 
     def _loss_and_grads(self, image, width, label):
         store = self.store
@@ -382,8 +392,8 @@ class GraphedStep:
     eager after the replay, so the learning-rate schedule and RCCL see the live
     host step count.
 
-    Capture needs every per-stream lazy resource (hipBLASLt workspace, kernel
-    attributes) to exist, so one eager forward + backward runs first on the
+    Capture needs every per-stream lazy resource (workspaces, kernel
+    attributes, hand-off flag words) to exist, so one eager forward + backward runs first on the
     capture stream; the BatchNorm moving statistics it would have updated are
     restored, and gradients are rewritten by every step anyway. The derived
     weight images are invalidated before capture so that their rebuild from
