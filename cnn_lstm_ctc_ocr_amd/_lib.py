@@ -115,6 +115,7 @@ SIGNATURES = {
     "ocrk_adam": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p],
     "ocrk_adam_ex": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _u32, _p],
     "ocrk_cast": [_p, _i32, _p, _i32, _i64, _p],
+    "ocrk_split_bf16": [_p, _i64, _p, _p, _p],
     "ocrk_permute3": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p],
     "ocrk_strided_copy": [_p, _i64, _i64, _i64, _i64, _p, _i32, _i64, _i64, _p],
     "ocrk_colsum_workspace_size": [_i64, _i32],

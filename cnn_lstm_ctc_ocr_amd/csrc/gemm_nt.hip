@@ -37,7 +37,10 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // LDS-DMA ring (BK = 32 -> 128-B rows, the bf16 BK = 64 geometry), and every
 // MFMA fragment is split at the read into bf16 hi / lo (mfma_util.h
 // split8_bf16) for the three bf16 products ah.bh + ah.bl + al.bh.
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false>
+// EXACT (with F32): exact fp32 products on v_mfma_f32_16x16x4_f32 instead of the split --
+// the fp32 Trainer's conv tower (kernels.f32_exact); lane group g supplies k = 8g + e to
+// the e-th of 8 MFMAs per 32-deep step (any k order sums the same products).
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false>
 __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
     // (its second pass over the accumulators would spill); launch_nt routes
@@ -183,6 +186,28 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
         const char* sa = smem + (kt % S) * STAGE;
         const char* sb = sa + A_BYTES;
+        if constexpr (F32 && EXACT) {
+            const int s0 = ((2 * g) ^ swz) * 16, s1 = ((2 * g + 1) ^ swz) * 16;
+            auto frag = [&](const char* row) {
+                V8<float> v;
+                v.q0 = *reinterpret_cast<const f32x4*>(row + s0);
+                v.q1 = *reinterpret_cast<const f32x4*>(row + s1);
+                return v;
+            };
+            V8<float> bv[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = frag(sb + (wn * WN + j * 16 + i16) * ROWB);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const V8<float> av = frag(sa + (wm * WM + i * 16 + i16) * ROWB);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.e(e), bv[j].e(e), acc[i][j], 0, 0, 0);
+            }
+            continue;
+        }
         if constexpr (F32) {
             // lane group g holds k = 8g .. 8g + 7 = fp32 chunks 2g, 2g + 1 of its row
             const int s0 = ((2 * g) ^ swz) * 16, s1 = ((2 * g + 1) ^ swz) * 16;
@@ -374,25 +399,26 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     }
 }
 
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false>
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false>
 int launch_nt(const GemmParams& p, hipStream_t stream) {
     if constexpr (NW == 8 && !F32) {
         if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
     }
     constexpr int LDS = S * (BM + BN) * BK * (F32 ? 4 : 2);
     static DeviceOnce configured;
-    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32>), LDS);
+    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT>),
+                LDS);
     dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
-    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32><<<grid, NW * 64, LDS, stream>>>(p);
+    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");
 }
 
-// fp32 operands on the bf16x3 split (BK = 32: 128-B fp32 rows)
-template <int AM>
+// fp32 operands (BK = 32: 128-B fp32 rows) on the bf16x3 split, or with EXACT products
+template <int AM, bool EXACT = false>
 int dispatch_nt_f32(const GemmParams& p, hipStream_t s) {
-    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM, 4, true>(p, s);
-    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM, 4, true>(p, s);
-    return launch_nt<128, 128, 32, 2, 2, AM, 4, true>(p, s);
+    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM, 4, true, EXACT>(p, s);
+    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM, 4, true, EXACT>(p, s);
+    return launch_nt<128, 128, 32, 2, 2, AM, 4, true, EXACT>(p, s);
 }
 
 // Tile configurations (OCRK_GEMM_NT_CFG picks one for experiments; by default
@@ -478,7 +504,11 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
         // shapes, the masked data gradients and OCRK_F32_MFMA=1)
         // (K >= 256 here: the first recurrent layer's input projection, K = 256, ran 3x
         // slower on the generic engine's bf16x3 staging -- 463 vs ~150 us per C5 bucket)
-        if (f32_exact_mfma() || p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 256 && p0.N > 64)) return -1;
+        // exact mode (the fp32 Trainer's conv tower): the implicit-GEMM convolutions on this
+        // ring with exact f32 products (option NT_F32_EXACT=0: the generic engine)
+        const bool exact = f32_exact_mfma();
+        if (exact && (amode == A_ROWK || !opt(OPT_NT_F32_EXACT))) return -1;
+        if (p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 256 && p0.N > 64)) return -1;
         GemmParams p = p0;
         p.epi_staged = 0;
         if (amode == A_ROWK) {
@@ -486,8 +516,10 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
             return dispatch_nt_f32<A_ROWK>(p, stream);
         }
         if (p.convC % 4 != 0 || p.ldb % 4 != 0) return -1;
-        if (amode == A_IM2COL) return dispatch_nt_f32<A_IM2COL>(p, stream);
-        if (amode == A_IM2COL_FLIP) return dispatch_nt_f32<A_IM2COL_FLIP>(p, stream);
+        if (amode == A_IM2COL) return exact ? dispatch_nt_f32<A_IM2COL, true>(p, stream)
+                                            : dispatch_nt_f32<A_IM2COL>(p, stream);
+        if (amode == A_IM2COL_FLIP) return exact ? dispatch_nt_f32<A_IM2COL_FLIP, true>(p, stream)
+                                                 : dispatch_nt_f32<A_IM2COL_FLIP>(p, stream);
         return -1;
     }
     if (dtype != OCRK_BF16) return -1;

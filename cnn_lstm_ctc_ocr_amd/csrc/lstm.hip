@@ -20,6 +20,7 @@
 // Backward step (reverse s): dh = dout + dG_{s+1} . W_h^T (K = 4H, same
 // streaming core), then the gate gradients; dG is published for the next
 // step and scattered into time order for the dW_x / dW_h / dX GEMMs.
+#include "gemm.h"
 #include "recur.h"
 
 using namespace ocrk;
@@ -398,13 +399,13 @@ struct LstmBwdOps {
     }
 };
 
-template <typename CT, int BR, int HU, int KC>
+template <typename CT, int BR, int HU, int KC, bool X3 = false>
 __global__ void __launch_bounds__(256)
 lstm_bwd_step_kernel(const CT* __restrict__ wh, const CT* __restrict__ dg_in, CT* __restrict__ dg_out,
                      float* __restrict__ dc_state, const int* __restrict__ seq_len, int s, int T, int B, int H,
                      const CT* __restrict__ dout, const float* __restrict__ cprev_t,
                      const CT* __restrict__ acts_t, CT* __restrict__ dG_t) {
-    using Core = RecurCore<CT, BR, HU, KC>;
+    using Core = RecurCore<CT, BR, HU, KC, X3>;
     __shared__ __attribute__((aligned(16))) char lds[Core::LDS_BYTES];
     const StepTile tl = step_tile(H / HU, B / BR);
     const int u0 = tl.u * HU, b0 = tl.b * BR, dir = tl.dir;
@@ -630,7 +631,12 @@ extern "C" int ocrk_lstm_bwd_step(const void* wh, const void* dg_in, void* dg_ou
     } else {
         OCRK_REQUIRE(H % 32 == 0 && B % 32 == 0, "ocrk_lstm_bwd_step: f32 needs H %% 32 == 0 and B %% 32 == 0");
         dim3 grid(H / 16 * (B / 32) * 2);
-        lstm_bwd_step_kernel<BWD_F32><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, (const float*)acts_t, (float*)dG_t);
+        // fp32 BPTT: exact f32 MFMA in exact mode, else the bf16x3 split (the fp32 Trainer's
+        // recurrent layers outside its conv tower, kernels.f32_exact)
+        if (ocrk::f32_exact_mfma())
+            lstm_bwd_step_kernel<BWD_F32><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, (const float*)acts_t, (float*)dG_t);
+        else
+            lstm_bwd_step_kernel<BWD_F32, true><<<grid, 256, 0, st>>>((const float*)wh, (const float*)dg_in, (float*)dg_out, dc_state, seq_len, s, T, B, H, (const float*)dout, cprev_t, (const float*)acts_t, (float*)dG_t);
     }
     return ocrk::launch_status("ocrk_lstm_bwd_step");
 }

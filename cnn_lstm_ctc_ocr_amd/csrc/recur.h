@@ -7,8 +7,12 @@
 
 namespace ocrk {
 
-template <typename CT, int BR, int NC, int KC>
+// X3 (CT = float): each fp32 fragment pair is split at the read into bf16 hi / lo
+// (split8_bf16) and multiplied as al.bh + ah.bl + ah.bh on the bf16 MFMA (the
+// fp32 loops outside exact mode, kernels.f32_exact); else exact f32 MFMA.
+template <typename CT, int BR, int NC, int KC, bool X3 = false>
 struct RecurCore {
+    static_assert(!X3 || sizeof(CT) == 4, "the split is of fp32 operands");
     using RT = typename RawT<CT>::T;
     static constexpr int LDK = KC + 8;
     static constexpr int NVA = (BR * KC / 8 + 255) / 256;
@@ -74,6 +78,20 @@ struct RecurCore {
                     bf16x8 af = *reinterpret_cast<const bf16x8*>(a + ks * 32);
                     bf16x8 bfr = *reinterpret_cast<const bf16x8*>(b + ks * 32);
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i], 0, 0, 0);
+                } else if constexpr (X3) {
+                    // the bf16 MFMA's operand layout is this staging's: lane group g holds
+                    // k = 32 ks + 8 g .. + 7 of its row
+                    V8<float> af, bfr;
+                    vload_lds(af, a + ks * 32);
+                    vload_lds(bfr, b + ks * 32);
+                    u32x4 ah, al, bh, bl;
+                    split8_bf16(af, ah, al);
+                    split8_bf16(bfr, bh, bl);
+                    const bf16x8 ahb = __builtin_bit_cast(bf16x8, ah), alb = __builtin_bit_cast(bf16x8, al);
+                    const bf16x8 bhb = __builtin_bit_cast(bf16x8, bh), blb = __builtin_bit_cast(bf16x8, bl);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alb, bhb, acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahb, blb, acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahb, bhb, acc[i], 0, 0, 0);
                 } else {
                     V8<float> af, bfr;
                     vload_lds(af, a + ks * 32);

@@ -182,6 +182,31 @@ extern "C" int ocrk_cast(const void* in, int in_dtype, void* out, int out_dtype,
     return ocrk::launch_status("ocrk_cast");
 }
 
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (RNE; |x - hi - lo| <= 2^-17 |x|):
+// the bf16x3 split as two bf16 planes, so a bf16 GEMM engine can form
+// ah.bh + ah.bl + al.bh in three accumulating calls. 8 elements per thread.
+__global__ void split_bf16_kernel(const float* __restrict__ x, unsigned* __restrict__ hi, unsigned* __restrict__ lo,
+                                  int64_t n8) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = reinterpret_cast<const float4*>(x)[2 * i], b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+        unsigned h[4], l[4];
+        ocrk::split2_bf16(a.x, a.y, h[0], l[0]);
+        ocrk::split2_bf16(a.z, a.w, h[1], l[1]);
+        ocrk::split2_bf16(b.x, b.y, h[2], l[2]);
+        ocrk::split2_bf16(b.z, b.w, h[3], l[3]);
+        reinterpret_cast<uint4*>(hi)[i] = make_uint4(h[0], h[1], h[2], h[3]);
+        reinterpret_cast<uint4*>(lo)[i] = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+}
+
+extern "C" int ocrk_split_bf16(const float* x, int64_t n, void* hi, void* lo, void* stream) {
+    OCRK_REQUIRE(n % 8 == 0 && ((uintptr_t)x | (uintptr_t)hi | (uintptr_t)lo) % 16 == 0,
+                 "ocrk_split_bf16: n=%lld must be a multiple of 8 and the buffers 16-B aligned", (long long)n);
+    if (n == 0) return OCRK_OK;
+    split_bf16_kernel<<<grid1d(n / 8), 256, 0, ocrk::as_stream(stream)>>>(x, (unsigned*)hi, (unsigned*)lo, n / 8);
+    return ocrk::launch_status("ocrk_split_bf16");
+}
+
 extern "C" int ocrk_permute3(const void* in, int in_dtype, int d0, int d1, int d2, void* out, int out_dtype,
                              void* stream) {
     int64_t n = (int64_t)d0 * d1 * d2;

@@ -609,6 +609,25 @@ def gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=None, defer=Non
 
 
 # ----------------------------------------------------------------- misc
+def split_bf16(x):
+    """(hi, lo) bf16 planes of an fp32 tensor: x = hi + lo to 2^-17 (ocrk_split_bf16)."""
+    _chk(x)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise TypeError("split_bf16 takes a contiguous float32 tensor")
+    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_like(hi)
+    call("ocrk_split_bf16", ptr(x), x.numel(), ptr(hi), ptr(lo), _stream(x))
+    return hi, lo
+
+
+def split_products(*tensors):
+    """Operand sets for an fp32 product on the bf16 engines through the split:
+    [(a_hi, b_hi, ...), (a_hi, b_lo), (a_lo, b_hi)] for two operands (the al.bl
+    term, ~2^-18 relative, is dropped -- mfma_util.h split2_bf16)."""
+    a, b = (split_bf16(t) for t in tensors)
+    return [(a[0], b[0]), (a[0], b[1]), (a[1], b[0])]
+
+
 def cast(x, dtype, out=None):
     _chk(x)
     out = out if out is not None else torch.empty(x.shape, dtype=dtype, device=x.device)

@@ -64,6 +64,17 @@ def _conv_precision(exact):
     return K.f32_exact() if exact else contextlib.nullcontext()
 
 
+def _conv_wgrad(split, x, dy, dw):
+    """dw += the 3x3 conv weight gradient; split (fp32 training, mixed policy): on the
+    bf16 engines over the (hi, lo) planes of x and dy -- a leaf gradient, so the
+    split's ~2^-16 product error reaches no other gradient."""
+    if split:
+        for xa, da in K.split_products(x, dy):
+            K.conv3x3_bwd_weight(xa, da, dw)
+    else:
+        K.conv3x3_bwd_weight(x, dy, dw)
+
+
 class _ConvBlock(torch.autograd.Function):
     """conv_{2k-1} -> conv_{2k} -> BN -> ReLU -> pool (model.py:134-146)."""
 
@@ -148,7 +159,7 @@ class _ConvBlock(torch.autograd.Function):
         if k > 1:
             _issue(store, late)
             with _conv_side(store, y_odd, dz):             # overlaps the data-gradient GEMM below
-                K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
+                _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
@@ -162,11 +173,11 @@ class _ConvBlock(torch.autograd.Function):
             # and conv1's after it on this one: 6.39 vs 6.37 ms)
             with _conv_side(store, x, dy_odd):
                 K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
-            K.conv3x3_bwd_weight(y_odd, dz, G[pe + "/kernel"])
+            _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             store.join()                                   # side-stream weight gradients are in
         else:
             with _conv_side(store, x, dy_odd):
-                K.conv3x3_bwd_weight(x, dy_odd, G[po + "/kernel"])
+                _conv_wgrad(ctx.exact, x, dy_odd, G[po + "/kernel"])
             if ctx.needs_input_grad[0]:
                 _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
@@ -362,29 +373,42 @@ class _BiLSTM(torch.autograd.Function):
         with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
             gf, gb = store.grads[f"{pre}/fw/lstm_cell/kernel"], store.grads[f"{pre}/bw/lstm_cell/kernel"]
             sk = gf.numel()                                                      # [In+H, 4H] f32 each
-            dg = dG.view(R, 2 * G4)
+            # fp32 on the split (not exact mode): the same GEMMs on the bf16 engines over the
+            # (hi, lo) planes, hi.hi + hi.lo + lo.hi -- the weight gradients are leaves, so their
+            # ~2^-16 product error reaches no other gradient
+            if dt == torch.float32 and not K.f32_mode_exact():
+                xg = K.split_products(x, dG)
+                hg = K.split_products(hprev, dG)
+                passes = [(xa, ha, ga) for (xa, ga), (ha, _g) in zip(xg, hg)]
+            else:
+                passes = [(x, hprev, dG)]
             if gb.data_ptr() == gf.data_ptr() + 4 * sk:
                 # both directions as one batched GEMM each (batch = direction: dG column
                 # block d * 4H, h_prev column block d * H, gradient d * (In+H) * 4H):
                 # dW_x = x^T . dG_d ; dW_h = h_prev_d^T . dG_d  (split-K over T*B)
                 def dw_x():
-                    K.gemm(x, dg, trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
-                           ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
-                           splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer, late=True)))
-                K.gemm(hprev.view(R, 2 * H), dg, trans_a=True, out=gf[n_in:], accumulate=True, M=H, N=G4, K=R,
-                       lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4, stride_c=sk,
-                       splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
+                    for xa, _ha, ga in passes:
+                        K.gemm(xa, ga.view(R, 2 * G4), trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R,
+                               lda=n_in, ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
+                               splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer, late=True)))
+                for _xa, ha, ga in passes:
+                    K.gemm(ha.view(R, 2 * H), ga.view(R, 2 * G4), trans_a=True, out=gf[n_in:], accumulate=True,
+                           M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4,
+                           stride_c=sk, splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
                 if layer > 1 and options.get("DEFER_DWX") == 1 and ctx.needs_input_grad[0]:
                     store.deferred.append((dw_x, (x, dG)))   # issued behind the next BPTT (fewer CUs held)
                 else:
                     dw_x()
             else:
-                for d, gk in enumerate((gf, gb)):
-                    dgd = dg[:, d * G4:]                                         # view, ldb = 8H
-                    K.gemm(x, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
-                           ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R, items=_tn_items(layer)))
-                    K.gemm(hprev.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
-                           M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, splits=_splits(H, G4, R, items=_tn_items(layer)))
+                for xa, ha, ga in passes:
+                    dg = ga.view(R, 2 * G4)
+                    for d, gk in enumerate((gf, gb)):
+                        dgd = dg[:, d * G4:]                                     # view, ldb = 8H
+                        K.gemm(xa, dgd, trans_a=True, out=gk, accumulate=True, M=n_in, N=G4, K=R, lda=n_in,
+                               ldb=2 * G4, ldc=G4, splits=_splits(n_in, G4, R, items=_tn_items(layer)))
+                        K.gemm(ha.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
+                               M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4,
+                               splits=_splits(H, G4, R, items=_tn_items(layer)))
         if ctx.needs_input_grad[0] and not dx_first:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
@@ -524,8 +548,11 @@ class _Logits(torch.autograd.Function):
         R = T * B
         dpre = K.relu_mask(dlogits.contiguous(), logits, dt)                       # [T,B,C]
         with side_work(store, x, dpre):
-            K.gemm(x, dpre, trans_a=True, out=store.grads["rnn/logits/kernel"], accumulate=True,
-                   M=D, N=C, K=R, lda=D, ldb=C, ldc=C, splits=_splits(D, C, R))
+            # fp32 on the split: the leaf gradient on the bf16 engines (as the recurrent dW)
+            split = dt == torch.float32 and not K.f32_mode_exact() and x.numel() % 8 == 0 and dpre.numel() % 8 == 0
+            for xa, pa in (K.split_products(x, dpre) if split else [(x, dpre)]):
+                K.gemm(xa, pa, trans_a=True, out=store.grads["rnn/logits/kernel"], accumulate=True,
+                       M=D, N=C, K=R, lda=D, ldb=C, ldc=C, splits=_splits(D, C, R))
             K.colsum(dpre, R, C, store.grads["rnn/logits/bias"])
         dx = None
         if ctx.needs_input_grad[0]:

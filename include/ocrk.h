@@ -89,7 +89,7 @@ const char* ocrk_last_error(void);
  * ocrk_set_option changes it (process-wide, takes effect at the next launch; the
  * "OCRK_" prefix is optional in `name`). Names: CONV_DIRECT, CONV_ROWS,
  * CONV_ROWS_WIDE, CONV_WGRAD_BLOCKS, LSTM_SPIN_LIMIT, PERSIST_LATE,
- * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP (meanings in
+ * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP, NT_F32_EXACT (meanings in
  * csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
 
@@ -99,6 +99,13 @@ int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
  * main stream (the weight gradients beside the data gradients; option
  * SIDE_CU_MASK). Released with ocrk_stream_destroy. No reference counterpart. */
 int ocrk_stream_create_cu_limited(int n_cus, void** stream);
+
+/* x = hi + lo, hi = bf16(x), lo = bf16(x - hi) (round to nearest even; |x - hi - lo| <=
+ * 2^-17 |x|): the bf16x3 split as two bf16 planes [n], so the bf16 GEMM engines form an
+ * fp32 product as hi.hi + hi.lo + lo.hi in three accumulating calls (the fp32 training
+ * step's weight gradients, train.Trainer). n % 8 == 0, 16-B aligned buffers.
+ * No reference counterpart (TF1 multiplies float32 directly). */
+int ocrk_split_bf16(const float* x, int64_t n, void* hi, void* lo, void* stream);
 int ocrk_stream_destroy(void* stream);
 int ocrk_get_option(const char* name, int64_t* value);
 

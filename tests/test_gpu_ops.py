@@ -112,6 +112,41 @@ def test_conv3x3_fwd_bwd(cuda, cin, cout, relu):
     np.testing.assert_allclose(dw.cpu().numpy(), dw_ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("B,H,W,cin,cout", [(4, 15, 127, 64, 64), (4, 7, 126, 128, 128), (6, 3, 125, 256, 256),
+                                             (3, 5, 9, 64, 32)])
+def test_f32_exact_conv_on_nt_ring(cuda, ocrk_opts, B, H, W, cin, cout):
+    """Exact-mode fp32 convolutions (the fp32 Trainer's conv tower) on the NT
+    ring's EXACT variant (v_mfma_f32_16x16x4_f32, option NT_F32_EXACT) against
+    the float64 graph and against the generic engine (NT_F32_EXACT=0): forward
+    with the BN-statistics epilogue, and the unmasked data gradient."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(B * cin + W)
+    x = rng.standard_normal((B, H, W, cin)).astype(np.float32)
+    w = (rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    z = G.conv2d(x.astype(np.float64), w.astype(np.float64), b.astype(np.float64), "same")
+    dy = rng.standard_normal(z.shape).astype(np.float32)
+    dx_ref, _, _ = G.conv2d_bwd(x.astype(np.float64), w.astype(np.float64), dy.astype(np.float64), "same")
+    w_nk = Kn.permute3(_t(w, cuda), 9 * cin, cout, 1, torch.float32).view(cout, 9 * cin)
+    w_bwd = Kn.permute3(_t(w, cuda), 9, cin, cout, torch.float32).view(cin, 9 * cout)
+    M = B * H * W
+    outs = {}
+    for mode in (1, 0):
+        ocrk_opts("NT_F32_EXACT", mode)
+        with Kn.f32_exact():
+            stats = torch.empty(Kn.conv_stats_tiles(M), 2, cout, device=cuda)
+            y = Kn.conv3x3_fwd(_t(x, cuda), w_nk, _t(b, cuda), False, stats=stats)
+            dx = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd)
+            mean, _ = Kn.bn_finalize(stats, M, cout, 1e-3, 0.99)
+        torch.cuda.synchronize()
+        outs[mode] = (y.cpu().numpy(), dx.cpu().numpy(), mean.cpu().numpy())
+        rel = lambda a, r: float(np.linalg.norm(a - r) / np.linalg.norm(r))   # noqa: E731
+        assert rel(outs[mode][0], z) < 2e-6, (mode, rel(outs[mode][0], z))   # exact fp32 products
+        assert rel(outs[mode][1], dx_ref) < 2e-6, (mode, rel(outs[mode][1], dx_ref))
+        np.testing.assert_allclose(outs[mode][2], z.reshape(-1, cout).mean(0), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-5)
+
+
 # W = 11 / 37: one / several 8-window column segments of the window-centric
 # routing pass, an odd width leaves an uncovered column for the 2x2/[2,2]
 # pool, H = 7 an uncovered row for the 2-row pools.
