@@ -377,9 +377,8 @@ class _BiLSTM(torch.autograd.Function):
             # (hi, lo) planes, hi.hi + hi.lo + lo.hi -- the weight gradients are leaves, so their
             # ~2^-16 product error reaches no other gradient
             if dt == torch.float32 and not K.f32_mode_exact():
-                xg = K.split_products(x, dG)
-                hg = K.split_products(hprev, dG)
-                passes = [(xa, ha, ga) for (xa, ga), (ha, _g) in zip(xg, hg)]
+                (xh, xl), (hh, hl), (gh, gl) = K.split_bf16(x), K.split_bf16(hprev), K.split_bf16(dG)
+                passes = [(xh, hh, gh), (xh, hh, gl), (xl, hl, gh)]          # hi.hi + hi.lo + lo.hi
             else:
                 passes = [(x, hprev, dG)]
             if gb.data_ptr() == gf.data_ptr() + 4 * sk:
