@@ -103,6 +103,9 @@ SIGNATURES = {
     "ocrk_lstm_fwd_persistent_f32_workspace_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_f32_flags_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_f32": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
+    "ocrk_lstm_bwd_persistent_f32_supported": [_i32, _i32],
+    "ocrk_lstm_bwd_persistent_f32_workspace_size": [_i32, _i32],
+    "ocrk_lstm_bwd_persistent_f32": [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_bwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_bwd_persistent_workspace_size": [_i32, _i32],
     "ocrk_lstm_bwd_persistent_slices": [_i32, _i32],

@@ -255,6 +255,266 @@ static int x3_rows(int B, int H) {
     return 0;
 }
 
+// ---------------------------------------------------------------- backward
+// The fp32 BPTT as ONE persistent launch per layer on the same split: member
+// (direction, 32-row batch slice, 32 units) of the gather form (grid B), 8 waves:
+// wave w takes gate w >> 1 and k-half w & 1 (256 of the gate's 512 dz columns),
+// its W_h slice [32 units][256 k] split once into resident hi / lo B fragments
+// (2 N-tiles x 8 k-steps x 2 planes = 128 VGPRs). Per reverse step a member
+//   1. waits until the group published dz_{i-1} (flag words, bounded spin);
+//   2. stages ITS 16 rows x 256 columns of dz_{i-1} hi and lo (16 LDS-DMA wave
+//      instructions of two unpadded 512-B rows, 16-B pieces XOR-swizzled by row
+//      on the global side) for M-tile 0, multiplies them (3 bf16 MFMAs per
+//      product), then the same rows 16-31 into the same 16 KB for M-tile 1:
+//      the two planes of 32 rows (32 KB per wave) do not fit beside each other
+//      in LDS, so the tiles are staged in turn; the cell's operands (acts,
+//      c_prev, dout: fp32) ride behind the first tile's DMA;
+//   3. the eight K-slice partials meet in LDS (each wave's own staging region,
+//      free after its MFMAs) and are summed in a fixed order;
+//   4. the cell's gradient in fp32 (2 units of one row per thread), dc kept in
+//      registers, bias partials summed over the steps;
+//   5. publishes dz as its hi / lo split (4-B stores per plane), drains,
+//      barriers, one lane raises the member flag; writes dz (fp32) in time order.
+// Hand-off form, census and counting flags: persist.h's, as every loop here.
+__global__ void __launch_bounds__(512, 1)
+lstm_bwd_persistent_f32x3_kernel(const float* __restrict__ wh, unsigned short* __restrict__ dzx,
+                                 const int* __restrict__ seq_len, int T, int B, const float* __restrict__ dout,
+                                 const float* __restrict__ cprev_t, const float* __restrict__ acts_t,
+                                 float* __restrict__ dG_t, unsigned* __restrict__ flags, unsigned* __restrict__ err,
+                                 unsigned spin_limit, float* __restrict__ bpart) {
+    constexpr int H = 32 * X3_KS, G4 = 4 * H;
+    constexpr int RB = PBR, UM = PHU;                   // 32 rows x 32 units per member
+    constexpr int NU = H / UM;                          // members per group (16)
+    constexpr int KW = 256, KSW = KW / 32;              // k columns / k-steps per wave
+    constexpr int REG = 2 * 16 * KW;                    // elements per wave region: [plane][16 rows][256]
+    constexpr int LDP = UM + 4;                         // partial row pitch (floats)
+    static_assert(RB * LDP * 4 <= REG * 2, "the partials fit the wave's staging region");
+    __shared__ __attribute__((aligned(16))) unsigned short sA[8 * REG];
+
+    int group, member;
+    persistent_role(2 * (B / RB), NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * UM, b0 = bs * RB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const int kbase = (w >> 1) * H + (w & 1) * KW;
+    gu32* gflags = (gu32*)(flags) + group * NU;
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
+
+    // resident B fragments, split once: N-tile j = units u0 + 16 j + c; k = kbase + 32 ks + 8 g
+    bf16x8 bh[2][KSW], bl[2][KSW];
+    const float* wdir = wh + (size_t)dir * H * G4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const float* row = wdir + (size_t)(u0 + 16 * j + c) * G4 + kbase + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KSW; ++ks) {
+            V8<float> v;
+            vload(v, row + ks * 32);
+            u32x4 hi, lo;
+            split8_bf16(v, hi, lo);
+            bh[j][ks] = __builtin_bit_cast(bf16x8, hi);
+            bl[j][ks] = __builtin_bit_cast(bf16x8, lo);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KSW; ++ks) asm volatile("" ::"v"(bh[j][ks]), "v"(bl[j][ks]));   // settled before the loop
+
+    // the cell item: row er, units eu, eu + 1 (all 4 gates)
+    const int er = tid >> 4, eu = 2 * (tid & 15);
+    const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));
+    float dcs[2] = {0.f, 0.f};
+    float bsum[4][2] = {};
+    const int64_t plane = (int64_t)2 * 2 * B * G4;      // elements per exchange plane ([parity][dir][B][4H])
+    auto zx_rsrc = __builtin_amdgcn_make_buffer_rsrc(dzx, 0, (int)(2 * plane * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t act_rsrc = uniform_rsrc(acts_t, (int64_t)T * B * 2 * G4 * 4);
+    const __amdgpu_buffer_rsrc_t cp_rsrc = uniform_rsrc(cprev_t, (int64_t)T * B * 2 * H * 4);
+    const __amdgpu_buffer_rsrc_t do_rsrc = uniform_rsrc(dout, (int64_t)T * B * 2 * H * 4);
+    // DMA lane geometry: instruction d covers rows 2d, 2d + 1 of a 16-row tile;
+    // lane l writes row 2d + (l >> 5), slot l & 31, fetching the global 16-B piece
+    // (l & 31) ^ (row & 15) of that row's wave columns
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    unsigned short* sa = sA + wu * REG;
+    unsigned dma_off[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const int r = 2 * d + (lane >> 5);
+        dma_off[d] = (unsigned)((r * G4 + kbase + 8 * ((lane & 31) ^ (r & 15))) * 2);
+    }
+    typedef __attribute__((address_space(3))) void* lds_p;
+
+    for (int i = 0; i < T; ++i) {
+        const int s = T - 1 - i;
+        const bool valid = s < elen;
+        const int t = step_time(dir, s, elen);
+        const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+        f32x2_t la[4], lcp, ldo;
+        auto load_late = [&]() {                        // 6 buffer loads
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                la[k] = __builtin_bit_cast(
+                    f32x2_t, __builtin_amdgcn_raw_buffer_load_b64(act_rsrc, (int)((tb * G4 + k * H + u0 + eu) * 4), 0, 0));
+            lcp = __builtin_bit_cast(f32x2_t, __builtin_amdgcn_raw_buffer_load_b64(cp_rsrc, (int)((tb * H + u0 + eu) * 4), 0, 0));
+            ldo = __builtin_bit_cast(f32x2_t, __builtin_amdgcn_raw_buffer_load_b64(
+                do_rsrc, (int)((((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu) * 4), 0, 0));
+        };
+        floatx4 acc[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[m][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (i > 0) {
+            // 1. wait until every member of the group published dz_{i-1} (flag >= base + i)
+            if (w == 0) {
+                unsigned spins = 0;
+                while (true) {
+                    unsigned f = base + (unsigned)i;
+                    if (lane < NU) f = poll_word(gflags + lane, local);
+                    if (__all(reached(f, base + (unsigned)i))) break;
+                    poll_pause();
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_BWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            const unsigned rb0 = (unsigned)(((int64_t)(((i - 1) & 1) * 2 + dir) * B + b0) * G4 * 2);
+            // 2. the two 16-row M-tiles of this wave's 256 columns, hi and lo planes, in turn
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const unsigned rbm = rb0 + (unsigned)(16 * m * G4 * 2);
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) {
+                    const unsigned poff = rbm + (unsigned)(pl * plane * 2);
+                    if (local) {
+#pragma unroll
+                        for (int d = 0; d < 8; ++d)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(zx_rsrc, (lds_p)(sa + pl * 16 * KW + d * 2 * KW), 16,
+                                                                     poff + dma_off[d], 0, 0, 2);
+                    } else {
+#pragma unroll
+                        for (int d = 0; d < 8; ++d)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(zx_rsrc, (lds_p)(sa + pl * 16 * KW + d * 2 * KW), 16,
+                                                                     poff + dma_off[d], 0, 0, 16);
+                    }
+                }
+                asm volatile("" ::: "memory");
+                if (m == 0) {
+                    load_late();                                 // 6 loads behind the first tile's 16 DMAs
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int ks = 0; ks < KSW; ++ks) {
+                    const int so = c * KW + 8 * ((4 * ks + g) ^ c);
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&sa[so]);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&sa[16 * KW + so]);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j][ks], acc[m][j], 0, 0, 0);
+                        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j][ks], acc[m][j], 0, 0, 0);
+                        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j][ks], acc[m][j], 0, 0, 0);
+                    }
+                }
+                // the tile's reads are in registers before the next tile's DMA into the same bytes
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else {
+            load_late();
+        }
+        // 3. the eight partials meet in LDS (each wave's own region): lane (c, g) holds
+        //    rows 16 m + 4 g + r of units 16 j + c
+        float* sP = reinterpret_cast<float*>(sa);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sP[(16 * m + 4 * g + r) * LDP + 16 * j + c] = acc[m][j][r];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the cell's operands landed
+        __syncthreads();
+
+        // 4. the cell's gradient for (row er, units eu, eu + 1)
+        float dz[4][2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float p[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) p[q] = reinterpret_cast<const float*>(sA + q * REG)[er * LDP + eu + e];
+            const float dh = (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) + ldo[e];
+            const float ai = la[0][e], aj = la[1][e], af = la[2][e], ao = la[3][e];
+            const float cp = lcp[e];
+            const float cc = af * cp + ai * aj;
+            const float tc = tanh_fast(cc);
+            const float dc = dcs[e] + dh * ao * (1.f - tc * tc);
+            dz[3][e] = valid ? dh * tc * ao * (1.f - ao) : 0.f;
+            dz[0][e] = valid ? dc * aj * ai * (1.f - ai) : 0.f;
+            dz[1][e] = valid ? dc * ai * (1.f - aj * aj) : 0.f;
+            dz[2][e] = valid ? dc * cp * af * (1.f - af) : 0.f;
+            dcs[e] = valid ? dc * af : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bsum[k][0] += dz[k][0];
+            bsum[k][1] += dz[k][1];
+        }
+        // 5. publish dz as hi / lo (4-B stores per plane and gate), drain, barrier, flag
+        {
+            const int64_t zbase = ((int64_t)((i & 1) * 2 + dir) * B + b0 + er) * G4 + u0 + eu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                unsigned hi, lo;
+                split2_bf16(dz[k][0], dz[k][1], hi, lo);
+                put4((gu32*)(dzx + zbase + k * H), hi, local);
+                put4((gu32*)(dzx + plane + zbase + k * H), lo, local);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                                 // every wave's partial reads done before the next DMA
+        if (tid == 0) raise_flag(gflags + member, base + (unsigned)(i + 1), local);
+        // the time-order copy for the weight-gradient and data-gradient GEMMs (drains behind the next step)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<f32x2_t*>(dG_t + tb * G4 + k * H + u0 + eu) = f32x2_t{dz[k][0], dz[k][1]};
+    }
+    // bias partials of this 32-row slice: the rows of every (gate, unit) meet in LDS
+    if (bpart) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(sA);       // [row][4 gates x 32 units], free after the loop
+        constexpr int LDR = 4 * UM + 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            red[er * LDR + k * UM + eu] = bsum[k][0];
+            red[er * LDR + k * UM + eu + 1] = bsum[k][1];
+        }
+        __syncthreads();
+        if (tid < 4 * UM) {
+            float sum = 0.f;
+            for (int r = 0; r < RB; ++r) sum += red[r * LDR + tid];
+            bpart[(int64_t)(bs * 2 + dir) * G4 + (tid / UM) * H + u0 + (tid % UM)] = sum;
+        }
+    }
+}
+
+static bool x3_bwd_fits(int B, int H) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (B % PBR || H != 32 * X3_KS) return false;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_f32x3_kernel, X3_THREADS, 0) !=
+        hipSuccess)
+        return false;
+    return 2L * (B / PBR) * (H / PHU) <= (long)cus * per_cu;
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" size_t ocrk_lstm_fwd_persistent_f32_workspace_size(int B, int H) {
     // flag word + XCC word per workgroup at 16-row slices (the larger count; 128-B block),
@@ -301,4 +561,39 @@ extern "C" int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, c
         lstm_fwd_persistent_f32x3_kernel<32><<<grid, X3_THREADS, 0, st>>>(gx, whT, hx, seq_len, T, B, out, hprev_t,
                                                                          cprev_t, acts_t, cnt, err, recur_spin_limit());
     return ocrk::launch_status("ocrk_lstm_fwd_persistent_f32");
+}
+
+// the fp32 BPTT on the split (exact mode keeps the per-step exact kernels)
+extern "C" int ocrk_lstm_bwd_persistent_f32_supported(int B, int H) {
+    if (B <= 0 || H != 32 * X3_KS) return 0;
+    return x3_bwd_fits(B, H) ? 1 : 0;
+}
+
+extern "C" size_t ocrk_lstm_bwd_persistent_f32_workspace_size(int B, int H) {
+    // the gather form's counters (persist.h), then the hi / lo dz exchange planes [2 planes][2 parities][2 dirs][B][4H] bf16
+    if (B <= 0 || B % PBR || H != 32 * X3_KS) return 0;
+    return persistent_counter_bytes(B, H) + (size_t)2 * 2 * 2 * B * 4 * H * sizeof(unsigned short);
+}
+
+extern "C" int ocrk_lstm_bwd_persistent_f32(const float* wh, const int* seq_len, int T, int B, int H,
+                                            const float* dout, const float* cprev_t, const float* acts_t, float* dG_t,
+                                            unsigned* err, unsigned* flags, float* dbias_part, void* ws,
+                                            size_t ws_bytes, void* stream) {
+    OCRK_REQUIRE(ocrk_lstm_bwd_persistent_f32_supported(B, H),
+                 "ocrk_lstm_bwd_persistent_f32: B=%d H=%d unsupported or not co-resident", B, H);
+    OCRK_REQUIRE(ws_bytes >= ocrk_lstm_bwd_persistent_f32_workspace_size(B, H),
+                 "ocrk_lstm_bwd_persistent_f32: workspace too small");
+    OCRK_REQUIRE(wh && seq_len && dout && cprev_t && acts_t && dG_t && err, "ocrk_lstm_bwd_persistent_f32: null operand");
+    OCRK_REQUIRE((int64_t)T * B * 8 * H * 4 < 0x7fffffffll, "ocrk_lstm_bwd_persistent_f32: acts exceed 2 GB");
+    OCRK_REQUIRE(T >= 1, "ocrk_lstm_bwd_persistent_f32: T=%d", T);
+    hipStream_t st = ocrk::as_stream(stream);
+    const size_t counters = persistent_counter_bytes(B, H);      // flags: ocrk_persistent_flags_size's buffer
+    unsigned* cnt = flags ? flags : (unsigned*)ws;
+    unsigned short* zx = (unsigned short*)((char*)ws + counters);
+    if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
+        return ocrk::launch_status("ocrk_lstm_bwd_persistent_f32 memset");
+    const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
+    lstm_bwd_persistent_f32x3_kernel<<<grid, X3_THREADS, 0, st>>>(wh, zx, seq_len, T, B, dout, cprev_t, acts_t, dG_t,
+                                                                  cnt, err, recur_spin_limit(), dbias_part);
+    return ocrk::launch_status("ocrk_lstm_bwd_persistent_f32");
 }

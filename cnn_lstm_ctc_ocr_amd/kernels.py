@@ -427,6 +427,19 @@ def lstm_f32_persistent_ok(B, H):
     return _PERSISTENT[key]
 
 
+def lstm_f32_bwd_persistent_ok(B, H):
+    """Run the fp32 BPTT as one persistent launch on the bf16x3 split
+    (csrc/lstm_f32x3.hip)? H = 512, B % 32 == 0 and the B-workgroup grid
+    co-resident; not in exact fp32 mode; OCRK_LSTM_PERSISTENT=0 selects the
+    per-step fp32 kernels."""
+    if not options.get("LSTM_PERSISTENT") or f32_mode_exact():
+        return False
+    key = ("f32bwd", B, H)
+    if key not in _PERSISTENT:
+        _PERSISTENT[key] = bool(_lib.lib().ocrk_lstm_bwd_persistent_f32_supported(B, H))
+    return _PERSISTENT[key]
+
+
 def lstm_fwd(gx, whT, seq_len, T, B, H, dtype, save=True):
     """One bidirectional LSTM layer's time loop. Returns (out, hprev, cprev, acts);
     save=False (no backward will run): the fp32 persistent loop skips the saved
@@ -512,6 +525,16 @@ def lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=None, defer=None):
     dtype = dout.dtype
     dev = dout.device
     dG = torch.empty(T, B, 2, 4 * H, dtype=dtype, device=dev)
+    if dtype == torch.float32 and lstm_f32_bwd_persistent_ok(B, H):
+        nb = _lib.lib().ocrk_lstm_bwd_persistent_f32_workspace_size(B, H)
+        ws = _ws(nb, dev)
+        part = torch.empty(B // 32, 2 * 4 * H, dtype=torch.float32, device=dev) if dbias is not None else None
+        call("ocrk_lstm_bwd_persistent_f32", ptr(wh), ptr(seq_len), T, B, H, ptr(dout), ptr(cprev), ptr(acts),
+             ptr(dG), ptr(lstm_error_word(dev)), ptr(persistent_flags("lstm_bwd_f32", B, H, dev)), ptr(part),
+             ptr(ws), nb, _stream(dout))
+        if dbias is not None:
+            _bias_parts(part, B // 32, 2 * 4 * H, dbias, defer)
+        return dG
     if lstm_persistent_ok(B, H, dtype):
         nb = _lib.lib().ocrk_lstm_bwd_persistent_workspace_size(B, H)
         ws = _ws(nb, dev)

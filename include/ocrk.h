@@ -330,6 +330,18 @@ size_t ocrk_lstm_fwd_persistent_f32_flags_size(int B, int H);
 int ocrk_lstm_fwd_persistent_f32(const float* gx, const float* whT, const int* seq_len, int T, int B, int H,
                                  float* out, float* hprev_t, float* cprev_t, float* acts_t, unsigned* err,
                                  unsigned* flags, void* ws, size_t ws_bytes, void* stream);
+/* a7' BPTT in fp32 on the same split: one persistent launch per layer, members
+ * (direction, 32-row slice, 32 units) of 8 waves (gate x k-half), W_h hi / lo resident,
+ * dz exchanged as hi / lo bf16 planes. wh f32 [2][H][4H]; dout / cprev_t f32
+ * [T][B][2][H] (dout as [T][B][2H]); acts_t / dG_t f32 [T][B][2][4H]; dbias_part f32
+ * [B/32][2][4H] (or NULL). H = 512, B % 32 == 0, the B-workgroup grid co-resident;
+ * flags: ocrk_persistent_flags_size(B, H). Not used in exact fp32 mode (the per-step
+ * exact kernels of ocrk_lstm_bwd_step). */
+int ocrk_lstm_bwd_persistent_f32_supported(int B, int H);
+size_t ocrk_lstm_bwd_persistent_f32_workspace_size(int B, int H);
+int ocrk_lstm_bwd_persistent_f32(const float* wh, const int* seq_len, int T, int B, int H, const float* dout,
+                                 const float* cprev_t, const float* acts_t, float* dG_t, unsigned* err,
+                                 unsigned* flags, float* dbias_part, void* ws, size_t ws_bytes, void* stream);
 int ocrk_lstm_bwd_persistent_supported(int B, int H);
 /* Rows of dbias_part the BPTT launch writes: B/16 when it runs the 16-row / 64-unit
  * member form (H = 512, its B-workgroup grid co-resident; 64 KB of dz gathered per CU

@@ -271,3 +271,56 @@ def test_f32_persistent_fwd_matches_oracle_and_step_kernels(cuda, ocrk_opts, T, 
     assert h2 is None and c2 is None and a2 is None
     assert torch.equal(o2, pers[0])
     K._PERSISTENT.clear()
+
+
+@pytest.mark.parametrize("T,B,n_in", [(19, 64, 64), (11, 96, 32), (23, 256, 256)])
+def test_f32_persistent_bwd_matches_oracle_and_step_kernels(cuda, ocrk_opts, T, B, n_in):
+    """The fp32 BPTT loop (csrc/lstm_f32x3.hip: one persistent launch, dz.W_h^T on
+    the bf16x3 split, dz exchanged as hi / lo planes) against the float64
+    oracle's BPTT and the per-step fp32 kernels on the same saved tensors:
+    dG <= 5e-5 relative, invalid steps exactly zero, the fused bias partials
+    (B/32 slices) against the column sums of its own dG and the oracle's."""
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    H = 512
+    rng = np.random.default_rng(41 + B)
+    x = rng.standard_normal((T, B, n_in)).astype(np.float32)
+    ks = [(rng.standard_normal((n_in + H, 4 * H)) * 0.05).astype(np.float32) for _ in range(2)]
+    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
+    seq = rng.integers(1, T + 1, B).astype(np.int32)
+    seq[:4] = [T, 1, T - 1, 2]
+    caches = [G.lstm_dir_fwd(x.astype(np.float64), seq, ks[d].astype(np.float64), bs[d].astype(np.float64),
+                             d == 1)[1] for d in range(2)]
+    gx = torch.from_numpy((np.einsum("tbi,dig->tbdg", x.astype(np.float64),
+                                     np.stack([k[:n_in] for k in ks]).astype(np.float64)) +
+                           np.stack(bs)[None, None]).astype(np.float32)).to(cuda).reshape(T * B, 8 * H)
+    whT = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))).to(cuda)
+    wh = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:] for k in ks]))).to(cuda)
+    seq_d = torch.from_numpy(seq).to(cuda)
+    K._PERSISTENT.clear()
+    assert K.lstm_f32_bwd_persistent_ok(B, H)
+    K.lstm_error_word(cuda).zero_()
+    _, _, cprev, acts = K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.float32)
+    dout_np = rng.standard_normal((T, B, 2 * H)).astype(np.float32)
+    dout = torch.from_numpy(dout_np).to(cuda)
+    dbs = []
+
+    def run():
+        db = torch.zeros(2 * 4 * H, device=cuda)
+        dbs.append(db)
+        return K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H, dbias=db)
+
+    dstep, dpers = _both(K, ocrk_opts, run)
+    assert K.lstm_error_word(cuda).item() == 0
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))   # noqa: E731
+    dz_ref = _bptt_ref(caches, [k.astype(np.float64) for k in ks], dout_np.astype(np.float64), T, B, H, n_in)
+    got, ref_step = dpers.cpu().numpy(), dstep.cpu().numpy()
+    print(f"fp32 BPTT dz rel err: persistent {rel(got, dz_ref):.3e} per-step {rel(ref_step, dz_ref):.3e} "
+          f"between {rel(got, ref_step):.3e}")
+    assert rel(got, dz_ref) < 5e-5
+    assert rel(got, ref_step) < 5e-5
+    for b in range(B):                                          # steps past a row's length: exact zeros
+        assert np.all(got[seq[b]:, b] == 0)
+    db_step, db_pers = dbs
+    assert rel(db_pers.cpu().numpy(), dpers.sum(dim=(0, 1)).reshape(-1).cpu().numpy()) < 1e-5
+    assert rel(db_pers.cpu().numpy(), dz_ref.sum(axis=(0, 1)).reshape(-1)) < 5e-5
+    assert rel(db_pers.cpu().numpy(), db_step.cpu().numpy()) < 5e-5
