@@ -271,7 +271,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         return;
     }
     const float* bias = p.bias ? p.bias + zb * p.strideBias : nullptr;
-    const bf16* mask = reinterpret_cast<const bf16*>(p.mask);   // bf16 path only (F32: no mask, gemm_nt)
+    const bf16* mask = reinterpret_cast<const bf16*>(p.mask);   // the C type's ReLU mask (F32: fp32, unstaged)
+    const float* maskf = reinterpret_cast<const float*>(p.mask);
     float* Cf = reinterpret_cast<float*>(p.C) + zb * p.strideC;
     bf16* Cb = reinterpret_cast<bf16*>(p.C) + zb * p.strideC;
     // Staged epilogue (bf16 C): the tile goes through LDS (pitch TP bytes, after
@@ -309,7 +310,11 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
                         if (p.relu) v = fmaxf(v, 0.f);
                         *e = (bf16)v;
                     } else {
-                        if (mask && !((float)mask[(int64_t)row * p.ldmask + col] > 0.f)) v = 0.f;
+                        if constexpr (F32) {
+                            if (maskf && !(maskf[(int64_t)row * p.ldmask + col] > 0.f)) v = 0.f;
+                        } else {
+                            if (mask && !((float)mask[(int64_t)row * p.ldmask + col] > 0.f)) v = 0.f;
+                        }
                         if (p.relu) v = fmaxf(v, 0.f);
                         const int64_t off = (int64_t)row * p.ldc + col;
                         if (p.c_bf16) {
@@ -501,14 +506,16 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
     if (!gemm_nt_enabled() || bmode != B_NK) return -1;
     if (dtype == OCRK_F32) {
         // fp32: the bf16x3 split on this ring (the generic engine keeps the short-K
-        // shapes, the masked data gradients and OCRK_F32_MFMA=1)
+        // shapes and OCRK_F32_MFMA=1)
         // (K >= 256 here: the first recurrent layer's input projection, K = 256, ran 3x
         // slower on the generic engine's bf16x3 staging -- 463 vs ~150 us per C5 bucket)
         // exact mode (the fp32 Trainer's conv tower): the implicit-GEMM convolutions on this
         // ring with exact f32 products (option NT_F32_EXACT=0: the generic engine)
         const bool exact = f32_exact_mfma();
         if (exact && (amode == A_ROWK || !opt(OPT_NT_F32_EXACT))) return -1;
-        if (p0.c_bf16 || p0.mask || p0.K % 4 != 0 || (p0.k_chunk < 256 && p0.N > 64)) return -1;
+        // (a ReLU mask -- the masked data gradients -- is fp32 here and read unstaged)
+        if (p0.c_bf16 || (p0.mask && !opt(OPT_NT_F32_MASK)) || p0.K % 4 != 0 || (p0.k_chunk < 256 && p0.N > 64))
+            return -1;
         GemmParams p = p0;
         p.epi_staged = 0;
         if (amode == A_ROWK) {

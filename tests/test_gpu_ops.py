@@ -118,7 +118,9 @@ def test_f32_exact_conv_on_nt_ring(cuda, ocrk_opts, B, H, W, cin, cout):
     """Exact-mode fp32 convolutions (the fp32 Trainer's conv tower) on the NT
     ring's EXACT variant (v_mfma_f32_16x16x4_f32, option NT_F32_EXACT) against
     the float64 graph and against the generic engine (NT_F32_EXACT=0): forward
-    with the BN-statistics epilogue, and the unmasked data gradient."""
+    with the BN-statistics epilogue, the unmasked data gradient, and the masked
+    one (the ReLU mask of the producing layer, fp32, in the epilogue) with the
+    producing layer's fused bias gradient."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     rng = np.random.default_rng(B * cin + W)
     x = rng.standard_normal((B, H, W, cin)).astype(np.float32)
@@ -127,6 +129,7 @@ def test_f32_exact_conv_on_nt_ring(cuda, ocrk_opts, B, H, W, cin, cout):
     z = G.conv2d(x.astype(np.float64), w.astype(np.float64), b.astype(np.float64), "same")
     dy = rng.standard_normal(z.shape).astype(np.float32)
     dx_ref, _, _ = G.conv2d_bwd(x.astype(np.float64), w.astype(np.float64), dy.astype(np.float64), "same")
+    mask = rng.standard_normal(x.shape).astype(np.float32)
     w_nk = Kn.permute3(_t(w, cuda), 9 * cin, cout, 1, torch.float32).view(cout, 9 * cin)
     w_bwd = Kn.permute3(_t(w, cuda), 9, cin, cout, torch.float32).view(cin, 9 * cout)
     M = B * H * W
@@ -137,9 +140,14 @@ def test_f32_exact_conv_on_nt_ring(cuda, ocrk_opts, B, H, W, cin, cout):
             stats = torch.empty(Kn.conv_stats_tiles(M), 2, cout, device=cuda)
             y = Kn.conv3x3_fwd(_t(x, cuda), w_nk, _t(b, cuda), False, stats=stats)
             dx = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd)
+            dbias = torch.full((cin,), 0.25, device=cuda)
+            dxm = Kn.conv3x3_bwd_data(_t(dy, cuda), w_bwd, relu_mask=_t(mask, cuda), dbias=dbias)
             mean, _ = Kn.bn_finalize(stats, M, cout, 1e-3, 0.99)
         torch.cuda.synchronize()
         outs[mode] = (y.cpu().numpy(), dx.cpu().numpy(), mean.cpu().numpy())
+        dxm_ref = dx_ref * (mask > 0)
+        assert float(np.linalg.norm(dxm.cpu().numpy() - dxm_ref) / np.linalg.norm(dxm_ref)) < 2e-6
+        np.testing.assert_allclose(dbias.cpu().numpy(), 0.25 + dxm_ref.reshape(-1, cin).sum(0), rtol=1e-5, atol=1e-4)
         rel = lambda a, r: float(np.linalg.norm(a - r) / np.linalg.norm(r))   # noqa: E731
         assert rel(outs[mode][0], z) < 2e-6, (mode, rel(outs[mode][0], z))   # exact fp32 products
         assert rel(outs[mode][1], dx_ref) < 2e-6, (mode, rel(outs[mode][1], dx_ref))
