@@ -77,6 +77,7 @@ enum Option : int {
     OPT_PP_DEEP,              // 1: the deep-lead ping-pong schedule for the plain (A_ROWK) GEMMs
     OPT_NT_F32_EXACT,         // 1 (default): exact-mode fp32 convolutions on the NT ring (0: generic engine)
     OPT_NT_F32_MASK,          // 1 (default): the masked fp32 data gradients on the NT ring too (0: generic engine)
+    OPT_NT_F32_X6,            // 1: exact-mode NT convolutions as six bf16 products (fp32-precision split; opt-in)
     OPT_COUNT
 };
 int64_t opt(Option o);

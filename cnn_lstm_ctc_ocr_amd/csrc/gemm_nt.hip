@@ -40,7 +40,8 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // EXACT (with F32): exact fp32 products on v_mfma_f32_16x16x4_f32 instead of the split --
 // the fp32 Trainer's conv tower (kernels.f32_exact); lane group g supplies k = 8g + e to
 // the e-th of 8 MFMAs per 32-deep step (any k order sums the same products).
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false>
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false,
+          bool X6 = false>
 __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
     // (its second pass over the accumulators would spill); launch_nt routes
@@ -186,6 +187,39 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
         const char* sa = smem + (kt % S) * STAGE;
         const char* sb = sa + A_BYTES;
+        if constexpr (F32 && EXACT && X6) {
+            // products to fp32 precision on the bf16 MFMA: each fragment split into
+            // hi / mid / lo at the read, six products per tile pair, smallest first
+            const int s0 = ((2 * g) ^ swz) * 16, s1 = ((2 * g + 1) ^ swz) * 16;
+            auto frag = [&](const char* row, bf16x8& h, bf16x8& m, bf16x8& l) {
+                V8<float> v;
+                v.q0 = *reinterpret_cast<const f32x4*>(row + s0);
+                v.q1 = *reinterpret_cast<const f32x4*>(row + s1);
+                u32x4 a, b, c;
+                split8_bf16x3(v, a, b, c);
+                h = __builtin_bit_cast(bf16x8, a);
+                m = __builtin_bit_cast(bf16x8, b);
+                l = __builtin_bit_cast(bf16x8, c);
+            };
+            bf16x8 bh[TN], bm[TN], bl[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) frag(sb + (wn * WN + j * 16 + i16) * ROWB, bh[j], bm[j], bl[j]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                bf16x8 ah, am, al;
+                frag(sa + (wm * WM + i * 16 + i16) * ROWB, ah, am, al);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            continue;
+        }
         if constexpr (F32 && EXACT) {
             const int s0 = ((2 * g) ^ swz) * 16, s1 = ((2 * g + 1) ^ swz) * 16;
             auto frag = [&](const char* row) {
@@ -404,26 +438,28 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     }
 }
 
-template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false>
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false,
+          bool X6 = false>
 int launch_nt(const GemmParams& p, hipStream_t stream) {
     if constexpr (NW == 8 && !F32) {
         if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
     }
     constexpr int LDS = S * (BM + BN) * BK * (F32 ? 4 : 2);
     static DeviceOnce configured;
-    set_dyn_lds(configured, reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT>),
-                LDS);
+    set_dyn_lds(configured,
+                reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6>), LDS);
     dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
-    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT><<<grid, NW * 64, LDS, stream>>>(p);
+    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6><<<grid, NW * 64, LDS, stream>>>(p);
     return launch_status("gemm_nt");
 }
 
 // fp32 operands (BK = 32: 128-B fp32 rows) on the bf16x3 split, or with EXACT products
-template <int AM, bool EXACT = false>
+// (X6: to fp32 precision as six bf16 products, else the f32 MFMA)
+template <int AM, bool EXACT = false, bool X6 = false>
 int dispatch_nt_f32(const GemmParams& p, hipStream_t s) {
-    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM, 4, true, EXACT>(p, s);
-    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM, 4, true, EXACT>(p, s);
-    return launch_nt<128, 128, 32, 2, 2, AM, 4, true, EXACT>(p, s);
+    if (p.N <= 32) return launch_nt<128, 32, 32, 3, 4, AM, 4, true, EXACT, X6>(p, s);
+    if (p.N <= 64) return launch_nt<128, 64, 32, 3, 2, AM, 4, true, EXACT, X6>(p, s);
+    return launch_nt<128, 128, 32, 2, 2, AM, 4, true, EXACT, X6>(p, s);
 }
 
 // Tile configurations (OCRK_GEMM_NT_CFG picks one for experiments; by default
@@ -523,10 +559,13 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
             return dispatch_nt_f32<A_ROWK>(p, stream);
         }
         if (p.convC % 4 != 0 || p.ldb % 4 != 0) return -1;
-        if (amode == A_IM2COL) return exact ? dispatch_nt_f32<A_IM2COL, true>(p, stream)
-                                            : dispatch_nt_f32<A_IM2COL>(p, stream);
-        if (amode == A_IM2COL_FLIP) return exact ? dispatch_nt_f32<A_IM2COL_FLIP, true>(p, stream)
-                                                 : dispatch_nt_f32<A_IM2COL_FLIP>(p, stream);
+        const bool x6 = exact && opt(OPT_NT_F32_X6);
+        if (amode == A_IM2COL) return x6 ? dispatch_nt_f32<A_IM2COL, true, true>(p, stream)
+                                      : exact ? dispatch_nt_f32<A_IM2COL, true>(p, stream)
+                                              : dispatch_nt_f32<A_IM2COL>(p, stream);
+        if (amode == A_IM2COL_FLIP) return x6 ? dispatch_nt_f32<A_IM2COL_FLIP, true, true>(p, stream)
+                                           : exact ? dispatch_nt_f32<A_IM2COL_FLIP, true>(p, stream)
+                                                   : dispatch_nt_f32<A_IM2COL_FLIP>(p, stream);
         return -1;
     }
     if (dtype != OCRK_BF16) return -1;

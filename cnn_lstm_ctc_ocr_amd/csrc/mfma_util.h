@@ -91,6 +91,29 @@ __device__ __forceinline__ void split8_bf16(const V8<float>& x, u32x4& hi, u32x4
     hi = u32x4{h[0], h[1], h[2], h[3]};
     lo = u32x4{l[0], l[1], l[2], l[3]};
 }
+// x = hi + mid + lo exactly (three RNE bf16 roundings of the running residual:
+// each residual is exact in fp32, the last one has <= 8 significant bits), for
+// products to fp32 precision on the bf16 MFMA: the six terms down to 2^-16
+// relative (hh, hm, mh, hl, mm, lh), the dropped ones <= 2^-25.
+__device__ __forceinline__ void split3_bf16(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+    const bf16x2_t h = __builtin_convertvector(f32x2_t{x0, x1}, bf16x2_t);
+    const f32x2_t r = f32x2_t{x0, x1} - __builtin_convertvector(h, f32x2_t);
+    const bf16x2_t m = __builtin_convertvector(r, bf16x2_t);
+    const bf16x2_t l = __builtin_convertvector(r - __builtin_convertvector(m, f32x2_t), bf16x2_t);
+    hi = __builtin_bit_cast(unsigned, h);
+    mid = __builtin_bit_cast(unsigned, m);
+    lo = __builtin_bit_cast(unsigned, l);
+}
+__device__ __forceinline__ void split8_bf16x3(const V8<float>& x, u32x4& hi, u32x4& mid, u32x4& lo) {
+    unsigned h[4], m[4], l[4];
+    split3_bf16(x.q0[0], x.q0[1], h[0], m[0], l[0]);
+    split3_bf16(x.q0[2], x.q0[3], h[1], m[1], l[1]);
+    split3_bf16(x.q1[0], x.q1[1], h[2], m[2], l[2]);
+    split3_bf16(x.q1[2], x.q1[3], h[3], m[3], l[3]);
+    hi = u32x4{h[0], h[1], h[2], h[3]};
+    mid = u32x4{m[0], m[1], m[2], m[3]};
+    lo = u32x4{l[0], l[1], l[2], l[3]};
+}
 
 // Buffer resource from provably wave-uniform words (readfirstlane; the byte
 // count clamped with integer ops -- HIP's min<int64_t> lowers to v_min_f64, a

@@ -37,6 +37,7 @@ constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"CONV_DIRECT", 1}, {"CONV_ROWS", 1}, {"CONV_ROWS_WIDE", 1}, {"CONV_WGRAD_BLOCKS", 1},
     {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0}, {"LSTM_BWD_PB16", 0},
     {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1}, {"PP_PERSIST_NK", 8}, {"PP_DEEP", 0}, {"NT_F32_EXACT", 1}, {"NT_F32_MASK", 1},
+    {"NT_F32_X6", 0},
 };
 std::atomic<int64_t> g_opts[OPT_COUNT];
 std::once_flag g_opts_once;

@@ -35,7 +35,8 @@ _HOST_DEFAULTS = {
 # kernel-side options (libocrk's registry, csrc/common.h)
 KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOCKS", "LSTM_SPIN_LIMIT",
                   "PERSIST_LATE", "LSTM_BWD_KSPLIT", "LSTM_BWD_PB16", "LSTM_BWD_R16", "CTC_LDS",
-                  "PP_PERSIST_NK", "PP_DEEP", "NT_F32_EXACT", "NT_F32_MASK")
+                  "PP_PERSIST_NK", "PP_DEEP", "NT_F32_EXACT", "NT_F32_MASK",
+                  "NT_F32_X6")
 
 
 def _env_int(name, default):

@@ -35,9 +35,16 @@ def _setup(cuda, dtype, B=32, W=64, seed=0, scale_rnn=20.0, sizes=SIZES, cell="l
     return store, vals, img, widths, labels, T
 
 
+@pytest.mark.parametrize("x6", [0, 1])
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
-def test_forward_train_mode_loss_and_grads_fp32(cuda, cell):
+def test_forward_train_mode_loss_and_grads_fp32(cuda, ocrk_opts, cell, x6):
+    """fp32 TRAIN forward + backward against the float64 graph. x6=0 (default): the
+    exact-mode convolutions on v_mfma_f32_16x16x4_f32, every gradient within 5e-4;
+    x6=1 (option NT_F32_X6): the same convolutions as six bf16 products of a
+    three-way split, bounded by what an fp32 restatement of the graph (the oracle
+    in float32) is off float64 on each tensor (x2, at least 5e-4)."""
     from cnn_lstm_ctc_ocr_amd import model
+    ocrk_opts("NT_F32_X6", x6)
     store, vals, img, widths, labels, T = _setup(cuda, torch.float32, cell=cell)
     # float64 oracle: an fp32 oracle's own rounding reaches 2e-3 on the conv-tower
     # gradients behind the GRU (measured against float64); the HIP path is closer than that
@@ -67,7 +74,24 @@ def test_forward_train_mode_loss_and_grads_fp32(cuda, cell):
             scale = max(scale, 1e-3 * np.linalg.norm(grads_ref[name.replace("/bias", "/kernel")]))
         errs[name] = float(np.linalg.norm(got - g) / max(scale, 1e-12))
     print("relative gradient errors:", errs)
-    assert max(errs.values()) < 5e-4, errs
+    if not x6:
+        assert max(errs.values()) < 5e-4, errs
+        return
+    # the six-product form: 5e-4, or twice what an fp32 restatement of the same graph
+    # (the oracle in float32) is off float64 on that tensor -- the conv-tower gradients
+    # sit behind BN amplification, where an fp32 summation order moves them by ~1e-3
+    ref32 = M.RefModel({k: v.astype(np.float32) for k, v in vals.items()}, cell, SIZES)
+    _, grads32, _, _, _ = ref32.loss_and_grads(x.astype(np.float32), widths, labels)
+    bound = {}
+    for name, g in grads_ref.items():
+        scale = np.linalg.norm(g)
+        if name.endswith("/bias") and name.split("/")[1] in ("conv2", "conv4", "conv6", "conv8"):
+            scale = max(scale, 1e-3 * np.linalg.norm(grads_ref[name.replace("/bias", "/kernel")]))
+        e32 = float(np.linalg.norm(np.asarray(grads32[name], np.float64) - g) / max(scale, 1e-12))
+        bound[name] = max(5e-4, 2 * e32)
+    print("fp32-oracle bounds:", bound)
+    bad = {k: (errs[k], bound[k]) for k in errs if errs[k] >= bound[k]}
+    assert not bad, bad
     # BN moving averages were updated exactly like the reference UPDATE_OPS
     for name, v in ref.bn_moving_updates().items():
         np.testing.assert_allclose(store.stats[name].cpu().numpy(), v, rtol=1e-4, atol=1e-6)
