@@ -8,10 +8,12 @@ Here the LSTM 512/512 model is trained from seed 0 on the reference's own data
 mjsynth_val_words000.npz, tools/make_val_fixture.py) through the training input
 semantics (first-row pad, 0.0 dynamic padding, mjsynth.py:185-194) in
 width-sorted batches of 32, a seeded shuffle per epoch -- for STEPS
-Trainer.step calls (Adam, train.py:120-137, at LR = 1e-3 instead of the
-reference's 1e-4 so the run leaves the blank plateau in ~1,500 steps instead
-of tens of thousands), in fp32 (the reference's precision) and in bf16 (the
-benched precision). Then:
+Trainer.step calls (Adam with the reference's exponential decay,
+train.py:120-137, at LR = 1e-3 instead of the reference's 1e-4 so the run
+leaves the blank plateau in ~1,500 steps instead of tens of thousands, and
+the decay scaled to the short run -- rate 0.5 per 1,000 steps instead of 0.9
+per 2^16 -- so the last evaluations are not taken on a 10x rate's noise), in
+fp32 (the reference's precision) and in bf16 (the benched precision). Then:
 
 * the fp32 model's shard CER (greedy, validate.py:81-92; CER = total edit
   distance / total label length, test.py:90-99) must be far below the
@@ -46,6 +48,7 @@ from oracle import ref_graph as G
 pytestmark = pytest.mark.gpu
 STEPS = 2500
 LR = 1e-3
+DECAY_RATE, DECAY_STEPS = 0.5, 1000
 WINDOW = 50
 EARLY = 1000              # steps before either run leaves the blank plateau
 EVAL_EVERY = 500
@@ -95,7 +98,7 @@ def train_on_shard(dtype, batches, device, steps=STEPS, lr=LR, eval_every=EVAL_E
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
     from cnn_lstm_ctc_ocr_amd.train import Trainer
     store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=dtype), device=device, seed=0)
-    tr = Trainer(store, learning_rate=lr)
+    tr = Trainer(store, learning_rate=lr, decay_rate=DECAY_RATE, decay_steps=DECAY_STEPS)
     rng = np.random.default_rng(7)
     dev = [(img.to(device=device, dtype=dtype), w, lab) for img, w, lab in batches]
     order = []
@@ -136,7 +139,7 @@ def _write_report():
 def test_fp32_leaves_blank_plateau(fp32_run):
     _store, losses, cers = fp32_run
     w = losses.reshape(-1, WINDOW).mean(1)
-    _REPORT.update(steps=STEPS, lr=LR, window=WINDOW, fp32_loss=[round(v, 4) for v in losses.tolist()],
+    _REPORT.update(steps=STEPS, lr=LR, decay=(DECAY_RATE, DECAY_STEPS), window=WINDOW, fp32_loss=[round(v, 4) for v in losses.tolist()],
                    fp32_window_mean=w.tolist(), fp32_cer=[(int(a), float(b)) for a, b in cers])
     _write_report()
     print(f"fp32 windows {np.round(w[::5], 2).tolist()}\nfp32 CER {cers}")
