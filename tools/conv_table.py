@@ -14,7 +14,7 @@ import os
 import re
 from collections import defaultdict
 
-FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, false)?>|conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel")
+FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, false)*>|conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel")
 B = 256
 LAYERS = [("conv2", 30, 254, 32, 32), ("conv3", 15, 127, 32, 64), ("conv4", 15, 127, 64, 64),
           ("conv5", 7, 126, 64, 128), ("conv6", 7, 126, 128, 128), ("conv7", 3, 125, 128, 256),
