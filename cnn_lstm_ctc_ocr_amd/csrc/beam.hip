@@ -719,13 +719,7 @@ ctc_beam_wave_kernel(const float* __restrict__ logits, const int* __restrict__ s
 }  // namespace
 
 // OCRK_BEAM_WAVE=0: the block form for every beam width (A/B)
-static bool wave_beam_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("OCRK_BEAM_WAVE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+static bool wave_beam_enabled() { return ocrk::opt(ocrk::OPT_BEAM_WAVE) != 0; }
 
 extern "C" size_t ocrk_ctc_beam_workspace_size(int T, int B, int beam_width) {
     if (T < 0 || B < 0 || beam_width < 1) return 0;

@@ -646,11 +646,8 @@ extern "C" int ocrk_bn_relu_pool_fwd(const void* z, int B, int H, int W, int C, 
 // pass-1 blocks (= rows of the partial-sum slab the ordered column sums walk on the
 // critical path): at most OCRK_BN_BWD_BLOCKS (default 2048)
 static int64_t bn_bwd_blocks(int64_t items) {
-    static const int64_t cap = [] {              // thread-safe once
-        const char* e = getenv("OCRK_BN_BWD_BLOCKS");
-        const long v = e ? atol(e) : 2048;
-        return (int64_t)(v >= 64 && v <= 8192 ? v : 2048);
-    }();
+    const int64_t v = ocrk::opt(ocrk::OPT_BN_BWD_BLOCKS);
+    const int64_t cap = v >= 64 && v <= 8192 ? v : 2048;
     return std::max<int64_t>(1, std::min<int64_t>(cap, ocrk::cdiv(items, 256 * 8)));
 }
 static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::cdiv(items, nb), 256) * 256; }
@@ -659,11 +656,7 @@ static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::c
 // [3,1]/[3,1]); 0 = use the pixel-centric kernel. OCRK_BN_ROUTE=0 disables it.
 constexpr int BN_ROUTE_SEG = 8;
 static int bn_route_variant(int kh, int kw, int sh, int sw, int H, int W) {
-    static const int on = [] {                 // thread-safe once
-        const char* e = getenv("OCRK_BN_ROUTE");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    if (!on || sh != kh || H < kh || W < kw) return 0;
+    if (!ocrk::opt(ocrk::OPT_BN_ROUTE) || sh != kh || H < kh || W < kw) return 0;
     if (kh == 2 && kw == 2 && sw == 2) return 1;
     if (kh == 2 && kw == 2 && sw == 1) return 2;
     if (kh == 3 && kw == 1 && sw == 1) return 3;

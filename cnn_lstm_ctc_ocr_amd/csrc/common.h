@@ -78,6 +78,20 @@ enum Option : int {
     OPT_NT_F32_EXACT,         // 1 (default): exact-mode fp32 convolutions on the NT ring (0: generic engine)
     OPT_NT_F32_MASK,          // 1 (default): the masked fp32 data gradients on the NT ring too (0: generic engine)
     OPT_NT_F32_X6,            // 1: exact-mode NT convolutions as six bf16 products (fp32-precision split; opt-in)
+    OPT_BEAM_WAVE,            // 1 (default): the one-wave beam search for K <= 16, 0 the block kernel
+    OPT_BN_BWD_BLOCKS,        // BN backward pass-1 workgroup cap (2048; 64 .. 8192)
+    OPT_BN_ROUTE,             // 1 (default): window-walk BN backward for the non-overlapping pools
+    OPT_CONV_TN_ITEMS,        // workgroup cap of the conv weight-gradient TN launches beside the backward (192)
+    OPT_CONV_TN4_ITEMS,       // split-K target items of the 4-wave TN conv weight gradients (512)
+    OPT_CONV_WGRAD_CUS,       // CUs the channel-block conv weight gradients take (192; 0 = every CU)
+    OPT_F32_MFMA,             // 1: exact f32 products for every fp32 GEMM of the process (else per ocrk_set_f32_gemm_mode)
+    OPT_GEMM_NT,              // 1 (default): the NT LDS-DMA ring, 0 the generic engine only
+    OPT_GEMM_NT_STAGED,       // 1 (default): the NT ring's LDS-staged bf16 epilogue, 0 direct 2-B stores
+    OPT_GEMM_PP,              // 1 (default): the ping-pong NT engine for the large plain GEMMs
+    OPT_GEMM_PPTN,            // 1 (default): the ping-pong TN engine for the wide weight gradients
+    OPT_GEMM_TN,              // 1 (default): the 4-wave TN engine, 0 the generic engine
+    OPT_LSTM_DMA,             // 1 (default): LDS-DMA staging in the per-step LSTM forward kernels
+    OPT_LSTM_BWD_DMA,         // 1 (default): LDS-DMA staging in the per-step LSTM backward kernels
     OPT_COUNT
 };
 int64_t opt(Option o);

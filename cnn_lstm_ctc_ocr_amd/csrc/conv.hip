@@ -401,12 +401,8 @@ extern "C" int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, i
 // items (of 256 CUs) leave those 64 CUs. Same-box A/B of the step: 5.241-5.248
 // ms vs 5.266-5.281 at 256 (one round on the chip); 224: 5.27, 160: 5.24-5.27.
 static int conv_tn_items() {
-    static const int n = [] {
-        const char* e = getenv("OCRK_CONV_TN_ITEMS");
-        const int v = e ? atoi(e) : 192;
-        return v >= 16 ? v : 192;
-    }();
-    return n;
+    const int64_t v = ocrk::opt(ocrk::OPT_CONV_TN_ITEMS);
+    return v >= 16 ? (int)v : 192;
 }
 
 static int wgrad_splits(int64_t M, int cin, int cout) {
@@ -417,11 +413,8 @@ static int wgrad_splits(int64_t M, int cin, int cout) {
         return (int)std::max<int64_t>(1, std::min<int64_t>(conv_tn_items() / tiles, M / 2048));
     }
     int64_t tiles = ocrk::cdiv(9 * cin, 128) * ocrk::cdiv(cout, cout <= 32 ? 32 : (cout <= 64 ? 64 : 128));
-    static const int items = [] {                        // OCRK_CONV_TN4_ITEMS: experiments
-        const char* e = getenv("OCRK_CONV_TN4_ITEMS");
-        const int v = e ? atoi(e) : 512;
-        return v >= 16 ? v : 512;
-    }();
+    const int64_t iv = ocrk::opt(ocrk::OPT_CONV_TN4_ITEMS);
+    const int items = iv >= 16 ? (int)iv : 512;
     int64_t want = ocrk::cdiv(items, tiles);
     int64_t maxs = std::max<int64_t>(1, M / 4096);
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, maxs));

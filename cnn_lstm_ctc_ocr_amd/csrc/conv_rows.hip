@@ -1140,10 +1140,7 @@ static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, in
     // stream, so they take at most 192 CUs (the other weight-gradient launches' cap):
     // same box 5.096-5.100 vs 5.097-5.113 ms with all 256, 5.106-5.123 at 128
     // (OCRK_CONV_WGRAD_CUS overrides; 0 = every CU)
-    static const int cap = [] {
-        const char* e = getenv("OCRK_CONV_WGRAD_CUS");
-        return e ? atoi(e) : 192;
-    }();
+    const int cap = (int)opt(OPT_CONV_WGRAD_CUS);
     const int cus = (nb > 1 && cap > 0) ? std::min(cap, cu_count()) : cu_count();
     const int grid = std::max(1, std::min(B, std::max(cus, 1) / nb));
     static DeviceOnce cfg;

@@ -549,11 +549,7 @@ size_t gemm_splitk_ws_bytes(int M, int N, int batch, int splits) {
 static std::atomic<int> g_f32_mode{0};
 
 bool f32_exact_mfma() {
-    static const bool env = [] {
-        const char* e = getenv("OCRK_F32_MFMA");
-        return e && e[0] == '1';
-    }();
-    return env || g_f32_mode.load(std::memory_order_relaxed) == 1;
+    return opt(OPT_F32_MFMA) == 1 || g_f32_mode.load(std::memory_order_relaxed) == 1;
 }
 
 template <typename CT, int AM, int BMD>

@@ -522,19 +522,11 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_nt_enabled() {
-    static const int on = [] {                 // thread-safe once OCRK_GEMM_NT=0: generic engine only
-        const char* e = getenv("OCRK_GEMM_NT");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on == 1;
+    return opt(OPT_GEMM_NT) != 0;              // 0: the generic engine only
 }
 
 bool nt_staged_enabled() {
-    static const int on = [] {                 // thread-safe once OCRK_GEMM_NT_STAGED=0: direct 2-B stores
-        const char* e = getenv("OCRK_GEMM_NT_STAGED");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on == 1;
+    return opt(OPT_GEMM_NT_STAGED) != 0;       // 0: direct 2-B stores
 }
 
 // Runs the NT engine when it covers (mode, dtype); returns -1 when it does not.

@@ -870,11 +870,7 @@ int dispatch_pp(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_pp_enabled() {
-    static const int on = [] {                 // thread-safe once OCRK_GEMM_PP=0: previous engines only
-        const char* e = getenv("OCRK_GEMM_PP");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on == 1;
+    return opt(OPT_GEMM_PP) != 0;              // 0: the previous engines only
 }
 
 // Runs the ping-pong engine when it covers (mode, dtype, shape); -1 otherwise.

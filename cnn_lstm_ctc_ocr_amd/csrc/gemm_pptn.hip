@@ -291,11 +291,7 @@ __global__ void __launch_bounds__(512) gemm_pptn_kernel(const GemmParams p) {
 }  // namespace
 
 bool gemm_pptn_enabled() {
-    static const int on = [] {                 // thread-safe once OCRK_GEMM_PPTN=0: the 4-wave TN engine
-        const char* e = getenv("OCRK_GEMM_PPTN");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on == 1;
+    return opt(OPT_GEMM_PPTN) != 0;            // 0: the 4-wave TN engine
 }
 
 // Runs the ping-pong TN engine when it covers the call; -1 otherwise.

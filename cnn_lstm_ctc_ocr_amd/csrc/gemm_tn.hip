@@ -268,11 +268,7 @@ int dispatch_tn(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 bool gemm_tn_enabled() {
-    static const int on = [] {                 // thread-safe once
-        const char* e = getenv("OCRK_GEMM_TN");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return on == 1;
+    return opt(OPT_GEMM_TN) != 0;
 }
 
 int gemm_tn(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t stream) {

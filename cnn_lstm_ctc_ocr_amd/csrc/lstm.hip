@@ -557,7 +557,7 @@ extern "C" int ocrk_lstm_debug_stamps(long long* buf) { g_lstm_dbg = buf; return
 // GEMM blocks (2 x 64 rows x 2H bytes) + gx tile (8 KB) + c tile (4 KB)
 static constexpr int lstm_fwd_dma_lds(int H) { return 2 * 64 * 2 * H + 64 * 64 * 2 + 64 * 16 * 4; }
 static bool lstm_dma_enabled() {
-    static const bool on = [] { const char* e = getenv("OCRK_LSTM_DMA"); return !(e && e[0] == '0'); }();
+    const bool on = ocrk::opt(ocrk::OPT_LSTM_DMA) != 0;
     if (on) {
         static DeviceOnce a512, a256;
         set_dyn_lds(a512, reinterpret_cast<const void*>(&lstm_fwd_step_dma_kernel<512>), lstm_fwd_dma_lds(512));
@@ -569,8 +569,7 @@ static bool lstm_dma_enabled() {
 // Backward ring + epilogue operands: 138 KB of dynamic LDS. OCRK_LSTM_BWD_DMA=0 disables it
 // (and a device that refuses the LDS limit falls back to the VGPR-staged kernel).
 static bool lstm_bwd_dma_enabled() {
-    static const bool on = [] { const char* e = getenv("OCRK_LSTM_BWD_DMA"); return !(e && e[0] == '0'); }();
-    if (!on) return false;
+    if (!ocrk::opt(ocrk::OPT_LSTM_BWD_DMA)) return false;
     static DeviceOnce once;
     static bool ok[kMaxDevices];
     once_per_device(once, [] {
