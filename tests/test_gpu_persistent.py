@@ -324,3 +324,30 @@ def test_f32_persistent_bwd_matches_oracle_and_step_kernels(cuda, ocrk_opts, T, 
     assert rel(db_pers.cpu().numpy(), dpers.sum(dim=(0, 1)).reshape(-1).cpu().numpy()) < 1e-5
     assert rel(db_pers.cpu().numpy(), dz_ref.sum(axis=(0, 1)).reshape(-1)) < 5e-5
     assert rel(db_pers.cpu().numpy(), db_step.cpu().numpy()) < 5e-5
+
+
+def test_f32_persistent_bwd_timeout_sets_status(cuda, ocrk_opts):
+    """The fp32 BPTT loop's bounded hand-off wait (spin limit forced to 1 poll):
+    the loop runs to completion, ORs OCRK_STATUS_LSTM_BWD_TIMEOUT into the status
+    word and the host raises at its next check; the default limit sets no bit."""
+    from cnn_lstm_ctc_ocr_amd import _lib
+    from cnn_lstm_ctc_ocr_amd import kernels as K
+    T, B, H = 24, 256, 512
+    torch.manual_seed(1)
+    wh = torch.randn(2, H, 4 * H, device=cuda) * 0.02
+    seq = torch.full((B,), T, dtype=torch.int32, device=cuda)
+    dout = torch.randn(T, B, 2 * H, device=cuda)
+    cprev = torch.randn(T, B, 2, H, device=cuda)
+    acts = torch.rand(T, B, 2, 4 * H, device=cuda)
+    K._PERSISTENT.clear()
+    assert K.lstm_f32_bwd_persistent_ok(B, H)
+    K.status_word(cuda).zero_()
+    ocrk_opts("LSTM_SPIN_LIMIT", 1)
+    K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    torch.cuda.synchronize()
+    ocrk_opts.reset("LSTM_SPIN_LIMIT")
+    with pytest.raises(_lib.DeviceError):
+        K.check_status(cuda)
+    assert K.read_status(cuda) == 0
+    K.lstm_bwd(wh, seq, dout, cprev, acts, T, B, H)
+    assert K.read_status(cuda) == 0
