@@ -447,6 +447,191 @@ lstm_fwd_persistent_kernel(const bf16* __restrict__ gx, const bf16* __restrict__
     }
 }
 
+// ------------------------------------------- forward, 16-row / 64-unit members
+// The forward loop above stages, per member and step, the group's h_{s-1} rows
+// of its 32 batch rows (32 KB at H = 512) and runs 64 MFMAs per wave on 4 waves.
+// Here a member owns 16 batch rows and 64 hidden units, as the 16-row BPTT
+// (groups = 2 x B/16 of 8 members: the same B workgroups, one per CU at B =
+// 256): 16 KB staged per step (two 1-KB row DMAs per wave into padded LDS rows),
+// 8 waves, wave w owning units 8w .. 8w+7 of all 4 gates = two 16-column N-tiles
+// over the full K = H with its W_h^T slice resident (2 x 16 k-steps x 4 VGPRs =
+// 128), 32 MFMAs per wave per step on the one 16-row M-tile. Cell: 2 units of one
+// row per thread, the step's gx read straight into registers behind the staging
+// DMA (4 buffer loads). Hand-off form, census, counting flags and the saved
+// tensors as the kernel above.
+constexpr int R16_ROWS = 16, R16_UNITS = 64;
+
+__global__ void __launch_bounds__(512, 1)
+lstm_fwd_r16_kernel(const bf16* __restrict__ gx, const bf16* __restrict__ whT, bf16* __restrict__ hx,
+                    const int* __restrict__ seq_len, int T, int B, bf16* __restrict__ out, bf16* __restrict__ hprev_t,
+                    float* __restrict__ cprev_t, bf16* __restrict__ acts_t, unsigned* __restrict__ flags,
+                    unsigned* __restrict__ err, unsigned spin_limit) {
+    constexpr int KS = 16, H = 512, G4 = 4 * H;
+    constexpr int RB = R16_ROWS, UM = R16_UNITS;
+    constexpr int NU = H / UM;                          // members per group (8)
+    constexpr int LDH = H + 8;                          // padded LDS row (bf16 elements)
+    constexpr int LDG = 4 * UM + 4;                     // padded gate row (floats)
+    __shared__ __attribute__((aligned(16))) unsigned short sh[RB * LDH];
+    __shared__ __attribute__((aligned(16))) float sG[RB * LDG];             // [row][gate][unit]
+
+    int group, member;
+    persistent_role(2 * (B / RB), NU, group, member);
+    const int dir = group & 1, bs = group >> 1;
+    const int u0 = member * UM, b0 = bs * RB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const int lu = 8 * w + (c & 7);                     // the unit (within the slice) of this lane's columns
+    gu32* gflags = (gu32*)(flags) + group * NU;
+    unsigned base;
+    const bool local = persistent_setup((gu32*)flags, group, NU, member, err, spin_limit, base);
+
+    // resident B fragments: N-tile j holds gates 2j + (c >> 3) of unit u0 + lu
+    bf16x8 bw[2][KS];
+    const bf16* wdir = whT + (size_t)dir * G4 * H;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bf16* row = wdir + (size_t)((2 * j + (c >> 3)) * H + u0 + lu) * H + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bw[j][ks] = *reinterpret_cast<const bf16x8*>(row + ks * 32);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(bw[j][ks]));   // settled before the loop
+
+    // the cell item: row er, units eu, eu + 1 (all 4 gates)
+    const int er = tid >> 5, eu = 2 * (tid & 31);
+    const int elen = seq_len[b0 + er];
+    asm volatile("" ::"v"(elen));
+    float cst[2] = {0.f, 0.f}, hst[2] = {0.f, 0.f};
+
+    const int64_t hx_elems = (int64_t)2 * 2 * B * H;
+    auto hx_rsrc = __builtin_amdgcn_make_buffer_rsrc(hx, 0, (int)(hx_elems * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gx_rsrc = uniform_rsrc(gx, (int64_t)T * B * 2 * G4 * 2);
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const unsigned lo16 = (unsigned)(lane * 16);
+
+    for (int s = 0; s < T; ++s) {
+        const bool valid = s < elen;
+        const int t = step_time(dir, s, elen);
+        const int64_t tb = ((int64_t)t * B + b0 + er) * 2 + dir;
+        unsigned lg[4];
+        auto load_gx = [&]() {                           // 4 buffer loads: 2 units x 4 gates
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                lg[k] = __builtin_amdgcn_raw_buffer_load_b32(gx_rsrc, (int)((tb * G4 + k * H + u0 + eu) * 2), 0, 0);
+        };
+        floatx4 acc[2];
+        acc[0] = acc[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (s > 0) {
+            // 1. wait until every member of the group published h_{s-1} (flag >= s)
+            if (w == 0) {
+                unsigned spins = 0;
+                while (true) {
+                    unsigned f = base + (unsigned)s;
+                    if (lane < NU) f = poll_word(gflags + lane, local);
+                    if (__all(reached(f, base + (unsigned)s))) break;
+                    poll_pause();
+                    if (++spins > spin_limit) {
+                        if (lane == 0) __hip_atomic_fetch_or(err, (unsigned)OCRK_STATUS_LSTM_FWD_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            // 2. stage the group's 16 h_{s-1} rows: rows 2w, 2w + 1, one 1-KB LDS-DMA each
+            const int64_t hbase = ((int64_t)(((s - 1) & 1) * 2 + dir) * B + b0) * H;
+            if (local) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int r = 2 * wu + q;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
+                        (unsigned)((hbase + (int64_t)r * H) * 2) + lo16, 0, 0, 2);      // nt
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int r = 2 * wu + q;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        hx_rsrc, (__attribute__((address_space(3))) void*)(sh + r * LDH), 16,
+                        (unsigned)((hbase + (int64_t)r * H) * 2) + lo16, 0, 0, 16);     // sc1
+                }
+            }
+            asm volatile("" ::: "memory");
+            load_gx();                                   // 4 loads behind the 2 DMAs
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            __syncthreads();
+            // 3. gates += h_{s-1} . W_h over the full K
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sh[c * LDH + ks * 32 + 8 * g]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[j][ks], acc[j], 0, 0, 0);
+            }
+        } else {
+            load_gx();
+        }
+        // 4. spill the gate pre-activations: lane (c, g) holds rows 4 g + r of N-tile j,
+        //    gate 2j + (c >> 3) of unit lu
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sG[(4 * g + r) * LDG + (2 * j + (c >> 3)) * UM + lu] = acc[j][r];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // gx landed
+        __syncthreads();
+
+        // 5. the cell update of (row er, units eu, eu + 1)
+        float a4[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f32x2_t z = *reinterpret_cast<const f32x2_t*>(&sG[er * LDG + k * UM + eu]);
+            a4[k][0] = z[0] + __uint_as_float(lg[k] << 16);
+            a4[k][1] = z[1] + __uint_as_float(lg[k] & 0xffff0000u);
+        }
+        float hn[2], cp[2], hp[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float ai = sig_fast(a4[0][e]);
+            const float aj = tanh_fast(a4[1][e]);
+            const float af = sig_fast(a4[2][e] + 1.0f);       // forget_bias = 1
+            const float ao = sig_fast(a4[3][e]);
+            const float cn = af * cst[e] + ai * aj;
+            const float h = ao * tanh_fast(cn);
+            a4[0][e] = valid ? ai : 0.f; a4[1][e] = valid ? aj : 0.f;
+            a4[2][e] = valid ? af : 0.f; a4[3][e] = valid ? ao : 0.f;
+            cp[e] = valid ? cst[e] : 0.f;
+            hp[e] = valid ? hst[e] : 0.f;
+            if (valid) { cst[e] = cn; hst[e] = (float)(bf16)h; }
+            hn[e] = hst[e];                                   // published state (carried when invalid)
+        }
+        auto pack2 = [](float x0, float x1) {
+            return (unsigned)bf16_bits(x0) | ((unsigned)bf16_bits(x1) << 16);
+        };
+
+        // 6. publish h_s (4-B stores), drain, barrier, one lane raises the flag
+        {
+            gu32* ph = (gu32*)(hx + ((int64_t)((s & 1) * 2 + dir) * B + b0 + er) * H + u0 + eu);
+            const unsigned v = pack2(hn[0], hn[1]);
+            if (local) *ph = v;
+            else __hip_atomic_store(ph, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) raise_flag(gflags + member, base + (unsigned)(s + 1), local);
+
+        // 7. the layer output (zeros past the length) and the tensors saved for the
+        //    backward pass (time order; they drain behind the next step)
+        *reinterpret_cast<unsigned*>(out + ((int64_t)t * B + b0 + er) * 2 * H + dir * H + u0 + eu) =
+            valid ? pack2(hn[0], hn[1]) : 0u;
+        *reinterpret_cast<unsigned*>(hprev_t + tb * H + u0 + eu) = pack2(hp[0], hp[1]);
+        *reinterpret_cast<f32x2_t*>(cprev_t + tb * H + u0 + eu) = f32x2_t{cp[0], cp[1]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<unsigned*>(acts_t + tb * G4 + k * H + u0 + eu) = pack2(a4[k][0], a4[k][1]);
+    }
+}
+
 // ---------------------------------------------------------------- backward
 // BPTT of the same layer as ONE persistent launch (groups, members and the
 // hand-off form of the forward). Member (group, unit slice) owns units
@@ -737,8 +922,6 @@ lstm_bwd_persistent_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, 
 // wave-locally (32 MFMAs); the eight K-slice partials meet in LDS in a fixed
 // order. Cell: 2 units of one row per thread. Hand-off form, census, counting
 // flags, late epilogue loads and bias partials as the gather kernel.
-constexpr int R16_ROWS = 16, R16_UNITS = 64;
-
 __global__ void __launch_bounds__(512, 1)
 lstm_bwd_r16_kernel(const bf16* __restrict__ wh, bf16* __restrict__ dzx, const int* __restrict__ seq_len, int T,
                     int B, const bf16* __restrict__ dout, const float* __restrict__ cprev_t,
@@ -1232,6 +1415,20 @@ extern "C" size_t ocrk_persistent_flags_size(int B, int H) {
     return (B > 0 && B % PBR == 0 && H > 0 && H % PHU == 0) ? persistent_counter_bytes(B, H) : 0;
 }
 
+// the 16-row / 64-unit forward (H = 512): default where its grid (B workgroups) is co-resident;
+// option LSTM_FWD_R16=0 keeps the 32-row kernel (A/B and tests)
+static bool lstm_fwd_r16(int B, int H) {
+    if (opt(OPT_LSTM_FWD_R16) == 0 || H != 512 || B % PBR) return false;         // flag words as the 32-row form
+    static ocrk::DeviceOnce once;
+    static int per_cu[ocrk::kMaxDevices];
+    const int dev = ocrk::current_device();
+    ocrk::once_per_device(once, [dev] {
+        int n = 0;
+        per_cu[dev] = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lstm_fwd_r16_kernel, 512, 0) == hipSuccess ? n : 0;
+    });
+    return 2L * (B / R16_ROWS) * (H / R16_UNITS) <= (long)ocrk::cu_count() * per_cu[dev];
+}
+
 extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                                         void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
                                         unsigned* flags, void* ws, size_t ws_bytes, void* stream) {
@@ -1243,6 +1440,13 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     bf16* hx = (bf16*)((char*)ws + counters);
     if (!flags && hipMemsetAsync(cnt, 0, counters, st) != hipSuccess)
         return ocrk::launch_status("ocrk_lstm_fwd_persistent memset");
+    if (lstm_fwd_r16(B, H) && (int64_t)T * B * 8 * H * 2 < 0x7fffffffll) {
+        // counters: 2 (B/16) x 8 members = the same count as 2 (B/32) x 16
+        lstm_fwd_r16_kernel<<<2u * (unsigned)(B / R16_ROWS) * (unsigned)(H / R16_UNITS), 512, 0, st>>>(
+            (const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out, (bf16*)hprev_t, cprev_t,
+            (bf16*)acts_t, cnt, err, lstm_spin_limit());
+        return ocrk::launch_status("ocrk_lstm_fwd_persistent");
+    }
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
     if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
         lstm_fwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)gx, (const bf16*)whT, hx, seq_len, T, B, (bf16*)out,

@@ -40,6 +40,7 @@ constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"NT_F32_X6", 0}, {"BEAM_WAVE", 1}, {"BN_BWD_BLOCKS", 2048}, {"BN_ROUTE", 1}, {"CONV_TN_ITEMS", 192},
     {"CONV_TN4_ITEMS", 512}, {"CONV_WGRAD_CUS", 192}, {"F32_MFMA", 0}, {"GEMM_NT", 1}, {"GEMM_NT_STAGED", 1},
     {"GEMM_PP", 1}, {"GEMM_PPTN", 1}, {"GEMM_TN", 1}, {"LSTM_DMA", 1}, {"LSTM_BWD_DMA", 1},
+    {"LSTM_FWD_R16", 1},
 };
 std::atomic<int64_t> g_opts[OPT_COUNT];
 std::once_flag g_opts_once;

@@ -92,7 +92,7 @@ const char* ocrk_last_error(void);
  * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP, NT_F32_EXACT,
  * NT_F32_MASK, NT_F32_X6, BEAM_WAVE, BN_BWD_BLOCKS, BN_ROUTE, CONV_TN_ITEMS, CONV_TN4_ITEMS,
  * CONV_WGRAD_CUS, F32_MFMA, GEMM_NT, GEMM_NT_STAGED, GEMM_PP, GEMM_PPTN, GEMM_TN, LSTM_DMA,
- * LSTM_BWD_DMA (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
+ * LSTM_BWD_DMA, LSTM_FWD_R16 (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
 
 /* A stream on the current device whose kernels run on only n_cus of its CUs
