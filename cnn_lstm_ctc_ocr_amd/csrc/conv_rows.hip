@@ -51,6 +51,12 @@ constexpr int RW_MAXW = 254;
 // by (r >> 2) & 3 as the TN engine's 64-B rows, so a transposed read's 16 k-rows spread)
 __device__ __forceinline__ int rw_off(int r, int c) { return r * RW_ROWB + ((c ^ ((r >> 2) & 3)) << 4); }
 
+// two fp32 values -> one word of two RNE bf16 (a single v_cvt_pk_bf16_f32; the
+// per-value casts + shift / or took three VALU instructions per pair)
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+}
+
 // workgroup barrier over LDS traffic only (the row prefetch loads stay in flight)
 __device__ __forceinline__ void rw_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -326,8 +332,7 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
                     const unsigned m = mk[n][i][e2];
                     const float v0 = __uint_as_float(m << 16) > 0.f ? acc[n][i][2 * e2] : 0.f;
                     const float v1 = __uint_as_float(m & 0xffff0000u) > 0.f ? acc[n][i][2 * e2 + 1] : 0.f;
-                    o[e2] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v0) |
-                            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v1) << 16);
+                    o[e2] = pack_bf16x2(v0, v1);
                 }
                 *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CI + 16 * i + 4 * g) = o;
             }
@@ -348,9 +353,12 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
 // W pixels: [B*H][2][cout] (sum, M2 about the row mean), finalized with
 // tile_rows = W). Same ring / band walk as the backward-data kernel above,
 // with x rows in the ring and the w_nk fragments resident.
+// RELU a template flag: a runtime flag compiled to a max and a select per output value
+// in the unrolled epilogue (the kernel's VALU count sets its row step)
+template <bool RELU>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
-                        bf16* __restrict__ y, float* __restrict__ stats, int relu, int B, int H, int W) {
+                        bf16* __restrict__ y, float* __restrict__ stats, int B, int H, int W) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float s_red[2][4][RW_CO];           // [sum | M2][wave][channel]
     const int tid = threadIdx.x, lane = tid & 63;
@@ -411,6 +419,11 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
     }
     load_row(xrow(min(h0 + 2, H - 1)), sd[0]);
     const float inv_w = 1.f / (float)W;
+    // pixels past the row (the last tile): weight 0 in the row statistics -- an FMA per
+    // value instead of an add and a select (exact: x * 1 and x * 0 of finite values)
+    float inrow[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) inrow[n] = 64 * wave + 16 * n + i16 < W ? 1.f : 0.f;
 
     auto step = [&](int h, auto P_) {
         constexpr int P = decltype(P_)::value;
@@ -443,15 +456,14 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
         float sum[2][4] = {};
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const bool in = 64 * wave + 16 * n + i16 < W;
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float v = acc[n][j][e] + bco[j][e];
-                    if (relu) v = fmaxf(v, 0.f);
+                    if constexpr (RELU) v = fmaxf(v, 0.f);
                     acc[n][j][e] = v;
-                    if (in) sum[j][e] += v;
+                    sum[j][e] = __builtin_fmaf(v, inrow[n], sum[j][e]);
                 }
         }
         bf16* orow = y + ((size_t)b * H + h) * W * RW_CO;
@@ -464,9 +476,9 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
             for (int j = 0; j < 2; ++j) {
                 u32x2 o;
 #pragma unroll
-                for (int e2 = 0; e2 < 2; ++e2)
-                    o[e2] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][j][2 * e2]) |
-                            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][j][2 * e2 + 1]) << 16);
+                for (int e2 = 0; e2 < 2; ++e2)         // one v_cvt_pk_bf16_f32 per pair
+                    o[e2] = __builtin_bit_cast(unsigned, __builtin_convertvector(
+                        (f32x2_t{acc[n][j][2 * e2], acc[n][j][2 * e2 + 1]}), bf16x2_t));
                 *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CO + 16 * j + 4 * g) = o;
             }
         }
@@ -501,13 +513,12 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
                 }
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
-                const bool in = 64 * wave + 16 * n + i16 < W;
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const float d = acc[n][j][e] - mean[j][e];
-                        if (in) q2[j][e] += d * d;
+                        const float d = (acc[n][j][e] - mean[j][e]) * inrow[n];
+                        q2[j][e] = __builtin_fmaf(d, d, q2[j][e]);
                     }
             }
 #pragma unroll
@@ -717,10 +728,10 @@ struct RfCfg {
     static constexpr int PH = KS >= 4 && NW > 4 ? 2 : 1;    // pixel parts per row (register budget)
 };
 
-template <int CI, int CO, int KPX, int CS>
+template <int CI, int CO, int KPX, int CS, bool RELU>
 __global__ void __launch_bounds__((RfCfg<CI, CO, KPX, CS>::NT), (RfCfg<CI, CO, KPX, CS>::PER_CU))
 conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
-                           bf16* __restrict__ y, float* __restrict__ stats, int relu, int B, int H, int W) {
+                           bf16* __restrict__ y, float* __restrict__ stats, int B, int H, int W) {
     using C = RfCfg<CI, CO, KPX, CS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -810,19 +821,18 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
 #pragma unroll
             for (int n = 0; n < PP; ++n) {
                 const int px = 16 * (ph * PP + n) + i16;
+                const float inrow = px < W ? 1.f : 0.f;      // FMA weight instead of a select per value
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float v = acc[n][e] + bco[e];
-                    if (relu) v = fmaxf(v, 0.f);
+                    if constexpr (RELU) v = fmaxf(v, 0.f);
                     acc[n][e] = v;
-                    if (px < W) sum[e] += v;
+                    sum[e] = __builtin_fmaf(v, inrow, sum[e]);
                 }
                 if (px < W) {
                     u32x2 o;
-                    o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][0]) |
-                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][1]) << 16);
-                    o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][2]) |
-                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)acc[n][3]) << 16);
+                    o[0] = pack_bf16x2(acc[n][0], acc[n][1]);
+                    o[1] = pack_bf16x2(acc[n][2], acc[n][3]);
                     *reinterpret_cast<u32x2*>(orow + (size_t)px * CO + 16 * wave + 4 * g) = o;
                 }
             }
@@ -841,8 +851,8 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
                         float q = 0.f;
 #pragma unroll
                         for (int n = 0; n < PP; ++n) {
-                            const float d = acc[n][e] - mean;
-                            if (16 * (ph * PP + n) + i16 < W) q += d * d;
+                            const float d = (acc[n][e] - mean) * (16 * (ph * PP + n) + i16 < W ? 1.f : 0.f);
+                            q = __builtin_fmaf(d, d, q);
                         }
                         q += dpp_row<0x128>(q);
                         q += dpp_row<0x124>(q);
@@ -882,10 +892,16 @@ template <int CI, int CO, int KPX, int CS = 1>
 static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, const float* bias, void* y, int relu,
                          float* stats, hipStream_t s) {
     using C = RfCfg<CI, CO, KPX, CS>;
-    static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS>), C::LDS);
-    conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
-        (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, relu, B, H, W);
+    static DeviceOnce cfg, cfg_r;
+    if (relu) {
+        set_dyn_lds(cfg_r, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, true>), C::LDS);
+        conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, true><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
+            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W);
+    } else {
+        set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, false>), C::LDS);
+        conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, false><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
+            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W);
+    }
     return launch_status("conv3x3_fwd_rows_co");
 }
 
@@ -1017,10 +1033,8 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
 #pragma unroll
                 for (int e = 0; e < 4; ++e) bsum[e] += v[e];
                 u32x2 o;
-                o[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16);
-                o[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
-                       ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16);
+                o[0] = pack_bf16x2(v[0], v[1]);
+                o[1] = pack_bf16x2(v[2], v[3]);
                 *reinterpret_cast<u32x2*>(orow + (size_t)px * CI + 16 * wave + 4 * g) = o;
             }
             if (h + 2 < H) store_row(h + 2, sx[P]);
@@ -1106,10 +1120,16 @@ int conv_rows_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,
         if (cout == 64) return launch_fwd_co<64, 64, 128>(x, B, H, W, w_nk, bias, y, relu, stats, s);
         return launch_fwd_co<64, 128, 128>(x, B, H, W, w_nk, bias, y, relu, stats, s);
     }
-    static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_kernel), RD_LDS);
-    conv3x3_fwd_rows_kernel<<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats,
-                                                              relu, B, H, W);
+    static DeviceOnce cfg, cfg_r;
+    if (relu) {
+        set_dyn_lds(cfg_r, reinterpret_cast<const void*>(&conv3x3_fwd_rows_kernel<true>), RD_LDS);
+        conv3x3_fwd_rows_kernel<true><<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y,
+                                                                        stats, B, H, W);
+    } else {
+        set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_kernel<false>), RD_LDS);
+        conv3x3_fwd_rows_kernel<false><<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y,
+                                                                         stats, B, H, W);
+    }
     return launch_status("conv3x3_fwd_rows");
 }
 
