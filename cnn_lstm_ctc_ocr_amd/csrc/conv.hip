@@ -307,6 +307,45 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
                     const void* relu_mask, float* stats, hipStream_t s);
 int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, hipStream_t s);
+bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout);
+int64_t conv_rows_dgrad_c1_parts(int B);
+int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask, const void* x,
+                       int x_is_u8, float* part, hipStream_t s);
+}
+
+// conv2's backward-data and conv1's weight gradient as one pass (bf16): the data
+// gradient dy1 = relu'(y1) . conv2^T(dz2) is contracted against conv1's input as
+// it is produced and never stored (its only consumer is conv1's weight gradient:
+// conv1 is the first layer). dz2 [B,H,W,32], x [B,H+2,W+2] u8 or bf16, y1 the
+// ReLU mask [B,H,W,32]; dw1 [3,3,1,32] / db1 [32] (+)= the sums.
+// workspace: part [B * bands][10 * 32] f32 | slab_sum's [SLAB_P][320] double
+extern "C" int ocrk_conv2_bwd_data_conv1_wgrad_supported(int B, int H, int W, int cin, int cout, int dtype) {
+    return dtype == OCRK_BF16 && ocrk::conv_rows_dgrad_c1_covers(B, H, W, cin, cout) ? 1 : 0;
+}
+
+extern "C" size_t ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(int B, int H, int W) {
+    (void)H; (void)W;
+    return ((size_t)ocrk::conv_rows_dgrad_c1_parts(std::max(B, 1)) * 10 * 32 * sizeof(float) + 15) / 16 * 16 +
+           (size_t)ocrk::SLAB_P * 10 * 32 * sizeof(double);
+}
+
+extern "C" int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int W, const void* w_bwd,
+                                               const void* relu_mask, const void* x, int x_is_u8, float* dw,
+                                               float* db, int accumulate, void* ws, size_t ws_bytes, int dtype,
+                                               void* stream) {
+    OCRK_REQUIRE(ocrk_conv2_bwd_data_conv1_wgrad_supported(B, H, W, 32, 32, dtype),
+                 "ocrk_conv2_bwd_data_conv1_wgrad: B=%d H=%d W=%d dtype=%d not covered", B, H, W, dtype);
+    OCRK_REQUIRE(dz && w_bwd && relu_mask && x && dw && db && ws, "ocrk_conv2_bwd_data_conv1_wgrad: null pointer");
+    OCRK_REQUIRE(ws_bytes >= ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(B, H, W) && (uintptr_t)ws % 16 == 0,
+                 "ocrk_conv2_bwd_data_conv1_wgrad: workspace too small or misaligned");
+    const int64_t nb = ocrk::conv_rows_dgrad_c1_parts(B);
+    OCRK_REQUIRE(nb < (1ll << 31), "ocrk_conv2_bwd_data_conv1_wgrad: too many rows");
+    hipStream_t s = ocrk::as_stream(stream);
+    float* part = (float*)ws;
+    int st = ocrk::conv_rows_dgrad_c1(dz, B, H, W, w_bwd, relu_mask, x, x_is_u8, part, s);
+    if (st) return st;
+    double* part2 = (double*)((char*)ws + ((size_t)nb * 10 * 32 * sizeof(float) + 15) / 16 * 16);
+    return ocrk::slab_sum(part, (int)nb, 10 * 32, part2, nullptr, dw, db, 9 * 32, accumulate, s);
 }
 
 extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,

@@ -222,9 +222,36 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
 constexpr int RD_BANDS = 2;                        // row bands per image: 2 workgroups per CU
 constexpr int RD_LDS = 4 * RW_XSLOT;               // 64.5 KB
 
+// conv1 weight gradient fused into conv2's backward-data (XIN != 0): dx = dy1, the
+// gradient at conv1's ReLU output, feeds only conv1's weight gradient
+//   dW1[kh][kw][ci] = sum_{h,w} x[h+kh][w+kw] . dy1[h][w][ci],  db1[ci] = sum dy1[h][w][ci]
+// (conv1 is 'valid' on the [H+2][W+2] single-channel image), so it is contracted
+// here as it is produced instead of written (125 MB at C3) and re-read by
+// conv1_wgrad_partial. Per row a wave multiplies A = X[tap][pixel] (taps 0-8, tap
+// row 9 = ones for db1) by B = dy1[pixel][ci] on the 16x16x32 bf16 MFMA, K = its
+// 64 pixels as two 32-pixel blocks: the dy1 block goes through a 2 KB per-wave
+// LDS tile ([pixel][ci], read back transposed with frag_tr), the x rows sit in a
+// 4-row f32 ring (preprocessed once per row), split hi + lo into bf16 (the u8
+// path's x = v/255 - 0.5 is not a bf16 value; |x - hi - lo| <= 2^-17 |x|).
+// 8 MFMAs per row beside the data gradient's 72; one [10][32] partial per workgroup.
+constexpr int RD_XROW = 260;                       // floats per x ring row (pixels 0 .. 257, zero past W + 1)
+constexpr int RD_XRING = 4 * RD_XROW * 4;          // 4.1 KB
+constexpr int RD_TSLOT = 32 * RW_ROWB;             // 2 KB: one wave's 32-pixel block of dy1
+constexpr int RD_LDS_C1 = RD_LDS + RD_XRING + 4 * RD_TSLOT;   // 76.6 KB (2 workgroups per CU)
+constexpr int RD_C1_PART = 10 * RW_CI;             // floats per workgroup partial: [tap 0-8 | bias][ci]
+
+// validate.py:61-62 (the preprocess conv.hip's conv1 kernels apply, same rounding)
+__device__ __forceinline__ float conv1_pre_u8(unsigned v) {
+#pragma clang fp contract(off)
+    return (float)v * (1.0f / 255.0f) - 0.5f;
+}
+
+template <int XIN>   // 0: dx out; 1 / 2: conv1's u8 / bf16 input -> conv1 weight-gradient partials, no dx
 __global__ void __launch_bounds__(256, 2)
 conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb, const bf16* __restrict__ mask,
-                          bf16* __restrict__ dx, int B, int H, int W) {
+                          bf16* __restrict__ dx, int B, int H, int W, const void* __restrict__ xin,
+                          float* __restrict__ c1part) {
+    constexpr bool C1 = XIN != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -232,9 +259,32 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
     const int b = blockIdx.x / RD_BANDS, band = blockIdx.x - b * RD_BANDS;
     const int rows = (H + RD_BANDS - 1) / RD_BANDS;
     const int h0 = band * rows, h1 = min(H, h0 + rows);
-    if (h0 >= h1) return;
+    if (h0 >= h1) {
+        if constexpr (C1)
+            for (int o = tid; o < RD_C1_PART; o += 256) c1part[(size_t)blockIdx.x * RD_C1_PART + o] = 0.f;
+        return;
+    }
 
-    for (int i = tid; i < RD_LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < (C1 ? RD_LDS_C1 : RD_LDS) / 16; i += 256)
+        reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+
+    // conv1 weight-gradient state (XIN != 0): x ring, this wave's dy1 tile, accumulators
+    float* xring = reinterpret_cast<float*>(smem + RD_LDS);
+    char* tile = smem + RD_LDS + RD_XRING + wave * RD_TSLOT;
+    const int XW = W + 2;
+    unsigned xraw = 0;
+    auto x_fetch = [&](int r) {                      // this thread's pixel of x row r (clamped: a fixed load count)
+        const size_t o = ((size_t)b * (H + 2) + r) * XW + min(tid, XW - 1);
+        if constexpr (XIN == 1) xraw = reinterpret_cast<const uint8_t*>(xin)[o];
+        else if constexpr (XIN == 2) xraw = reinterpret_cast<const unsigned short*>(xin)[o];
+    };
+    auto x_put = [&](int r) {
+        if (tid < XW)
+            xring[(r & 3) * RD_XROW + tid] = XIN == 1 ? conv1_pre_u8(xraw) : __uint_as_float(xraw << 16);
+    };
+    floatx4 c1acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+    const int kr0 = 4 * g + (i16 >> 2), mq = 4 * (i16 & 3);   // frag_tr lane geometry (k-row, ci offset)
+    const int tap = min(i16, 8), tkh = tap / 3, tkw = tap - 3 * tkh;
 
     // resident A fragments: ci tile i, tap t -> w_bwd[16 i + i16][t][8 g .. 8 g + 7]
     bf16x8 wa[9][2];
@@ -278,6 +328,12 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
             store_row(r, sd[1]);
         }
     }
+    if constexpr (C1) {                              // x rows h0 .. h0+2 (conv1 is 'valid': all inside)
+        for (int r = h0; r <= h0 + 2; ++r) {
+            x_fetch(r);
+            x_put(r);
+        }
+    }
     load_row(drow(min(h0 + 2, H - 1)), sd[0]);
 
     auto step = [&](int h, auto P_) {
@@ -286,6 +342,7 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         load_row(drow(min(h + 3, H - 1)), sd[1 - P]);
+        if constexpr (C1) x_fetch(min(h + 3, H + 1));
         // the ReLU mask of this row's outputs, in flight during the MFMAs
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         u32x2 mk[4][2];
@@ -319,31 +376,96 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
             }
         }
         // lane: ci 16 i + 4 g .. +3 of pixel 64 q + 16 n + i16
-        bf16* orow = dx + ((size_t)b * H + h) * W * RW_CI;
+        auto dx_bits = [&](int n, int i) {
+            u32x2 o;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int px = 64 * wave + 16 * n + i16;
-            if (px >= W) continue;
+            for (int e2 = 0; e2 < 2; ++e2) {
+                const unsigned m = mk[n][i][e2];
+                const float v0 = __uint_as_float(m << 16) > 0.f ? acc[n][i][2 * e2] : 0.f;
+                const float v1 = __uint_as_float(m & 0xffff0000u) > 0.f ? acc[n][i][2 * e2 + 1] : 0.f;
+                o[e2] = pack_bf16x2(v0, v1);
+            }
+            return o;
+        };
+        if constexpr (!C1) {
+            bf16* orow = dx + ((size_t)b * H + h) * W * RW_CI;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                u32x2 o;
+            for (int n = 0; n < 4; ++n) {
+                const int px = 64 * wave + 16 * n + i16;
+                if (px >= W) continue;
 #pragma unroll
-                for (int e2 = 0; e2 < 2; ++e2) {
-                    const unsigned m = mk[n][i][e2];
-                    const float v0 = __uint_as_float(m << 16) > 0.f ? acc[n][i][2 * e2] : 0.f;
-                    const float v1 = __uint_as_float(m & 0xffff0000u) > 0.f ? acc[n][i][2 * e2 + 1] : 0.f;
-                    o[e2] = pack_bf16x2(v0, v1);
+                for (int i = 0; i < 2; ++i)
+                    *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CI + 16 * i + 4 * g) = dx_bits(n, i);
+            }
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {             // the wave's pixel blocks 64 q + 32 kb .. +31
+#pragma unroll
+                for (int nn = 0; nn < 2; ++nn) {
+                    const int n = 2 * kb + nn;
+                    const bool in = 64 * wave + 16 * n + i16 < W;   // pixels past the row contribute zero
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        u32x2 o = dx_bits(n, i);
+                        if (!in) o = u32x2{0u, 0u};
+                        *reinterpret_cast<u32x2*>(tile + rw_off(16 * nn + i16, 2 * i + (g >> 1)) + (g & 1) * 8) = o;
+                    }
                 }
-                *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CI + 16 * i + 4 * g) = o;
+                // the wave's own tile writes land before its transposed reads
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bf16x8 bfr[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c = 16 * j + mq;
+                    bfr[j] = frag_tr(reinterpret_cast<const unsigned short*>(tile + rw_off(kr0, c >> 3) + (c & 7) * 2),
+                                     16 * RW_CO);
+                }
+                // A: lane row = tap (i16; 9 = the ones row of db1, 10-15 unused), k-slots of frag_tr's order
+                const float* xs = xring + ((h + tkh) & 3) * RD_XROW + 64 * wave + 32 * kb + 4 * g + tkw;
+                u32x4 ah, al;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int q = (p & 1) * 2 + (p >> 1) * 16;
+                    unsigned hi2, lo2;
+                    split2_bf16(xs[q], xs[q + 1], hi2, lo2);
+                    ah[p] = i16 < 9 ? hi2 : (i16 == 9 ? 0x3f803f80u : 0u);
+                    al[p] = i16 < 9 ? lo2 : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c1acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), bfr[j], c1acc[j],
+                                                                       0, 0, 0);
+                if constexpr (XIN == 1) {                // a bf16 input is exact in hi
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        c1acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), bfr[j],
+                                                                           c1acc[j], 0, 0, 0);
+                }
             }
         }
         // dy row h+2 into the slot of row h-2 (or zeros past the image)
         if (h + 2 < H) store_row(h + 2, sd[P]);
         else if (h + 2 == H) zero_row(h + 2);
+        if constexpr (C1)                                // x row h+3 into the slot of row h-1
+            if (h + 3 < H + 2) x_put(h + 3);
     };
     for (int h = h0; h < h1; h += 2) {
         step(h, std::integral_constant<int, 0>{});
         if (h + 1 < h1) step(h + 1, std::integral_constant<int, 1>{});
+    }
+    if constexpr (C1) {
+        // the four waves' [10][32] partials (lane: taps 4 g .. 4 g + 3 of ci 16 j + i16), added in wave order
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * g + e < 10) red[wave * RD_C1_PART + (4 * g + e) * RW_CI + 16 * j + i16] = c1acc[j][e];
+        __syncthreads();
+        for (int o = tid; o < RD_C1_PART; o += 256)
+            c1part[(size_t)blockIdx.x * RD_C1_PART + o] =
+                ((red[o] + red[RD_C1_PART + o]) + red[2 * RD_C1_PART + o]) + red[3 * RD_C1_PART + o];
     }
 }
 
@@ -1143,10 +1265,34 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     if (!relu_mask || stats) return -1;
     static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel), RD_LDS);
-    conv3x3_dgrad_rows_kernel<<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)dy, (const bf16*)w_bwd,
-                                                                (const bf16*)relu_mask, (bf16*)dx, B, H, W);
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<0>), RD_LDS);
+    conv3x3_dgrad_rows_kernel<0><<<B * RD_BANDS, 256, RD_LDS, s>>>((const bf16*)dy, (const bf16*)w_bwd,
+                                                                   (const bf16*)relu_mask, (bf16*)dx, B, H, W,
+                                                                   nullptr, nullptr);
     return launch_status("conv3x3_dgrad_rows");
+}
+
+bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout) {
+    return rows_enabled() && B >= 1 && H >= 1 && W >= 1 && W <= RW_MAXW && cin == RW_CI && cout == RW_CO;
+}
+
+int64_t conv_rows_dgrad_c1_parts(int B) { return (int64_t)B * RD_BANDS; }
+
+// conv2's backward-data with conv1's weight gradient contracted in (no dx): one
+// [10][32] f32 partial per workgroup into `part` ([B * RD_BANDS][10][32])
+int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask, const void* x,
+                       int x_is_u8, float* part, hipStream_t s) {
+    static DeviceOnce cfg_u8, cfg_bf;
+    if (x_is_u8) {
+        set_dyn_lds(cfg_u8, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<1>), RD_LDS_C1);
+        conv3x3_dgrad_rows_kernel<1><<<B * RD_BANDS, 256, RD_LDS_C1, s>>>(
+            (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)relu_mask, nullptr, B, H, W, x, part);
+    } else {
+        set_dyn_lds(cfg_bf, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<2>), RD_LDS_C1);
+        conv3x3_dgrad_rows_kernel<2><<<B * RD_BANDS, 256, RD_LDS_C1, s>>>(
+            (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)relu_mask, nullptr, B, H, W, x, part);
+    }
+    return launch_status("conv3x3_dgrad_rows_c1");
 }
 
 // an XCT -> DCT layer as (XCT / CI) x (DCT / CO) channel blocks of CI x CO

@@ -84,6 +84,27 @@ def conv1_bwd_weight(x, dz, dw, db, accumulate=True):
          int(accumulate), ptr(ws), nb, dtype_code(dz.dtype), _stream(x))
 
 
+def conv2_bwd_data_conv1_wgrad_ok(dz, x):
+    """The fused conv2 backward-data + conv1 weight gradient covers this shape
+    (bf16, conv2's 32 -> 32 on the row-walking kernel, x u8 or bf16)."""
+    B, H, W, C = dz.shape
+    return (x.dtype in (torch.uint8, torch.bfloat16) and tuple(x.shape) == (B, H + 2, W + 2)
+            and bool(_lib.lib().ocrk_conv2_bwd_data_conv1_wgrad_supported(B, H, W, C, C, dtype_code(dz.dtype))))
+
+
+def conv2_bwd_data_conv1_wgrad(dz, w_bwd, relu_mask, x, dw, db, accumulate=True):
+    """dw1 / db1 (+)= conv1's weight / bias gradient, from conv2's pre-BN gradient dz
+    through conv2's backward-data and conv1's ReLU (relu_mask = conv1's output),
+    without storing dy1 (ocrk_conv2_bwd_data_conv1_wgrad)."""
+    _chk(dz, w_bwd, relu_mask, x, dw, db)
+    B, H, W, _ = dz.shape
+    nb = _lib.lib().ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(B, H, W)
+    ws = _ws(nb, dz.device)
+    call("ocrk_conv2_bwd_data_conv1_wgrad", ptr(dz), B, H, W, ptr(w_bwd), ptr(relu_mask), ptr(x),
+         int(x.dtype == torch.uint8), ptr(dw), ptr(db), int(accumulate), ptr(ws), nb, dtype_code(dz.dtype),
+         _stream(dz))
+
+
 def conv_stats_tiles(M):
     return _lib.lib().ocrk_conv_stats_tiles(M)
 

@@ -161,6 +161,16 @@ class _ConvBlock(torch.autograd.Function):
             with _conv_side(store, y_odd, dz):             # overlaps the data-gradient GEMM below
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
+        if k == 1 and not ctx.exact and options.get("CONV1_FUSED") and K.conv2_bwd_data_conv1_wgrad_ok(dz, x):
+            # the step's tail: conv2's weight gradient (y1, dz) on the side stream beside one
+            # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
+            # contracted as it is produced, never stored: its only consumer is conv1's dW)
+            _issue(store, late)
+            with _conv_side(store, y_odd, dz):
+                _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
+            K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, y_odd, x, G[po + "/kernel"], G[po + "/bias"])
+            store.join()                                   # side-stream weight gradients are in
+            return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
                                     defer=late)

@@ -23,6 +23,7 @@ _HOST_DEFAULTS = {
     "DEFER_BIAS": 0,          # 1: bias reductions on their own stream (measured slower)
     "DEFER_DWX": 0,           # 1: an upper layer's dW_x behind the lower BPTT (measured no gain)
     "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
+    "CONV1_FUSED": 1,         # 0: conv2's backward-data stores dy1, conv1's weight gradient re-reads it
     "TN_ITEMS": 256,          # workgroup cap of the recurrent weight-gradient launches
     "TN_ITEMS_L1": 160,       # the same for the first layer (beside the conv backward)
     "TN_ITEMS_LATE": 0,       # deferred dW_x cap (0: TN_ITEMS)

@@ -170,6 +170,19 @@ size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
 int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,
                           float* dw, float* db, int accumulate, void* ws, size_t ws_bytes, int dtype,
                           void* stream);
+/* conv2's backward-data and conv1's weight gradient in one pass (bf16; conv2's
+ * Cin = Cout = 32, W <= 254): replaces ocrk_conv3x3_bwd_data(dz2, ..., relu_mask = y1)
+ * followed by ocrk_conv1_bwd_weight(x, dy1) -- the backprop of conv_layer 2 and 1
+ * (model.py:84-109,134-137; TF1's Conv2DBackpropInput of conv2 + Conv2DBackpropFilter
+ * and the bias gradient of conv1). dy1 is contracted against x as it is produced and
+ * never stored. dz [B,H,W,32] (H, W: conv1's output size), w_bwd [32][3][3][32],
+ * relu_mask = y1 [B,H,W,32], x [B,H+2,W+2] u8 (x_is_u8: the fused preprocess) or bf16;
+ * dw [3][3][1][32] / db [32] f32 (+)= the gradients (fixed-order reduction). */
+int ocrk_conv2_bwd_data_conv1_wgrad_supported(int B, int H, int W, int cin, int cout, int dtype);
+size_t ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(int B, int H, int W);
+int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                                    const void* x, int x_is_u8, float* dw, float* db, int accumulate, void* ws,
+                                    size_t ws_bytes, int dtype, void* stream);
 
 /* a2 conv2..conv8 -- conv_layer (model.py:84-109) with 'same' padding as an
  * implicit GEMM on MFMA. x [B,H,W,cin]; w_nk [cout][3][3][cin] (dtype);

@@ -91,6 +91,55 @@ def test_bf16_conv_engines_at_layer_shapes(cuda, ocrk_opts, B, H, W, cin, cout, 
     assert _rel(dw.cpu().numpy(), dw_ref) < 1e-4
 
 
+@pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70)])
+@pytest.mark.parametrize("x_u8", [True, False])
+def test_conv2_bwd_data_fused_conv1_wgrad(cuda, B, IH, IW, x_u8):
+    """conv2's backward-data with conv1's weight gradient contracted in
+    (ocrk_conv2_bwd_data_conv1_wgrad, the bench's k = 1 backward): against the
+    float64 oracle on the kernel's own bf16 dy1 (relu'(y1) . conv2^T dz, rounded
+    once), and against the unfused pair (bf16 dy1 stored, then conv1_bwd_weight).
+    Shapes: the bench crop (30 x 254), odd band heights (15 rows: 8 + 7), one
+    conv1 output row (the second band empty: a zero partial), a narrow row."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(IH * 1000 + IW + x_u8)
+    H, W = IH - 2, IW - 2
+    img = rng.integers(0, 256, (B, IH, IW)).astype(np.uint8)
+    x = G.preprocess(img) if x_u8 else _bf(rng.standard_normal((B, IH, IW)))
+    w1 = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
+    w2 = _bf(rng.standard_normal((3, 3, 32, 32)) / np.sqrt(288))
+    y1 = _bf(rng.standard_normal((B, H, W, 32)))                    # conv1's output: the ReLU mask
+    dz = _bf(rng.standard_normal((B, H, W, 32)))
+    dx_ref, _, _ = G.conv2d_bwd(y1.astype(np.float64), w2.astype(np.float64), dz.astype(np.float64), "same")
+    dy1 = _bf(dx_ref * (y1 > 0))
+    _, dw_ref, db_ref = G.conv2d_bwd(np.asarray(x, np.float64)[..., None], w1.astype(np.float64),
+                                     dy1.astype(np.float64), "valid", need_dx=False)
+    xd = torch.from_numpy(img).to(cuda) if x_u8 else torch.from_numpy(x).to(cuda).bfloat16()
+    dzd = torch.from_numpy(dz).to(cuda).bfloat16()
+    y1d = torch.from_numpy(y1).to(cuda).bfloat16()
+    w_bwd = Kn.permute3(torch.from_numpy(w2).to(cuda), 9, 32, 32, torch.bfloat16).view(32, 9 * 32)
+    assert Kn.conv2_bwd_data_conv1_wgrad_ok(dzd, xd)
+    prev_w = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
+    prev_b = rng.standard_normal(32).astype(np.float32)
+    dw = torch.from_numpy(prev_w).to(cuda)
+    db = torch.from_numpy(prev_b).to(cuda)
+    Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, y1d, xd, dw, db, accumulate=True)
+    # f32 accumulation over B*H*W pixels of bf16 dy1 x (hi + lo) x: ~1e-6 relative; the
+    # reference's dy1 is the float64 sum rounded once, so the ~5e-5 of elements whose
+    # fp32 sum rounds to the neighbouring bf16 value add up to ~2e-5 here
+    assert _rel(dw.cpu().numpy() - prev_w, dw_ref) < 1e-4
+    assert _rel(db.cpu().numpy() - prev_b, db_ref) < 1e-4
+    # the unfused pair on the same bf16 dy1 bits (only the summation order and the
+    # hi + lo split of x differ)
+    dy1d = Kn.conv3x3_bwd_data(dzd, w_bwd, relu_mask=y1d)
+    dw2, db2 = torch.zeros(3, 3, 1, 32, device=cuda), torch.zeros(32, device=cuda)
+    Kn.conv1_bwd_weight(xd, dy1d, dw2, db2, accumulate=False)
+    assert _rel(dw2.cpu().numpy(), dw_ref) < 1e-4
+    assert _rel(dw.cpu().numpy() - prev_w, dw2.cpu().numpy()) < 2e-5
+    assert _rel(db.cpu().numpy() - prev_b, db2.cpu().numpy()) < 2e-5
+    np.testing.assert_allclose(dw.cpu().numpy() - prev_w, dw2.cpu().numpy(), rtol=1e-3,
+                               atol=1e-5 * float(np.abs(dw_ref).max()))
+
+
 @pytest.mark.parametrize("M_,N,K,tag", [(8000, 4096, 256, "proj L1"), (8000, 4096, 1024, "proj L2"),
                                          (8000, 1024, 4096, "dx L2"), (8000, 256, 4096, "dx L1"),
                                          (8000, 1024, 96, "logits dx")])
