@@ -56,7 +56,9 @@ SIGNATURES = {
     "ocrk_conv1_bwd_weight": [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv2_bwd_data_conv1_wgrad_supported": [_i32, _i32, _i32, _i32, _i32, _i32],
     "ocrk_conv2_bwd_data_conv1_wgrad_workspace_size": [_i32, _i32, _i32],
-    "ocrk_conv2_bwd_data_conv1_wgrad": [_p, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_conv2_bwd_data_conv1_wgrad": [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _i32, _p, _sz, _i32,
+                                        _p],
+    "ocrk_conv1_fwd_relu_bits": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i32, _p],
     "ocrk_conv_stats_tiles": [_i64],
     "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],
     "ocrk_conv3x3_bwd_data_workspace_size": [_i32, _i32, _i32, _i32],

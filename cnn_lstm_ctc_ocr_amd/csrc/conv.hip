@@ -68,7 +68,7 @@ __device__ __forceinline__ void conv1_stage(const TIn* __restrict__ x, int H, in
 template <typename TIn, typename TOut, int COUT>
 __global__ void __launch_bounds__(256)
 conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __restrict__ w,
-                 const float* __restrict__ bias, TOut* __restrict__ y) {
+                 const float* __restrict__ bias, TOut* __restrict__ y, uint8_t* __restrict__ bits) {
     constexpr int G = COUT / 8;
     static_assert(COUT % 8 == 0 && 256 % G == 0, "channel groups");
     __shared__ float sx[C1_WR + 2][C1_PX + 2];
@@ -101,14 +101,19 @@ conv1_fwd_kernel(const TIn* __restrict__ x, int B, int H, int W, const float* __
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw) px[kh * 3 + kw] = sx[r + kh][p + kw];
             F8 o;
+            unsigned on = 0;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 float acc = br[c];
 #pragma unroll
                 for (int k = 0; k < 9; ++k) acc = fmaf(px[k], wr[k][c], acc);
                 o.v[c] = fmaxf(acc, 0.f);
+                on |= (o.v[c] > 0.f ? 1u : 0u) << c;
             }
             store8(yrow + (int64_t)p * COUT, o);
+            // the ReLU's bit mask (bit c of byte g: channel 8 g + c of the pixel), the
+            // backward's mask at 1/16 of the bf16 output's bytes
+            if (bits) bits[(((int64_t)b * Ho + ho0 + r) * Wo + wo0 + p) * (COUT / 8) + c0 / 8] = (uint8_t)on;
         }
     }
 }
@@ -237,8 +242,8 @@ conv1_wgrad_partial(const TIn* __restrict__ x, const TG* __restrict__ dz, int B,
 }
 
 // ------------------------------------------------------------------ C ABI
-extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, const float* w,
-                              const float* bias, int cout, void* y, int dtype, void* stream) {
+static int conv1_fwd_run(const void* x, int x_is_u8, int B, int H, int W, const float* w, const float* bias,
+                         int cout, void* y, uint8_t* bits, int dtype, void* stream) {
     OCRK_REQUIRE(B >= 0 && H >= 3 && W >= 3, "ocrk_conv1_fwd: bad shape B=%d H=%d W=%d", B, H, W);
     OCRK_REQUIRE(cout == 32, "ocrk_conv1_fwd: Cout=%d (this build carries the model.py:47 Cout=32)", cout);
     if (B == 0) return OCRK_OK;
@@ -247,13 +252,27 @@ extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, c
     dim3 grid((unsigned)blocks);
     hipStream_t s = ocrk::as_stream(stream);
     if (x_is_u8) {
-        if (dtype == OCRK_BF16) conv1_fwd_kernel<uint8_t, bf16, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (bf16*)y);
-        else conv1_fwd_kernel<uint8_t, float, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (float*)y);
+        if (dtype == OCRK_BF16) conv1_fwd_kernel<uint8_t, bf16, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (bf16*)y, bits);
+        else conv1_fwd_kernel<uint8_t, float, 32><<<grid, 256, 0, s>>>((const uint8_t*)x, B, H, W, w, bias, (float*)y, bits);
     } else {
-        if (dtype == OCRK_BF16) conv1_fwd_kernel<bf16, bf16, 32><<<grid, 256, 0, s>>>((const bf16*)x, B, H, W, w, bias, (bf16*)y);
-        else conv1_fwd_kernel<float, float, 32><<<grid, 256, 0, s>>>((const float*)x, B, H, W, w, bias, (float*)y);
+        if (dtype == OCRK_BF16) conv1_fwd_kernel<bf16, bf16, 32><<<grid, 256, 0, s>>>((const bf16*)x, B, H, W, w, bias, (bf16*)y, bits);
+        else conv1_fwd_kernel<float, float, 32><<<grid, 256, 0, s>>>((const float*)x, B, H, W, w, bias, (float*)y, bits);
     }
     return ocrk::launch_status("ocrk_conv1_fwd");
+}
+
+extern "C" int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, const float* w,
+                              const float* bias, int cout, void* y, int dtype, void* stream) {
+    return conv1_fwd_run(x, x_is_u8, B, H, W, w, bias, cout, y, nullptr, dtype, stream);
+}
+
+// the same with the ReLU's bit mask: relu_bits u8 [B,H-2,W-2][cout/8], bit c of byte g
+// = (y[..][8 g + c] > 0) -- the mask ocrk_conv2_bwd_data_conv1_wgrad reads
+extern "C" int ocrk_conv1_fwd_relu_bits(const void* x, int x_is_u8, int B, int H, int W, const float* w,
+                                        const float* bias, int cout, void* y, void* relu_bits, int dtype,
+                                        void* stream) {
+    OCRK_REQUIRE(relu_bits, "ocrk_conv1_fwd_relu_bits: null mask");
+    return conv1_fwd_run(x, x_is_u8, B, H, W, w, bias, cout, y, (uint8_t*)relu_bits, dtype, stream);
 }
 
 static int64_t conv1_blocks(int B, int H, int W) {
@@ -309,15 +328,16 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
                     void* ws, size_t ws_bytes, hipStream_t s);
 bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout);
 int64_t conv_rows_dgrad_c1_parts(int B);
-int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask, const void* x,
-                       int x_is_u8, float* part, hipStream_t s);
+int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                       const void* relu_bits, const void* x, int x_is_u8, float* part, hipStream_t s);
 }
 
 // conv2's backward-data and conv1's weight gradient as one pass (bf16): the data
 // gradient dy1 = relu'(y1) . conv2^T(dz2) is contracted against conv1's input as
 // it is produced and never stored (its only consumer is conv1's weight gradient:
 // conv1 is the first layer). dz2 [B,H,W,32], x [B,H+2,W+2] u8 or bf16, y1 the
-// ReLU mask [B,H,W,32]; dw1 [3,3,1,32] / db1 [32] (+)= the sums.
+// ReLU mask [B,H,W,32] -- or relu_bits, its bit mask from ocrk_conv1_fwd_relu_bits (u8
+// [B,H,W][4], 1/16 of the bytes; exactly one of the two); dw1 [3,3,1,32] / db1 [32] (+)= the sums.
 // workspace: part [B * bands][10 * 32] f32 | slab_sum's [SLAB_P][320] double
 extern "C" int ocrk_conv2_bwd_data_conv1_wgrad_supported(int B, int H, int W, int cin, int cout, int dtype) {
     return dtype == OCRK_BF16 && ocrk::conv_rows_dgrad_c1_covers(B, H, W, cin, cout) ? 1 : 0;
@@ -330,19 +350,20 @@ extern "C" size_t ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(int B, int H, i
 }
 
 extern "C" int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int W, const void* w_bwd,
-                                               const void* relu_mask, const void* x, int x_is_u8, float* dw,
-                                               float* db, int accumulate, void* ws, size_t ws_bytes, int dtype,
-                                               void* stream) {
+                                               const void* relu_mask, const void* relu_bits, const void* x,
+                                               int x_is_u8, float* dw, float* db, int accumulate, void* ws,
+                                               size_t ws_bytes, int dtype, void* stream) {
     OCRK_REQUIRE(ocrk_conv2_bwd_data_conv1_wgrad_supported(B, H, W, 32, 32, dtype),
                  "ocrk_conv2_bwd_data_conv1_wgrad: B=%d H=%d W=%d dtype=%d not covered", B, H, W, dtype);
-    OCRK_REQUIRE(dz && w_bwd && relu_mask && x && dw && db && ws, "ocrk_conv2_bwd_data_conv1_wgrad: null pointer");
+    OCRK_REQUIRE(dz && w_bwd && x && dw && db && ws, "ocrk_conv2_bwd_data_conv1_wgrad: null pointer");
+    OCRK_REQUIRE(!relu_mask != !relu_bits, "ocrk_conv2_bwd_data_conv1_wgrad: give exactly one of relu_mask / relu_bits");
     OCRK_REQUIRE(ws_bytes >= ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(B, H, W) && (uintptr_t)ws % 16 == 0,
                  "ocrk_conv2_bwd_data_conv1_wgrad: workspace too small or misaligned");
     const int64_t nb = ocrk::conv_rows_dgrad_c1_parts(B);
     OCRK_REQUIRE(nb < (1ll << 31), "ocrk_conv2_bwd_data_conv1_wgrad: too many rows");
     hipStream_t s = ocrk::as_stream(stream);
     float* part = (float*)ws;
-    int st = ocrk::conv_rows_dgrad_c1(dz, B, H, W, w_bwd, relu_mask, x, x_is_u8, part, s);
+    int st = ocrk::conv_rows_dgrad_c1(dz, B, H, W, w_bwd, relu_mask, relu_bits, x, x_is_u8, part, s);
     if (st) return st;
     double* part2 = (double*)((char*)ws + ((size_t)nb * 10 * 32 * sizeof(float) + 15) / 16 * 16);
     return ocrk::slab_sum(part, (int)nb, 10 * 32, part2, nullptr, dw, db, 9 * 32, accumulate, s);

@@ -246,7 +246,9 @@ __device__ __forceinline__ float conv1_pre_u8(unsigned v) {
     return (float)v * (1.0f / 255.0f) - 0.5f;
 }
 
-template <int XIN>   // 0: dx out; 1 / 2: conv1's u8 / bf16 input -> conv1 weight-gradient partials, no dx
+// BITS: the ReLU mask as conv1's bit mask (u32 per pixel, bit c = channel c: ocrk_conv1_fwd_relu_bits)
+// instead of its bf16 output -- 4 B per pixel read instead of 64
+template <int XIN, bool BITS = false>   // XIN 0: dx out; 1 / 2: conv1's u8 / bf16 input -> conv1 dW partials, no dx
 __global__ void __launch_bounds__(256, 2)
 conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb, const bf16* __restrict__ mask,
                           bf16* __restrict__ dx, int B, int H, int W, const void* __restrict__ xin,
@@ -346,14 +348,21 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
         // the ReLU mask of this row's outputs, in flight during the MFMAs
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         u32x2 mk[4][2];
-        const bf16* mrow = mask + ((size_t)b * H + h) * W * RW_CI;
+        unsigned mb[4];
+        if constexpr (BITS) {
+            const unsigned* mrow = reinterpret_cast<const unsigned*>(mask) + ((size_t)b * H + h) * W;
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+            for (int n = 0; n < 4; ++n) mb[n] = mrow[min(64 * wave + 16 * n + i16, W - 1)];
+        } else {
+            const bf16* mrow = mask + ((size_t)b * H + h) * W * RW_CI;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int px = min(64 * wave + 16 * n + i16, W - 1);
-                mk[n][i] = *reinterpret_cast<const u32x2*>(mrow + (size_t)px * RW_CI + 16 * i + 4 * g);
-            }
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int px = min(64 * wave + 16 * n + i16, W - 1);
+                    mk[n][i] = *reinterpret_cast<const u32x2*>(mrow + (size_t)px * RW_CI + 16 * i + 4 * g);
+                }
+        }
         floatx4 acc[4][2];
 #pragma unroll
         for (int n = 0; n < 4; ++n)
@@ -380,10 +389,17 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
             u32x2 o;
 #pragma unroll
             for (int e2 = 0; e2 < 2; ++e2) {
-                const unsigned m = mk[n][i][e2];
-                const float v0 = __uint_as_float(m << 16) > 0.f ? acc[n][i][2 * e2] : 0.f;
-                const float v1 = __uint_as_float(m & 0xffff0000u) > 0.f ? acc[n][i][2 * e2 + 1] : 0.f;
-                o[e2] = pack_bf16x2(v0, v1);
+                bool k0, k1;
+                if constexpr (BITS) {
+                    const unsigned sh = mb[n] >> (16 * i + 4 * g + 2 * e2);
+                    k0 = sh & 1u;
+                    k1 = sh & 2u;
+                } else {
+                    const unsigned m = mk[n][i][e2];
+                    k0 = __uint_as_float(m << 16) > 0.f;
+                    k1 = __uint_as_float(m & 0xffff0000u) > 0.f;
+                }
+                o[e2] = pack_bf16x2(k0 ? acc[n][i][2 * e2] : 0.f, k1 ? acc[n][i][2 * e2 + 1] : 0.f);
             }
             return o;
         };
@@ -1280,17 +1296,23 @@ int64_t conv_rows_dgrad_c1_parts(int B) { return (int64_t)B * RD_BANDS; }
 
 // conv2's backward-data with conv1's weight gradient contracted in (no dx): one
 // [10][32] f32 partial per workgroup into `part` ([B * RD_BANDS][10][32])
-int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask, const void* x,
-                       int x_is_u8, float* part, hipStream_t s) {
-    static DeviceOnce cfg_u8, cfg_bf;
-    if (x_is_u8) {
-        set_dyn_lds(cfg_u8, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<1>), RD_LDS_C1);
-        conv3x3_dgrad_rows_kernel<1><<<B * RD_BANDS, 256, RD_LDS_C1, s>>>(
-            (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)relu_mask, nullptr, B, H, W, x, part);
+template <int XIN, bool BITS>
+static void launch_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* mask, const void* x,
+                            float* part, hipStream_t s) {
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<XIN, BITS>), RD_LDS_C1);
+    conv3x3_dgrad_rows_kernel<XIN, BITS><<<B * RD_BANDS, 256, RD_LDS_C1, s>>>(
+        (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)mask, nullptr, B, H, W, x, part);
+}
+
+int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                       const void* relu_bits, const void* x, int x_is_u8, float* part, hipStream_t s) {
+    if (relu_bits) {
+        if (x_is_u8) launch_dgrad_c1<1, true>(dy, B, H, W, w_bwd, relu_bits, x, part, s);
+        else launch_dgrad_c1<2, true>(dy, B, H, W, w_bwd, relu_bits, x, part, s);
     } else {
-        set_dyn_lds(cfg_bf, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_kernel<2>), RD_LDS_C1);
-        conv3x3_dgrad_rows_kernel<2><<<B * RD_BANDS, 256, RD_LDS_C1, s>>>(
-            (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)relu_mask, nullptr, B, H, W, x, part);
+        if (x_is_u8) launch_dgrad_c1<1, false>(dy, B, H, W, w_bwd, relu_mask, x, part, s);
+        else launch_dgrad_c1<2, false>(dy, B, H, W, w_bwd, relu_mask, x, part, s);
     }
     return launch_status("conv3x3_dgrad_rows_c1");
 }

@@ -61,8 +61,9 @@ def seq_len(widths):
 
 
 # --------------------------------------------------------------------- conv
-def conv1_fwd(x, w, b, dtype):
-    """x: uint8 [B,H,W] (fused preprocess) or float [B,H,W]; w f32 [3,3,1,C]; -> [B,H-2,W-2,C]."""
+def conv1_fwd(x, w, b, dtype, relu_bits=False):
+    """x: uint8 [B,H,W] (fused preprocess) or float [B,H,W]; w f32 [3,3,1,C]; -> [B,H-2,W-2,C].
+    relu_bits: also return the ReLU's bit mask, u8 [B,H-2,W-2,C/8] (ocrk_conv1_fwd_relu_bits)."""
     _chk(x, w, b)
     B, H, W = x.shape[0], x.shape[1], x.shape[2]
     C = w.shape[-1]
@@ -70,6 +71,11 @@ def conv1_fwd(x, w, b, dtype):
     is_u8 = x.dtype == torch.uint8
     if not is_u8 and x.dtype != dtype:
         raise TypeError("conv1 float input must have the compute dtype")
+    if relu_bits:
+        bits = torch.empty(B, H - 2, W - 2, C // 8, dtype=torch.uint8, device=x.device)
+        call("ocrk_conv1_fwd_relu_bits", ptr(x), int(is_u8), B, H, W, ptr(w), ptr(b), C, ptr(y), ptr(bits),
+             dtype_code(dtype), _stream(x))
+        return y, bits
     call("ocrk_conv1_fwd", ptr(x), int(is_u8), B, H, W, ptr(w), ptr(b), C, ptr(y), dtype_code(dtype), _stream(x))
     return y
 
@@ -92,15 +98,20 @@ def conv2_bwd_data_conv1_wgrad_ok(dz, x):
             and bool(_lib.lib().ocrk_conv2_bwd_data_conv1_wgrad_supported(B, H, W, C, C, dtype_code(dz.dtype))))
 
 
-def conv2_bwd_data_conv1_wgrad(dz, w_bwd, relu_mask, x, dw, db, accumulate=True):
+def conv2_bwd_data_conv1_wgrad(dz, w_bwd, relu_mask, x, dw, db, accumulate=True, relu_bits=None):
     """dw1 / db1 (+)= conv1's weight / bias gradient, from conv2's pre-BN gradient dz
-    through conv2's backward-data and conv1's ReLU (relu_mask = conv1's output),
+    through conv2's backward-data and conv1's ReLU (relu_mask = conv1's output, or
+    relu_bits = its bit mask from conv1_fwd(..., relu_bits=True) with relu_mask None),
     without storing dy1 (ocrk_conv2_bwd_data_conv1_wgrad)."""
-    _chk(dz, w_bwd, relu_mask, x, dw, db)
+    _chk(dz, w_bwd, relu_mask, relu_bits, x, dw, db)
+    if (relu_mask is None) == (relu_bits is None):
+        raise ValueError("give exactly one of relu_mask / relu_bits")
     B, H, W, _ = dz.shape
+    if relu_bits is not None and (relu_bits.dtype != torch.uint8 or tuple(relu_bits.shape) != (B, H, W, 4)):
+        raise ValueError("relu_bits must be uint8 [B, H, W, 4]")
     nb = _lib.lib().ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(B, H, W)
     ws = _ws(nb, dz.device)
-    call("ocrk_conv2_bwd_data_conv1_wgrad", ptr(dz), B, H, W, ptr(w_bwd), ptr(relu_mask), ptr(x),
+    call("ocrk_conv2_bwd_data_conv1_wgrad", ptr(dz), B, H, W, ptr(w_bwd), ptr(relu_mask), ptr(relu_bits), ptr(x),
          int(x.dtype == torch.uint8), ptr(dw), ptr(db), int(accumulate), ptr(ws), nb, dtype_code(dz.dtype),
          _stream(dz))
 

@@ -91,7 +91,13 @@ class _ConvBlock(torch.autograd.Function):
         P = store.params
         pe = f"convnet/{even}"
         ctx.bn_sync = None
-        if k == 1:
+        ctx.relu_bits = None
+        if k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
+            # the ReLU's bit mask for the fused conv2 backward-data + conv1 weight gradient
+            # (it reads 4 B per pixel instead of y1's 64)
+            y_odd, bits = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt, relu_bits=True)
+            ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(y_odd, x) else None
+        elif k == 1:
             y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
         else:
             w_nk, _ = store.conv_images(odd, dt)
@@ -168,7 +174,9 @@ class _ConvBlock(torch.autograd.Function):
             _issue(store, late)
             with _conv_side(store, y_odd, dz):
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
-            K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, y_odd, x, G[po + "/kernel"], G[po + "/bias"])
+            bits = ctx.relu_bits
+            K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, None if bits is not None else y_odd, x, G[po + "/kernel"],
+                                         G[po + "/bias"], relu_bits=bits)
             store.join()                                   # side-stream weight gradients are in
             return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)

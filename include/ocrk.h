@@ -165,6 +165,11 @@ int ocrk_edit_distance(const int64_t* hyp, const int* hyp_len, int hyp_stride, c
  * [3][3][1][cout], bias f32 [cout]; y dtype [B,H-2,W-2,cout]. */
 int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, const float* w, const float* bias,
                    int cout, void* y, int dtype, void* stream);
+/* The same, also writing the ReLU's bit mask relu_bits u8 [B,H-2,W-2][cout/8]: bit c of
+ * byte g = (y[...][8 g + c] > 0) -- the training forward's mask for conv2's fused
+ * backward (ocrk_conv2_bwd_data_conv1_wgrad), 1/16 of y's bf16 bytes. */
+int ocrk_conv1_fwd_relu_bits(const void* x, int x_is_u8, int B, int H, int W, const float* w, const float* bias,
+                             int cout, void* y, void* relu_bits, int dtype, void* stream);
 /* conv1 weight/bias gradient from dz = dL/d(pre-ReLU conv1), f32 outputs. */
 size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
 int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,
@@ -176,13 +181,15 @@ int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int
  * (model.py:84-109,134-137; TF1's Conv2DBackpropInput of conv2 + Conv2DBackpropFilter
  * and the bias gradient of conv1). dy1 is contracted against x as it is produced and
  * never stored. dz [B,H,W,32] (H, W: conv1's output size), w_bwd [32][3][3][32],
- * relu_mask = y1 [B,H,W,32], x [B,H+2,W+2] u8 (x_is_u8: the fused preprocess) or bf16;
- * dw [3][3][1][32] / db [32] f32 (+)= the gradients (fixed-order reduction). */
+ * the ReLU mask: relu_mask = y1 [B,H,W,32] or relu_bits = its bit mask from
+ * ocrk_conv1_fwd_relu_bits (exactly one non-NULL); x [B,H+2,W+2] u8 (x_is_u8: the
+ * fused preprocess) or bf16; dw [3][3][1][32] / db [32] f32 (+)= the gradients
+ * (fixed-order reduction). */
 int ocrk_conv2_bwd_data_conv1_wgrad_supported(int B, int H, int W, int cin, int cout, int dtype);
 size_t ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(int B, int H, int W);
 int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int W, const void* w_bwd, const void* relu_mask,
-                                    const void* x, int x_is_u8, float* dw, float* db, int accumulate, void* ws,
-                                    size_t ws_bytes, int dtype, void* stream);
+                                    const void* relu_bits, const void* x, int x_is_u8, float* dw, float* db,
+                                    int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
 
 /* a2 conv2..conv8 -- conv_layer (model.py:84-109) with 'same' padding as an
  * implicit GEMM on MFMA. x [B,H,W,cin]; w_nk [cout][3][3][cin] (dtype);

@@ -91,9 +91,33 @@ def test_bf16_conv_engines_at_layer_shapes(cuda, ocrk_opts, B, H, W, cin, cout, 
     assert _rel(dw.cpu().numpy(), dw_ref) < 1e-4
 
 
+def _relu_bits(y):
+    """conv1's ReLU bit mask on the host: u8 [..., C/8], bit c of byte g = y[..., 8 g + c] > 0."""
+    pos = (np.asarray(y) > 0).reshape(*y.shape[:-1], y.shape[-1] // 8, 8).astype(np.uint8)
+    return (pos << np.arange(8, dtype=np.uint8)).sum(-1).astype(np.uint8)
+
+
+@pytest.mark.parametrize("x_u8", [True, False])
+def test_conv1_fwd_relu_bits(cuda, x_u8):
+    """ocrk_conv1_fwd_relu_bits: the same y bits as ocrk_conv1_fwd, and the bit
+    mask of y > 0 (the fused conv2 backward's ReLU mask)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(5 + x_u8)
+    img = rng.integers(0, 256, (3, 32, 131)).astype(np.uint8)
+    x = torch.from_numpy(img).to(cuda) if x_u8 else Kn.preprocess(torch.from_numpy(img).to(cuda), torch.bfloat16)
+    w = torch.from_numpy(rng.standard_normal((3, 3, 1, 32)).astype(np.float32)).to(cuda)
+    b = torch.from_numpy(rng.standard_normal(32).astype(np.float32) * 0.1).to(cuda)
+    y = Kn.conv1_fwd(x, w, b, torch.bfloat16)
+    y2, bits = Kn.conv1_fwd(x, w, b, torch.bfloat16, relu_bits=True)
+    assert torch.equal(y, y2)
+    assert bits.shape == (3, 30, 129, 4)
+    np.testing.assert_array_equal(bits.cpu().numpy(), _relu_bits(y.float().cpu().numpy()))
+
+
 @pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70)])
 @pytest.mark.parametrize("x_u8", [True, False])
-def test_conv2_bwd_data_fused_conv1_wgrad(cuda, B, IH, IW, x_u8):
+@pytest.mark.parametrize("mask", ["bf16", "bits"])
+def test_conv2_bwd_data_fused_conv1_wgrad(cuda, B, IH, IW, x_u8, mask):
     """conv2's backward-data with conv1's weight gradient contracted in
     (ocrk_conv2_bwd_data_conv1_wgrad, the bench's k = 1 backward): against the
     float64 oracle on the kernel's own bf16 dy1 (relu'(y1) . conv2^T dz, rounded
@@ -122,7 +146,11 @@ def test_conv2_bwd_data_fused_conv1_wgrad(cuda, B, IH, IW, x_u8):
     prev_b = rng.standard_normal(32).astype(np.float32)
     dw = torch.from_numpy(prev_w).to(cuda)
     db = torch.from_numpy(prev_b).to(cuda)
-    Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, y1d, xd, dw, db, accumulate=True)
+    if mask == "bits":
+        bits = torch.from_numpy(_relu_bits(y1)).to(cuda)
+        Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, None, xd, dw, db, accumulate=True, relu_bits=bits)
+    else:
+        Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, y1d, xd, dw, db, accumulate=True)
     # f32 accumulation over B*H*W pixels of bf16 dy1 x (hi + lo) x: ~1e-6 relative; the
     # reference's dy1 is the float64 sum rounded once, so the ~5e-5 of elements whose
     # fp32 sum rounds to the neighbouring bf16 value add up to ~2e-5 here
