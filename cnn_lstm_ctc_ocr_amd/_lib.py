@@ -79,6 +79,9 @@ SIGNATURES = {
                               _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_bn_moments": [_p, _i32, _i32, _i64, _i32, _p, _p, _sz, _p],
     "ocrk_bn_finalize_moments": [_p, _i32, _f32, _f32, _p, _p, _p, _p, _p],
+    "ocrk_bn_bwd_pooled_bias_slab_rows": [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32],
+    "ocrk_bn_relu_pool_bwd_pooled": [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
+                                     _i32, _p, _p, _p, _p, _i32, _p, _p, _sz, _i32, _p],
     "ocrk_bn_relu_pool_bwd_reduce": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
                                      _i32, _p, _p, _i32, _p, _p, _sz, _i32, _p],
     "ocrk_bn_relu_pool_bwd_apply": [_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32,
@@ -144,6 +147,7 @@ _RESTYPE.update({n: ctypes.c_size_t for n in SIGNATURES if n.endswith("_workspac
 _RESTYPE["ocrk_conv_stats_tiles"] = ctypes.c_size_t
 _RESTYPE["ocrk_persistent_flags_size"] = ctypes.c_size_t
 _RESTYPE["ocrk_bn_bwd_bias_slab_rows"] = ctypes.c_size_t
+_RESTYPE["ocrk_bn_bwd_pooled_bias_slab_rows"] = ctypes.c_size_t
 _RESTYPE["ocrk_crc32c"] = ctypes.c_uint32
 
 

@@ -14,6 +14,8 @@
 // deterministic two-pass BN backward (partials -> ordered sum -> apply). For
 // the path's pools both passes walk the pooling windows (bn_bwd_route_kernel;
 // the apply pass repeats the walk instead of reading a staged gradient image).
+#include <type_traits>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -302,8 +304,61 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
     }
 }
 
+// N consecutive channels of one pixel (N = 4 or 8): raw bits as loaded, widened at use
+template <typename T, int N> struct RawN;
+template <> struct RawN<bf16, 8> { uint4 q; };
+template <> struct RawN<bf16, 4> { uint2 q; };
+template <> struct RawN<float, 8> { float4 a, b; };
+template <> struct RawN<float, 4> { float4 a; };
+template <typename T, int N>
+__device__ __forceinline__ RawN<T, N> load_raw(const T* p) {
+    RawN<T, N> r;
+    if constexpr (std::is_same<T, bf16>::value) {
+        if constexpr (N == 8) r.q = *reinterpret_cast<const uint4*>(p);
+        else r.q = *reinterpret_cast<const uint2*>(p);
+    } else {
+        r.a = reinterpret_cast<const float4*>(p)[0];
+        if constexpr (N == 8) r.b = reinterpret_cast<const float4*>(p)[1];
+    }
+    return r;
+}
+template <typename T, int N>
+__device__ __forceinline__ void widen(const RawN<T, N>& r, float (&f)[N]) {
+    if constexpr (std::is_same<T, bf16>::value) {
+        const unsigned* w = reinterpret_cast<const unsigned*>(&r.q);
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) {
+            f[2 * i] = __uint_as_float(w[i] << 16);
+            f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    } else {
+        f[0] = r.a.x; f[1] = r.a.y; f[2] = r.a.z; f[3] = r.a.w;
+        if constexpr (N == 8) { f[4] = r.b.x; f[5] = r.b.y; f[6] = r.b.z; f[7] = r.b.w; }
+    }
+}
+template <typename T, int N>
+__device__ __forceinline__ void load_n(const T* p, float (&f)[N]) { widen<T, N>(load_raw<T, N>(p), f); }
+template <typename T, int N>
+__device__ __forceinline__ void store_n(T* p, const float (&f)[N]) {
+    if constexpr (std::is_same<T, bf16>::value) {
+        unsigned w[N / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) {
+            union { bf16 e[2]; unsigned u; } c;
+            c.e[0] = (bf16)f[2 * i];
+            c.e[1] = (bf16)f[2 * i + 1];
+            w[i] = c.u;
+        }
+        if constexpr (N == 8) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+        else *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+    } else {
+        reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+        if constexpr (N == 8) reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+    }
+}
+
 // pass 1, window-centric (the pools of the path: KH == stride_h, SW <= KW).
-// Thread = (image b, pooled row ho, SEG consecutive pooled columns, 8
+// Thread = (image b, pooled row ho, SEG consecutive pooled columns, NCH
 // channels). It streams the KH pre-pool rows of its column range left to
 // right through a KW-column register window, evaluates each pooling window
 // ONCE ([TF1] first max, row-major scan of relu(bn(z))), adds dp to the
@@ -313,6 +368,8 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
 // PRE = (KW-1)/SW windows left of the range that still reach into it are
 // re-evaluated (their own columns are not retired here). Rows below the last
 // pooling window, and columns right of it, receive no gradient: zeros.
+// NCH = 4 halves the thread's registers (~110 instead of ~205 VGPRs at 8: two
+// waves per SIMD made the serial walk latency-bound) at 8-B accesses.
 //
 // APPLY = pass 2 of the same window walk: instead of staging the routed
 // gradient da for a streaming apply pass (2 x |z| more bytes), the walk is
@@ -320,7 +377,10 @@ bn_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, i
 // dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n), its per-block
 // column sums (the conv bias gradient) into `slab` (C per block). Pixels no
 // window covers (rows below the last window) have da = 0 but a non-zero dz.
-template <typename T, int KH, int KW, int SW, int SEG, bool APPLY = false>
+// DG (with APPLY): also the dgamma partials sum da * xhat from z (slab rows of 2C:
+// [bias | dgamma]) -- the pooled-output pass 1 recovers xhat only to the stored
+// output's precision, so dgamma itself is summed here, from z as the walk's pass 1 does.
+template <typename T, int KH, int KW, int SW, int SEG, bool APPLY = false, int NCH = 8, bool DG = false>
 __global__ void __launch_bounds__(256)
 bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, int H, int W, int C,
                     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -328,17 +388,18 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
                     int nseg, int tasks_per_block, float* __restrict__ slab, T* __restrict__ da_out,
                     const float* __restrict__ dsum = nullptr) {
     static_assert(SW >= 1 && SW <= KW, "stride <= window");
+    static_assert(NCH == 4 || NCH == 8, "4 or 8 channels per thread");
     constexpr int PRE = (KW - 1) / SW;
-    __shared__ float red[256][17];
-    const int G = C / 8;
+    __shared__ float red[256][2 * NCH + 1];
+    const int G = C / NCH;
     const int Ho = (H - KH) / KH + 1, Wo = (W - KW) / SW + 1;
     const int tasks = B * Ho * nseg * G;
     const int g = threadIdx.x % G;
-    const int c0 = g * 8;
-    float sc[8], sf[8], mu[8], is[8], am[8], bm[8];
+    const int c0 = g * NCH;
+    float sc[NCH], sf[NCH], mu[NCH], is[NCH], am[NCH], bm[NCH];
     const float inv_n = 1.f / (float)((int64_t)B * H * W);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NCH; ++i) {
         is[i] = invstd[c0 + i];
         mu[i] = mean[c0 + i];
         sc[i] = gamma[c0 + i] * is[i];
@@ -346,9 +407,9 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
         am[i] = APPLY ? dsum[c0 + i] * inv_n : 0.f;
         bm[i] = APPLY ? dsum[C + c0 + i] * inv_n : 0.f;
     }
-    float s1[8], s2[8];
+    float s1[NCH], s2[NCH];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+    for (int i = 0; i < NCH; ++i) s1[i] = s2[i] = 0.f;
     const int t0 = blockIdx.x * tasks_per_block;
     const int t1 = min(tasks, t0 + tasks_per_block);
     for (int task = t0 + threadIdx.x; task < t1; task += 256) {
@@ -362,42 +423,44 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
         const T* zrow = z + (((int64_t)b * H + ho * KH) * W) * C + c0;
         T* drow = da_out + (((int64_t)b * H + ho * KH) * W) * C + c0;
 
-        float zr[KW][KH][8], dr[KW][KH][8];
-        auto retire = [&](int x, const float (&zc)[KH][8], const float (&dc)[KH][8]) {
+        float zr[KW][KH][NCH], dr[KW][KH][NCH];
+        auto retire = [&](int x, const float (&zc)[KH][NCH], const float (&dc)[KH][NCH]) {
             if (x < own0 || x >= own1) return;
 #pragma unroll
             for (int dh = 0; dh < KH; ++dh) {
-                F8 o;
+                float o[NCH];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
+                for (int i = 0; i < NCH; ++i) {
                     const float d = fmaf(zc[dh][i], sc[i], sf[i]) > 0.f ? dc[dh][i] : 0.f;
                     const float xh = (zc[dh][i] - mu[i]) * is[i];
                     if constexpr (APPLY) {
-                        o.v[i] = sc[i] * (d - am[i] - xh * bm[i]);
-                        s1[i] += o.v[i];
+                        o[i] = sc[i] * (d - am[i] - xh * bm[i]);
+                        s1[i] += o[i];
+                        if constexpr (DG) s2[i] += d * xh;
                     } else {
                         s1[i] += d;
                         s2[i] += d * xh;
-                        o.v[i] = d;
+                        o[i] = d;
                     }
                 }
-                if (APPLY || da_out) store8(drow + ((int64_t)dh * W + x) * C, o);
+                if (APPLY || da_out) store_n<T, NCH>(drow + ((int64_t)dh * W + x) * C, o);
             }
             if (tail_rows && (APPLY || da_out)) {
                 for (int h = Ho * KH; h < H; ++h) {
-                    F8 o;
+                    float o[NCH];
                     if constexpr (APPLY) {
-                        const F8 zt = load8(z + (((int64_t)b * H + h) * W + x) * C + c0);
+                        float zt[NCH];
+                        load_n<T, NCH>(z + (((int64_t)b * H + h) * W + x) * C + c0, zt);
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            o.v[i] = sc[i] * (-am[i] - (zt.v[i] - mu[i]) * is[i] * bm[i]);
-                            s1[i] += o.v[i];
+                        for (int i = 0; i < NCH; ++i) {
+                            o[i] = sc[i] * (-am[i] - (zt[i] - mu[i]) * is[i] * bm[i]);
+                            s1[i] += o[i];
                         }
                     } else {
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) o.v[i] = 0.f;
+                        for (int i = 0; i < NCH; ++i) o[i] = 0.f;
                     }
-                    store8(da_out + (((int64_t)b * H + h) * W + x) * C + c0, o);
+                    store_n<T, NCH>(da_out + (((int64_t)b * H + h) * W + x) * C + c0, o);
                 }
             }
         };
@@ -406,9 +469,9 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
         for (int j = 0; j < KW; ++j)
 #pragma unroll
             for (int dh = 0; dh < KH; ++dh) {
-                F8 v = load8(zrow + ((int64_t)dh * W + wfirst * SW + j) * C);
+                load_n<T, NCH>(zrow + ((int64_t)dh * W + wfirst * SW + j) * C, zr[j][dh]);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) { zr[j][dh][i] = v.v[i]; dr[j][dh][i] = 0.f; }
+                for (int i = 0; i < NCH; ++i) dr[j][dh][i] = 0.f;
             }
         auto dp_off = [&](int wo) {
             return dp_time_major ? (((int64_t)wo * B + b) * Ho + ho) * C + c0
@@ -418,23 +481,25 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
         // window's compute then waits only for loads issued a window earlier (in-order
         // vmcnt), not for the loads just issued (a same-window dp load behind the
         // prefetch made every window wait vmcnt(0))
-        F8 gp = load8(dp + dp_off(wfirst));
+        float gp[NCH];
+        load_n<T, NCH>(dp + dp_off(wfirst), gp);
         for (int wo = wfirst; wo < wb; ++wo) {
             const int x0 = wo * SW;
             // next window's pooled gradient and new columns in flight first, kept raw
             // (converted when they enter the window, after this window's work)
-            Pend8<T> nz[SW][KH];
-            Pend8<T> gpn;
+            RawN<T, NCH> nz[SW][KH];
+            RawN<T, NCH> gpn;
             const bool more = wo + 1 < wb;
             if (more) {
-                gpn = load_pend8(dp + dp_off(wo + 1));
+                gpn = load_raw<T, NCH>(dp + dp_off(wo + 1));
 #pragma unroll
                 for (int j = 0; j < SW; ++j)
 #pragma unroll
-                    for (int dh = 0; dh < KH; ++dh) nz[j][dh] = load_pend8(zrow + ((int64_t)dh * W + x0 + KW + j) * C);
+                    for (int dh = 0; dh < KH; ++dh)
+                        nz[j][dh] = load_raw<T, NCH>(zrow + ((int64_t)dh * W + x0 + KW + j) * C);
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < NCH; ++i) {
                 float best = -INFINITY;
                 int arg = -1;
 #pragma unroll
@@ -448,29 +513,26 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
                 for (int dh = 0; dh < KH; ++dh)
 #pragma unroll
                     for (int j = 0; j < KW; ++j)
-                        if (arg == dh * KW + j) dr[j][dh][i] += gp.v[i];
+                        if (arg == dh * KW + j) dr[j][dh][i] += gp[i];
             }
             // the first SW columns leave the window
 #pragma unroll
             for (int j = 0; j < SW; ++j) retire(x0 + j, zr[j], dr[j]);
             if (!more) break;
-            gp = cvt8(gpn);
+            widen<T, NCH>(gpn, gp);
 #pragma unroll
             for (int j = 0; j + SW < KW; ++j)
 #pragma unroll
                 for (int dh = 0; dh < KH; ++dh)
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) { zr[j][dh][i] = zr[j + SW][dh][i]; dr[j][dh][i] = dr[j + SW][dh][i]; }
+                    for (int i = 0; i < NCH; ++i) { zr[j][dh][i] = zr[j + SW][dh][i]; dr[j][dh][i] = dr[j + SW][dh][i]; }
 #pragma unroll
             for (int j = 0; j < SW; ++j)
 #pragma unroll
                 for (int dh = 0; dh < KH; ++dh) {
-                    const F8 v = cvt8(nz[j][dh]);
+                    widen<T, NCH>(nz[j][dh], zr[KW - SW + j][dh]);
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        zr[KW - SW + j][dh][i] = v.v[i];
-                        dr[KW - SW + j][dh][i] = 0.f;
-                    }
+                    for (int i = 0; i < NCH; ++i) dr[KW - SW + j][dh][i] = 0.f;
                 }
         }
         // columns still in the last window, then the uncovered ones on the right
@@ -478,32 +540,92 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 #pragma unroll
         for (int j = SW; j < KW; ++j) retire(xl + j, zr[j], dr[j]);
         for (int x = max(xl + KW, own0); x < own1; ++x) {
-            float zc[KH][8], dc[KH][8];                     // no gradient (z matters only for APPLY's dz)
+            float zc[KH][NCH], dc[KH][NCH];                 // no gradient (z matters only for APPLY's dz)
 #pragma unroll
             for (int dh = 0; dh < KH; ++dh) {
-                F8 zt;
-                if constexpr (APPLY) zt = load8(zrow + ((int64_t)dh * W + x) * C);
+                if constexpr (APPLY) {
+                    load_n<T, NCH>(zrow + ((int64_t)dh * W + x) * C, zc[dh]);
+                } else {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    zc[dh][i] = APPLY ? zt.v[i] : 0.f;
-                    dc[dh][i] = 0.f;
+                    for (int i = 0; i < NCH; ++i) zc[dh][i] = 0.f;
                 }
+#pragma unroll
+                for (int i = 0; i < NCH; ++i) dc[dh][i] = 0.f;
             }
             retire(x, zc, dc);
         }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
+    for (int i = 0; i < NCH; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][NCH + i] = s2[i]; }
     __syncthreads();
-    const int nout = APPLY ? C : 2 * C;
+    const int nout = (APPLY && !DG) ? C : 2 * C;
     for (int o = threadIdx.x; o < nout; o += 256) {
-        int which = o / C, c = o % C, gg = c / 8, ci = c % 8;
+        int which = o / C, c = o % C, gg = c / NCH, ci = c % NCH;
         float s = 0.f;
-        for (int q = gg; q < 256; q += G) s += red[q][which * 8 + ci];
+        for (int q = gg; q < 256; q += G) s += red[q][which * NCH + ci];
         slab[(int64_t)blockIdx.x * nout + o] = s;
     }
 }
 
+
+// pass 1 from the forward's pooled output p (its saved result, the next layer's
+// input) instead of z: the routed gradient da is dp at each window's first max when
+// that max is ReLU-active (p > 0), and there xhat = (p - beta) / gamma, so
+//   sum da = sum_{p > 0} dp,   sum da * xhat = sum_{p > 0} dp * (p - beta) / gamma
+// over the POOLED elements -- a stream over p and dp (1/4 of z's bytes for the 2x2
+// pools, 1/2 and 1/3 for the others) instead of the window walk over z. xhat is
+// recovered from the stored p (bf16 in the bf16 path: the same 2^-9 class of error
+// as the bf16 z the walk reads); where |gamma| is tiny the recovery is not used
+// (ocrk_bn_relu_pool_bwd_pooled falls back to the walk). Per-block [s1 | s2] rows of
+// 2C, the window walk's slab format. Thread = 8 channels, 4 items in flight.
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_pooled_sums_kernel(const T* __restrict__ p, const T* __restrict__ dp, int64_t items, int C,
+                          const float* __restrict__ gamma, const float* __restrict__ beta, int items_per_block,
+                          float* __restrict__ slab) {
+    __shared__ float red[256][17];
+    const int G = C / 8;
+    const int g = threadIdx.x % G, c0 = 8 * g;     // fixed: items_per_block % 256 == 0, 256 % G == 0
+    float rg[8], bt[8], s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        rg[i] = gamma[c0 + i] != 0.f ? 1.f / gamma[c0 + i] : 0.f;   // gamma = 0: xhat unrecoverable (term dropped)
+        bt[i] = beta[c0 + i];
+        s1[i] = s2[i] = 0.f;
+    }
+    const int64_t i0 = (int64_t)blockIdx.x * items_per_block;
+    const int64_t i1 = min(items, i0 + items_per_block);
+    constexpr int U = 4;
+    for (int64_t it = i0 + threadIdx.x; it < i1; it += 256 * U) {
+        Pend8<T> pr[U], dr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = min(it + 256 * u, i1 - 1);       // clamped (a fixed load count)
+            pr[u] = load_pend8(p + q * 8);
+            dr[u] = load_pend8(dp + q * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (it + 256 * u >= i1) break;
+            const F8 pv = cvt8(pr[u]), dv = cvt8(dr[u]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float d = pv.v[i] > 0.f ? dv.v[i] : 0.f;
+                s1[i] += d;
+                s2[i] += d * ((pv.v[i] - bt[i]) * rg[i]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { red[threadIdx.x][i] = s1[i]; red[threadIdx.x][8 + i] = s2[i]; }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 2 * C; o += 256) {
+        const int which = o / C, c = o % C, gg = c / 8, ci = c % 8;
+        float s = 0.f;
+        for (int q = gg; q < 256; q += G) s += red[q][which * 8 + ci];
+        slab[(int64_t)blockIdx.x * 2 * C + o] = s;
+    }
+}
 
 // pass 2 (streaming): dz = gamma*invstd*(da - sum(da)/n - xhat*sum(da*xhat)/n),
 // plus per-block partial column sums of dz -- the gradient of the conv bias
@@ -654,7 +776,33 @@ static int64_t bn_bwd_ipb(int64_t items, int64_t nb) { return ocrk::cdiv(ocrk::c
 
 // Window-centric pass 1 covers the path's pools (2x2/[2,2], 2x2/[2,1],
 // [3,1]/[3,1]); 0 = use the pixel-centric kernel. OCRK_BN_ROUTE=0 disables it.
-constexpr int BN_ROUTE_SEG = 8;
+// pooled columns per thread of the window walk (option BN_ROUTE_SEG: 4, 8 or 16) and
+// channels per thread (BN_ROUTE_NCH: 4 or 8)
+static int bn_route_seg() {
+    const int64_t v = ocrk::opt(ocrk::OPT_BN_ROUTE_SEG);
+    return (v == 4 || v == 16) ? (int)v : 8;
+}
+static int bn_route_nch() { return ocrk::opt(ocrk::OPT_BN_ROUTE_NCH) == 8 ? 8 : 4; }
+
+template <typename T, int KH, int KW, int SW, bool APPLY, int NCH, bool DG, typename... A>
+static void launch_route_n(int seg, int nr, hipStream_t s, A... args) {
+    switch (seg) {
+    case 4: bn_bwd_route_kernel<T, KH, KW, SW, 4, APPLY, NCH, DG><<<nr, 256, 0, s>>>(args...); break;
+    case 16: bn_bwd_route_kernel<T, KH, KW, SW, 16, APPLY, NCH, DG><<<nr, 256, 0, s>>>(args...); break;
+    default: bn_bwd_route_kernel<T, KH, KW, SW, 8, APPLY, NCH, DG><<<nr, 256, 0, s>>>(args...); break;
+    }
+}
+template <typename T, int KH, int KW, int SW, bool APPLY, bool DG = false, typename... A>
+static void launch_route(int seg, int nr, hipStream_t s, A... args) {
+    if (bn_route_nch() == 8) launch_route_n<T, KH, KW, SW, APPLY, 8, DG>(seg, nr, s, args...);
+    else launch_route_n<T, KH, KW, SW, APPLY, 4, DG>(seg, nr, s, args...);
+}
+template <typename T, int KH, int KW, int SW, typename... A>
+static void launch_apply(bool dg, int seg, int nr, hipStream_t s, A... args) {
+    if (dg) launch_route<T, KH, KW, SW, true, true>(seg, nr, s, args...);
+    else launch_route<T, KH, KW, SW, true, false>(seg, nr, s, args...);
+}
+
 static int bn_route_variant(int kh, int kw, int sh, int sw, int H, int W) {
     if (!ocrk::opt(ocrk::OPT_BN_ROUTE) || sh != kh || H < kh || W < kw) return 0;
     if (kh == 2 && kw == 2 && sw == 2) return 1;
@@ -663,10 +811,10 @@ static int bn_route_variant(int kh, int kw, int sh, int sw, int H, int W) {
     return 0;
 }
 
-// part [SLAB_P][2C] doubles | slab [nb][2C] | dsum [2C] | bias slab [nb][C] | routed da [B*H*W*C]
-// (4 B per element: any dtype)
+// part [SLAB_P][2C] doubles | slab [nb][2C] | dsum [2C] | bias slab [nb][2C] | routed da [B*H*W*C]
+// (4 B per element: any dtype; the bias slab's rows are [bias | dgamma] in the pooled form)
 static size_t bn_ws_floats(int64_t nb, int C) {
-    size_t f = (size_t)SLAB_P * 2 * C * 2 + (size_t)(nb * 2 * C + 2 * C + nb * C);
+    size_t f = (size_t)SLAB_P * 2 * C * 2 + (size_t)(nb * 2 * C + 2 * C + nb * 2 * C);
     return (f + 3) / 4 * 4;                                           // 16-B align the da image
 }
 
@@ -677,18 +825,26 @@ extern "C" size_t ocrk_bn_bwd_workspace_size(int B, int H, int W, int C) {
     return bn_ws_floats(nb, C) * sizeof(float) + (size_t)B * H * W * C * sizeof(float);
 }
 
-// Rows of the conv-bias partial-sum slab the apply pass writes (one per block).
-static int64_t bn_bwd_bias_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw) {
+// The window walk's launch: tasks (b, pooled row, column segment, channel group),
+// tasks per block (a multiple of 256) and blocks, at most nb of them.
+struct WalkGrid { int nseg, tpb, blocks; };
+static WalkGrid walk_grid(int B, int H, int W, int C, int kh, int kw, int sw, int64_t nb) {
+    const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
+    const int nseg = (int)ocrk::cdiv(Wo, bn_route_seg());
+    const int64_t tasks = (int64_t)B * Ho * nseg * (C / bn_route_nch());
+    const int64_t nbr = std::max<int64_t>(1, std::min<int64_t>(nb, ocrk::cdiv(tasks, 256)));
+    const int64_t tpb = ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256;
+    return WalkGrid{nseg, (int)tpb, (int)ocrk::cdiv(tasks, tpb)};
+}
+
+// Rows of the conv-bias partial-sum slab the apply pass writes (one per block);
+// pooled: the pass-1-from-pooled-output form (every route variant applies by walking).
+static int64_t bn_bwd_bias_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw, bool pooled = false) {
     const int64_t items = (int64_t)B * H * W * (C / 8);
     int64_t nb = bn_bwd_blocks(items);
     nb = ocrk::cdiv(items, bn_bwd_ipb(items, nb));
-    if (bn_route_variant(kh, kw, sh, sw, H, W) % 2 == 1) {             // window-walk apply (variants 1, 3)
-        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
-        const int64_t tasks = (int64_t)B * Ho * ocrk::cdiv(Wo, BN_ROUTE_SEG) * (C / 8);
-        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
-        const int64_t tpb = ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256;
-        return ocrk::cdiv(tasks, tpb);
-    }
+    const int rk = bn_route_variant(kh, kw, sh, sw, H, W);
+    if (rk == 1 || rk == 3 || (rk == 2 && pooled)) return walk_grid(B, H, W, C, kh, kw, sw, nb).blocks;
     return nb;
 }
 
@@ -697,11 +853,17 @@ extern "C" size_t ocrk_bn_bwd_bias_slab_rows(int B, int H, int W, int C, int kh,
     return (size_t)bn_bwd_bias_rows(B, H, W, C, kh, kw, sh, sw);
 }
 
+extern "C" size_t ocrk_bn_bwd_pooled_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw) {
+    if (C < 8 || C % 8 != 0 || (int64_t)B * H * W == 0) return 1;
+    return (size_t)bn_bwd_bias_rows(B, H, W, C, kh, kw, sh, sw, true);
+}
+
 static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C, const float* mean,
                        const float* invstd, const float* gamma, const float* beta, int kh, int kw, int sh, int sw,
                        int dp_time_major, void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
                        float* bias_slab_out, void* ws, size_t ws_bytes, int dtype, void* stream, int phase = 0,
-                       float* dsum_out = nullptr, const float* dsum_in = nullptr, const double* count = nullptr) {
+                       float* dsum_out = nullptr, const float* dsum_in = nullptr, const double* count = nullptr,
+                       const void* pooled = nullptr) {
     // phase 0: both passes; 1: pass 1 + the ordered sums only (dsum_out gets them); 2: the
     // apply pass from cross-rank sums dsum_in over count pixels (ws as left by phase 1)
     OCRK_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "ocrk_bn_relu_pool_bwd: C=%d unsupported", C);
@@ -721,9 +883,15 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
     hipStream_t s = ocrk::as_stream(stream);
     int nr = (int)nb;                                   // slab rows of pass 1
     const int rk = bn_route_variant(kh, kw, sh, sw, H, W);
-    if (rk) {
+    const int seg = bn_route_seg();
+    // pass 1 from the pooled output (window-walk pools only: pass 2 then walks for all three)
+    const bool from_pooled = pooled && rk;
+    const int64_t pitems = from_pooled ? (int64_t)B * ((H - kh) / sh + 1) * ((W - kw) / sw + 1) * (C / 8) : 0;
+    if (from_pooled) {
+        nr = (int)std::max<int64_t>(1, std::min<int64_t>(nb, ocrk::cdiv(pitems, 256 * 4)));
+    } else if (rk) {
         const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
-        const int64_t tasks = (int64_t)B * Ho * ocrk::cdiv(Wo, BN_ROUTE_SEG) * (C / 8);
+        const int64_t tasks = (int64_t)B * Ho * ocrk::cdiv(Wo, seg) * (C / bn_route_nch());
         const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
         nr = (int)ocrk::cdiv(tasks, ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
     }
@@ -732,10 +900,19 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
         bn_dsum_scale_kernel<<<ocrk::cdiv(2 * C, 256), 256, 0, s>>>(dsum_in, count, npix, 2 * C, dsum);
         st = ocrk::launch_status("ocrk_bn_relu_pool_bwd_apply scale");
         if (st) return st;
+    } else if (from_pooled) {
+        const int ipb2 = (int)(ocrk::cdiv(ocrk::cdiv(pitems, nr), 256) * 256);
+        nr = (int)ocrk::cdiv(pitems, ipb2);
+        if (dtype == OCRK_BF16)
+            bn_bwd_pooled_sums_kernel<bf16><<<nr, 256, 0, s>>>((const bf16*)pooled, (const bf16*)dp, pitems, C, gamma,
+                                                               beta, ipb2, slab);
+        else
+            bn_bwd_pooled_sums_kernel<float><<<nr, 256, 0, s>>>((const float*)pooled, (const float*)dp, pitems, C,
+                                                                gamma, beta, ipb2, slab);
     } else if (rk) {
         const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
-        const int nseg = (int)ocrk::cdiv(Wo, BN_ROUTE_SEG);
-        const int64_t tasks = (int64_t)B * Ho * nseg * (C / 8);
+        const int nseg = (int)ocrk::cdiv(Wo, seg);
+        const int64_t tasks = (int64_t)B * Ho * nseg * (C / bn_route_nch());
         const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
         const int tpb = (int)(ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
 #define ROUTE_ARGS B, H, W, C, mean, invstd, gamma, beta, dp_time_major, nseg, tpb, slab
@@ -744,15 +921,15 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
             bf16* dd = (bf16*)da;
             // pass 1 stages da only for the overlapping 2x2/[2,1] pools (their pass 2
             // streams it: measured faster than re-walking the windows); else pass 2 re-walks
-            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
-            else if (rk == 2) bn_bwd_route_kernel<bf16, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
-            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
+            if (rk == 1) launch_route<bf16, 2, 2, 2, false>(seg, nr, s, zz, pp, ROUTE_ARGS, (bf16*)nullptr, (const float*)nullptr);
+            else if (rk == 2) launch_route<bf16, 2, 2, 1, false>(seg, nr, s, zz, pp, ROUTE_ARGS, dd, (const float*)nullptr);
+            else launch_route<bf16, 3, 1, 1, false>(seg, nr, s, zz, pp, ROUTE_ARGS, (bf16*)nullptr, (const float*)nullptr);
         } else {
             const float *zz = (const float*)z, *pp = (const float*)dp;
             float* dd = (float*)da;
-            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
-            else if (rk == 2) bn_bwd_route_kernel<float, 2, 2, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, dd);
-            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG><<<nr, 256, 0, s>>>(zz, pp, ROUTE_ARGS, nullptr);
+            if (rk == 1) launch_route<float, 2, 2, 2, false>(seg, nr, s, zz, pp, ROUTE_ARGS, (float*)nullptr, (const float*)nullptr);
+            else if (rk == 2) launch_route<float, 2, 2, 1, false>(seg, nr, s, zz, pp, ROUTE_ARGS, dd, (const float*)nullptr);
+            else launch_route<float, 3, 1, 1, false>(seg, nr, s, zz, pp, ROUTE_ARGS, (float*)nullptr, (const float*)nullptr);
         }
 #undef ROUTE_ARGS
     } else if (dtype == OCRK_BF16) {
@@ -763,31 +940,37 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
     if (phase != 2) {
         st = ocrk::launch_status("ocrk_bn_relu_pool_bwd reduce");
         if (st) return st;
-        st = slab_sum(slab, nr, 2 * C, part, phase == 1 ? dsum_out : dsum, dbeta, dgamma, C, accumulate, s);   // dbeta | dgamma
+        st = slab_sum(slab, nr, 2 * C, part, phase == 1 ? dsum_out : dsum, dbeta, from_pooled ? nullptr : dgamma, C,
+                      accumulate, s);   // dbeta | dgamma (pooled: dgamma from the apply walk)
         if (st || phase == 1) return st;
     }
-    if (rk == 1 || rk == 3) {
+    if (rk == 1 || rk == 3 || (rk == 2 && from_pooled)) {
         // pass 2 repeats the window walk (no staged da image): dz and the conv-bias partial sums
-        const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
-        const int nseg = (int)ocrk::cdiv(Wo, BN_ROUTE_SEG);
-        const int64_t tasks = (int64_t)B * Ho * nseg * (C / 8);
-        const int64_t nbr = std::min<int64_t>(nb, ocrk::cdiv(tasks, 256));
-        const int tpb = (int)(ocrk::cdiv(ocrk::cdiv(tasks, nbr), 256) * 256);
+        const WalkGrid wg = walk_grid(B, H, W, C, kh, kw, sw, nb);
+        const int nseg = wg.nseg, tpb = wg.tpb;
+        nr = wg.blocks;
 #define APPLY_ARGS B, H, W, C, mean, invstd, gamma, beta, dp_time_major, nseg, tpb, bslab
+        const bool dg = from_pooled;                  // [bias | dgamma] rows: dgamma summed from z here
         if (dtype == OCRK_BF16) {
             const bf16 *zz = (const bf16*)z, *pp = (const bf16*)dp;
             bf16* dd = (bf16*)dz;
-            if (rk == 1) bn_bwd_route_kernel<bf16, 2, 2, 2, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
-            else bn_bwd_route_kernel<bf16, 3, 1, 1, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+            const float* ds = dsum;
+            if (rk == 1) launch_apply<bf16, 2, 2, 2>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
+            else if (rk == 2) launch_apply<bf16, 2, 2, 1>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
+            else launch_apply<bf16, 3, 1, 1>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
         } else {
             const float *zz = (const float*)z, *pp = (const float*)dp;
             float* dd = (float*)dz;
-            if (rk == 1) bn_bwd_route_kernel<float, 2, 2, 2, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
-            else bn_bwd_route_kernel<float, 3, 1, 1, BN_ROUTE_SEG, true><<<nr, 256, 0, s>>>(zz, pp, APPLY_ARGS, dd, dsum);
+            const float* ds = dsum;
+            if (rk == 1) launch_apply<float, 2, 2, 2>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
+            else if (rk == 2) launch_apply<float, 2, 2, 1>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
+            else launch_apply<float, 3, 1, 1>(dg, seg, nr, s, zz, pp, APPLY_ARGS, dd, ds);
         }
 #undef APPLY_ARGS
         st = ocrk::launch_status("ocrk_bn_relu_pool_bwd apply (window walk)");
-        if (st || !dbias || bias_slab_out) return st;
+        if (st || bias_slab_out) return st;
+        if (dg) return slab_sum(bslab, nr, 2 * C, part, nullptr, dbias, dgamma, C, accumulate, s);
+        if (!dbias) return st;
         return slab_sum(bslab, nr, C, part, nullptr, dbias, nullptr, C, accumulate, s);
     }
     float* bs = (dbias || bias_slab_out) ? bslab : nullptr;
@@ -821,6 +1004,24 @@ extern "C" int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, 
     OCRK_REQUIRE(bias_slab, "ocrk_bn_relu_pool_bwd_slab: bias_slab is required");
     return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
                        dbeta, nullptr, accumulate, bias_slab, ws, ws_bytes, dtype, stream);
+}
+
+// The same with pass 1 read from the forward's pooled output `pooled` (the
+// ocrk_bn_relu_pool_fwd result: same layout as dp) instead of walking z -- see
+// bn_bwd_pooled_sums_kernel (dgamma from xhat = (pooled - beta) / gamma; gamma = 0
+// drops a channel's xhat terms). The window-walk pools only (2x2/[2,2], 2x2/[2,1],
+// [3,1]/[3,1]; other pools take the z form). dgamma is summed from z in the apply
+// walk. bias_slab (or NULL: dbias and dgamma (+)= their sums directly) gets
+// ocrk_bn_bwd_pooled_bias_slab_rows(...) rows of 2C, [bias | dgamma] partials.
+extern "C" int ocrk_bn_relu_pool_bwd_pooled(const void* z, const void* pooled, const void* dp, int B, int H, int W,
+                                            int C, const float* mean, const float* invstd, const float* gamma,
+                                            const float* beta, int kh, int kw, int sh, int sw, int dp_time_major,
+                                            void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                                            float* bias_slab, void* ws, size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(pooled, "ocrk_bn_relu_pool_bwd_pooled: pooled is required");
+    return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
+                       dbeta, bias_slab ? nullptr : dbias, accumulate, bias_slab, ws, ws_bytes, dtype, stream, 0,
+                       nullptr, nullptr, nullptr, pooled);
 }
 
 // The two passes apart, for BatchNorm statistics over several ranks' batches:

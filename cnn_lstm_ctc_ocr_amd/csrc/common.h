@@ -81,6 +81,8 @@ enum Option : int {
     OPT_BEAM_WAVE,            // 1 (default): the one-wave beam search for K <= 16, 0 the block kernel
     OPT_BN_BWD_BLOCKS,        // BN backward pass-1 workgroup cap (2048; 64 .. 8192)
     OPT_BN_ROUTE,             // 1 (default): window-walk BN backward for the non-overlapping pools
+    OPT_BN_ROUTE_SEG,         // pooled columns per thread of the window walk (8; 4, 8 or 16)
+    OPT_BN_ROUTE_NCH,         // channels per thread of the window walk (4; or 8)
     OPT_CONV_TN_ITEMS,        // workgroup cap of the conv weight-gradient TN launches beside the backward (192)
     OPT_CONV_TN4_ITEMS,       // split-K target items of the 4-wave TN conv weight gradients (512)
     OPT_CONV_WGRAD_CUS,       // CUs the channel-block conv weight gradients take (192; 0 = every CU)
@@ -89,6 +91,7 @@ enum Option : int {
     OPT_GEMM_NT_STAGED,       // 1 (default): the NT ring's LDS-staged bf16 epilogue, 0 direct 2-B stores
     OPT_GEMM_PP,              // 1 (default): the ping-pong NT engine for the large plain GEMMs
     OPT_GEMM_PPTN,            // 1 (default): the ping-pong TN engine for the wide weight gradients
+    OPT_PP_MIN_N,             // narrowest plain GEMM (N) on the ping-pong engine (512)
     OPT_GEMM_TN,              // 1 (default): the 4-wave TN engine, 0 the generic engine
     OPT_LSTM_DMA,             // 1 (default): LDS-DMA staging in the per-step LSTM forward kernels
     OPT_LSTM_BWD_DMA,         // 1 (default): LDS-DMA staging in the per-step LSTM backward kernels

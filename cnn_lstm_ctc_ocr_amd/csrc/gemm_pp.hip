@@ -890,7 +890,8 @@ int gemm_pp(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t st
 #endif
     // the convolutions stay on the NT / row engines: routed here (N >= 128) they measured
     // 1.4-2.1x slower per layer and 5.23-5.51 vs 5.08-5.11 ms per step (round 4)
-    if (!all && (amode != A_ROWK || p.N < 512)) return -1;         // OCRK_GEMM_PP=2: every shape (make exp)
+    // plain GEMMs from N >= PP_MIN_N (512: the narrow L1 data gradient, N = 256, stays on NT)
+    if (!all && (amode != A_ROWK || p.N < opt(OPT_PP_MIN_N))) return -1;   // OCRK_GEMM_PP=2: every shape (make exp)
     if (p.N < 96) return -1;
     // 32-bit buffer offsets
     const int64_t a_bytes = (amode == A_ROWK ? (int64_t)p.M * p.lda : (int64_t)p.M * p.convC) * 2;

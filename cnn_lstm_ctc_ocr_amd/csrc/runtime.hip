@@ -37,9 +37,10 @@ constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"CONV_DIRECT", 1}, {"CONV_ROWS", 1}, {"CONV_ROWS_WIDE", 1}, {"CONV_WGRAD_BLOCKS", 1},
     {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0}, {"LSTM_BWD_PB16", 0},
     {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1}, {"PP_PERSIST_NK", 8}, {"PP_DEEP", 0}, {"NT_F32_EXACT", 1}, {"NT_F32_MASK", 1},
-    {"NT_F32_X6", 0}, {"BEAM_WAVE", 1}, {"BN_BWD_BLOCKS", 2048}, {"BN_ROUTE", 1}, {"CONV_TN_ITEMS", 192},
+    {"NT_F32_X6", 0}, {"BEAM_WAVE", 1}, {"BN_BWD_BLOCKS", 2048}, {"BN_ROUTE", 1}, {"BN_ROUTE_SEG", 8}, {"BN_ROUTE_NCH", 4},
+    {"CONV_TN_ITEMS", 192},
     {"CONV_TN4_ITEMS", 512}, {"CONV_WGRAD_CUS", 192}, {"F32_MFMA", 0}, {"GEMM_NT", 1}, {"GEMM_NT_STAGED", 1},
-    {"GEMM_PP", 1}, {"GEMM_PPTN", 1}, {"GEMM_TN", 1}, {"LSTM_DMA", 1}, {"LSTM_BWD_DMA", 1},
+    {"GEMM_PP", 1}, {"GEMM_PPTN", 1}, {"PP_MIN_N", 512}, {"GEMM_TN", 1}, {"LSTM_DMA", 1}, {"LSTM_BWD_DMA", 1},
     {"LSTM_FWD_R16", 1},
 };
 std::atomic<int64_t> g_opts[OPT_COUNT];

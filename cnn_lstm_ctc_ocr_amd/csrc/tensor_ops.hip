@@ -30,31 +30,33 @@ namespace ocrk {
 namespace {
 
 // Column sums of a [nslab][NC] f32 slab matrix in a fixed order, double
-// accumulation. One launch: a 256-thread workgroup per 64 columns, 16 column
-// quads x 16 row groups; a thread's rows are loaded 8 at a time (16-B loads,
-// all in flight) and added in row order, then the 16 row groups meet in LDS
-// in a fixed order. The slab tables here are <= ~2k rows x a few hundred
-// columns (a few hundred KB): one launch beats the two-stage form's two on the
-// step's critical path, and a 4-wave workgroup still finds a CU slot beside
-// the other stream's GEMMs (a 16-wave one waited behind them). Rows not a
+// accumulation. One launch: a 256-thread workgroup per 16 columns, 4 column
+// quads x 64 row groups; a thread's rows are loaded 16 at a time (16-B loads,
+// all in flight) and added in row order, then the 64 row groups meet in LDS in a
+// fixed order. The slab tables here are <= ~2k rows x a few hundred columns (a
+// few hundred KB) and sit on the step's critical path between a BN backward's
+// passes: the previous 64-column / 16-row-group form walked a 2048-row slab in 16
+// dependent rounds on one or two CUs (8-17 us per call in the step); this one in
+// 2 rounds on 4+ CUs. One launch still beats the two-stage form's two, and a
+// 4-wave workgroup finds a CU slot beside the other stream's GEMMs. Rows not a
 // multiple of 4 columns wide (or unaligned) take the two-stage form below.
 __global__ void __launch_bounds__(256)
 slab_sum_fused(const float* __restrict__ slab, int nslab, int NC, int ld, float* __restrict__ res,
                float* __restrict__ dst_lo, float* __restrict__ dst_hi, int split, int accumulate) {
-    constexpr int RG = 16;
-    __shared__ double red[RG][65];
-    const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
-    const int c0 = blockIdx.x * 64 + 4 * cq;
+    constexpr int RG = 64, CQ = 4, U = 16;
+    __shared__ double red[RG][4 * CQ + 1];
+    const int cq = threadIdx.x % CQ, rg = threadIdx.x / CQ;
+    const int c0 = blockIdx.x * 4 * CQ + 4 * cq;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     if (c0 < NC) {
         const float* col = slab + c0;
         int i = rg;
-        for (; i + 7 * RG < nslab; i += 8 * RG) {
-            f32x4 v[8];
+        for (; i + (U - 1) * RG < nslab; i += U * RG) {
+            f32x4 v[U];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(col + (int64_t)(i + u * RG) * ld);
+            for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const f32x4*>(col + (int64_t)(i + u * RG) * ld);
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) s[e] += v[u][e];
         }
@@ -67,8 +69,8 @@ slab_sum_fused(const float* __restrict__ slab, int nslab, int NC, int ld, float*
 #pragma unroll
     for (int e = 0; e < 4; ++e) red[rg][4 * cq + e] = s[e];
     __syncthreads();
-    if (threadIdx.x < 64) {
-        const int c = blockIdx.x * 64 + threadIdx.x;
+    if (threadIdx.x < 4 * CQ) {
+        const int c = blockIdx.x * 4 * CQ + threadIdx.x;
         if (c >= NC) return;
         double t = 0.0;
         for (int y = 0; y < RG; ++y) t += red[y][threadIdx.x];
@@ -115,7 +117,7 @@ int slab_sum(const float* slab, int nslab, int NC, double* part, float* res, flo
              int split, int accumulate, hipStream_t s, int ld) {
     const int l = ld > 0 ? ld : NC;
     if (NC % 4 == 0 && l % 4 == 0 && ((uintptr_t)slab & 15) == 0) {
-        slab_sum_fused<<<(NC + 63) / 64, 256, 0, s>>>(slab, nslab, NC, l, res, dst_lo, dst_hi, split, accumulate);
+        slab_sum_fused<<<(NC + 15) / 16, 256, 0, s>>>(slab, nslab, NC, l, res, dst_lo, dst_hi, split, accumulate);
         return ocrk::launch_status("slab sum");
     }
     slab_sum_stage1<<<dim3((NC + 63) / 64, SLAB_P), 256, 0, s>>>(slab, nslab, NC, ld > 0 ? ld : NC, part);

@@ -248,14 +248,17 @@ def bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=False):
 
 
 def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate=True,
-                     dbias=None, defer=None, sync=None):
+                     dbias=None, defer=None, sync=None, pooled=None):
     """dz of BN + ReLU + max-pool; dgamma, dbeta and (optionally) dbias = column
     sums of dz (the conv bias in front of the BN) accumulate in f32. With a
     `defer` list the dbias reduction is appended to it as (fn, tensors)
     (ocrk_bn_relu_pool_bwd_slab + ocrk_slab_sum, same bits). sync = (group,
     count): SyncBN -- the batch statistics were bn_finalize_sync's, so the
-    backward's two sums are SUM-all-reduced over `group` between its passes."""
-    _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta, dbias)
+    backward's two sums are SUM-all-reduced over `group` between its passes.
+    pooled: the forward's output (bn_relu_pool_fwd's result, dp's layout) -- the
+    dgamma / dbeta pass then streams it and dp instead of walking z
+    (ocrk_bn_relu_pool_bwd_pooled; not with sync)."""
+    _chk(z, dp, mean, invstd, gamma, beta, dgamma, dbeta, dbias, pooled)
     B, H, W, C = z.shape
     kh, kw, sh, sw = pool
     nb = _lib.lib().ocrk_bn_bwd_workspace_size(B, H, W, C)
@@ -264,6 +267,23 @@ def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgam
     if sync is not None:
         return _bn_bwd_sync(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgamma, dbeta, accumulate, dbias,
                             defer, sync, dz, ws, nb)
+    if pooled is not None:
+        if pooled.shape != dp.shape or pooled.dtype != dp.dtype:
+            raise ValueError("pooled must have dp's shape and dtype")
+        slab = None
+        if dbias is not None and defer is not None:
+            # [bias | dgamma] partial rows: both reductions deferred
+            rows = _lib.lib().ocrk_bn_bwd_pooled_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
+            slab = torch.empty(rows, 2 * C, dtype=torch.float32, device=z.device)
+        call("ocrk_bn_relu_pool_bwd_pooled", ptr(z), ptr(pooled), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd),
+             ptr(gamma), ptr(beta), kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta),
+             ptr(dbias), int(accumulate), ptr(slab), ptr(ws), nb, dtype_code(z.dtype), _stream(z))
+        if slab is not None:
+            def _late():
+                slab_sum(slab, rows, C, 2 * C, dbias, accumulate)
+                slab_sum(slab.view(-1)[C:], rows, C, 2 * C, dgamma, accumulate)
+            defer.append((_late, (slab,)))
+        return dz
     if dbias is not None and defer is not None:
         rows = _lib.lib().ocrk_bn_bwd_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
         slab = torch.empty(rows, C, dtype=torch.float32, device=z.device)

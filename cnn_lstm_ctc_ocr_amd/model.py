@@ -133,7 +133,7 @@ class _ConvBlock(torch.autograd.Function):
         p = K.bn_relu_pool_fwd(z, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                POOLS[even], time_major=(k == 4))
         ctx.store, ctx.k = store, k
-        ctx.save_for_backward(x, y_odd, z, mean, invstd)
+        ctx.save_for_backward(x, y_odd, z, mean, invstd, p)
         return p
 
     @staticmethod
@@ -144,7 +144,7 @@ class _ConvBlock(torch.autograd.Function):
     @staticmethod
     def _backward(ctx, dp):
         store, k = ctx.store, ctx.k
-        x, y_odd, z, mean, invstd = ctx.saved_tensors
+        x, y_odd, z, mean, invstd, pooled = ctx.saved_tensors
         dt = store.cfg.dtype
         P, G = store.params, store.grads
         odd, even = f"conv{2 * k - 1}", f"conv{2 * k}"
@@ -160,7 +160,9 @@ class _ConvBlock(torch.autograd.Function):
                                 POOLS[even], dp_time_major=(k == 4),
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
                                 dbias=G[pe + "/bias"], defer=late,      # conv bias grad fused
-                                sync=ctx.bn_sync)
+                                sync=ctx.bn_sync,
+                                # dgamma / dbeta from the saved pooled output instead of a walk over z
+                                pooled=pooled if ctx.bn_sync is None and options.get("POOLED_BN") else None)
         B, H, W, C = dz.shape
         if k > 1:
             _issue(store, late)
@@ -236,6 +238,7 @@ def convnet_layers(inputs, widths, mode, store=None):
     if x.dtype not in (torch.uint8, store.cfg.dtype):
         x = K.cast(x, store.cfg.dtype)
     track = torch.is_grad_enabled() and training
+    store.prefetch_images()                                # beside conv1 (f32 weights, no image)
     h = x
     for k in (1, 2, 3, 4):
         variables = _block_variables(store, k) if track else []

@@ -23,6 +23,8 @@ _HOST_DEFAULTS = {
     "DEFER_BIAS": 0,          # 1: bias reductions on their own stream (measured slower)
     "DEFER_DWX": 0,           # 1: an upper layer's dW_x behind the lower BPTT (measured no gain)
     "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
+    "PREFETCH_IMAGES": 0,     # 1: the weight-image refresh on its own stream beside conv1 (measured slower)
+    "POOLED_BN": 1,           # 0: the BN backward's dgamma / dbeta pass walks z instead of the pooled output
     "CONV1_FUSED": 1,         # 0: conv2's backward-data stores dy1, conv1's weight gradient re-reads it
     "TN_ITEMS": 256,          # workgroup cap of the recurrent weight-gradient launches
     "TN_ITEMS_L1": 160,       # the same for the first layer (beside the conv backward)
@@ -37,8 +39,8 @@ _HOST_DEFAULTS = {
 KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOCKS", "LSTM_SPIN_LIMIT",
                   "PERSIST_LATE", "LSTM_BWD_KSPLIT", "LSTM_BWD_PB16", "LSTM_BWD_R16", "CTC_LDS",
                   "PP_PERSIST_NK", "PP_DEEP", "NT_F32_EXACT", "NT_F32_MASK",
-                  "NT_F32_X6", "BEAM_WAVE", "BN_BWD_BLOCKS", "BN_ROUTE", "CONV_TN_ITEMS", "CONV_TN4_ITEMS",
-                  "CONV_WGRAD_CUS", "F32_MFMA", "GEMM_NT", "GEMM_NT_STAGED", "GEMM_PP", "GEMM_PPTN", "GEMM_TN",
+                  "NT_F32_X6", "BEAM_WAVE", "BN_BWD_BLOCKS", "BN_ROUTE", "BN_ROUTE_SEG", "BN_ROUTE_NCH", "CONV_TN_ITEMS", "CONV_TN4_ITEMS",
+                  "CONV_WGRAD_CUS", "F32_MFMA", "GEMM_NT", "GEMM_NT_STAGED", "GEMM_PP", "GEMM_PPTN", "PP_MIN_N", "GEMM_TN",
                   "LSTM_DMA", "LSTM_BWD_DMA", "LSTM_FWD_R16")
 
 

@@ -90,8 +90,9 @@ const char* ocrk_last_error(void);
  * "OCRK_" prefix is optional in `name`). Names: CONV_DIRECT, CONV_ROWS,
  * CONV_ROWS_WIDE, CONV_WGRAD_BLOCKS, LSTM_SPIN_LIMIT, PERSIST_LATE,
  * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP, NT_F32_EXACT,
- * NT_F32_MASK, NT_F32_X6, BEAM_WAVE, BN_BWD_BLOCKS, BN_ROUTE, CONV_TN_ITEMS, CONV_TN4_ITEMS,
- * CONV_WGRAD_CUS, F32_MFMA, GEMM_NT, GEMM_NT_STAGED, GEMM_PP, GEMM_PPTN, GEMM_TN, LSTM_DMA,
+ * NT_F32_MASK, NT_F32_X6, BEAM_WAVE, BN_BWD_BLOCKS, BN_ROUTE, BN_ROUTE_SEG,
+ * BN_ROUTE_NCH, CONV_TN_ITEMS, CONV_TN4_ITEMS,
+ * CONV_WGRAD_CUS, F32_MFMA, GEMM_NT, GEMM_NT_STAGED, GEMM_PP, GEMM_PPTN, PP_MIN_N, GEMM_TN, LSTM_DMA,
  * LSTM_BWD_DMA, LSTM_FWD_R16 (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
 
@@ -274,6 +275,21 @@ int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, int H, int 
                                int sh, int sw, int dp_time_major, void* dz, float* dgamma, float* dbeta,
                                int accumulate, float* bias_slab, void* ws, size_t ws_bytes, int dtype,
                                void* stream);
+/* The same with pass 1 (the dgamma / dbeta sums) read from the forward's pooled
+ * output `pooled` (ocrk_bn_relu_pool_fwd's result, laid out as dp) instead of walking
+ * z: sum dy = sum_{pooled > 0} dp, sum dy * xhat = sum_{pooled > 0} dp (pooled - beta) / gamma
+ * (xhat recovered at each window's max; gamma = 0 drops that channel's xhat terms).
+ * Window-walk pools only (2x2/[2,2], 2x2/[2,1], [3,1]/[3,1]); others take the z form.
+ * dgamma itself is summed from z in the apply walk (xhat as the z form computes it).
+ * bias_slab: NULL (dbias (+)= the conv-bias gradient) or the caller's
+ * [ocrk_bn_bwd_pooled_bias_slab_rows(...)][2C] partial rows [bias | dgamma] -- both
+ * reductions are then the caller's (ocrk_slab_sum over each half; dbias ignored). */
+size_t ocrk_bn_bwd_pooled_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw);
+int ocrk_bn_relu_pool_bwd_pooled(const void* z, const void* pooled, const void* dp, int B, int H, int W, int C,
+                                 const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                 int kh, int kw, int sh, int sw, int dp_time_major, void* dz, float* dgamma,
+                                 float* dbeta, float* dbias, int accumulate, float* bias_slab, void* ws,
+                                 size_t ws_bytes, int dtype, void* stream);
 /* The backward's two passes apart, for SyncBN: _reduce accumulates this rank's
  * dgamma / dbeta and writes dsum f32 [2C] (sum dy | sum dy*xhat through the ReLU
  * and pool routing); SUM-all-reduce dsum over the ranks; _apply forms dz from

@@ -27,8 +27,12 @@ def _bf(a):
     return torch.from_numpy(np.ascontiguousarray(a, np.float32)).bfloat16().float().numpy()
 
 
+@pytest.mark.parametrize("pooled", [False, True])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:4])) + f"-p{''.join(map(str, c[4]))}")
-def test_bn_bwd_bf16_vs_oracle(cuda, case):
+def test_bn_bwd_bf16_vs_oracle(cuda, case, pooled):
+    """pooled: the dgamma / dbeta pass streams the forward's pooled output and dp
+    (ocrk_bn_relu_pool_bwd_pooled; xhat at each window's max recovered from the bf16
+    output for the dz correction term, dgamma itself summed from z in the apply walk)."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     B, H, W, C, pool = case
     rng = np.random.default_rng(B * H + W + C)
@@ -47,7 +51,8 @@ def test_bn_bwd_bf16_vs_oracle(cuda, case):
 
     dg, db = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
     dbias = torch.zeros(C, device=cuda)
-    dz = Kn.bn_relu_pool_bwd(zd, dpd, mean_d, inv_d, t(gamma), t(beta), pool, tm, dg, db, accumulate=False, dbias=dbias)
+    dz = Kn.bn_relu_pool_bwd(zd, dpd, mean_d, inv_d, t(gamma), t(beta), pool, tm, dg, db, accumulate=False, dbias=dbias,
+                             pooled=p if pooled else None)
     torch.cuda.synchronize()
     got = dz.float().cpu().numpy(), dg.cpu().numpy(), db.cpu().numpy(), dbias.cpu().numpy()
     scale = np.abs(got[0]).max()
@@ -62,3 +67,48 @@ def test_bn_bwd_bf16_vs_oracle(cuda, case):
     assert rel(got[1], dg_ref) < 1e-3
     assert rel(got[2], db_ref) < 1e-3
     assert np.abs(got[3] - dz_ref.sum(axis=(0, 1, 2))).max() <= 1e-3 * scale * np.sqrt(B * H * W)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", CASES[:4], ids=lambda c: "x".join(map(str, c[:4])))
+def test_bn_bwd_pooled_matches_z_form(cuda, case, dtype):
+    """The pooled-output pass 1 against the z walk on the same inputs: dbeta is the
+    same terms (another order), dgamma is summed from z in both; dz differs only
+    through sum(da * xhat), whose xhat the pooled form recovers as (p - beta) / gamma
+    (bf16 p: ~2^-9 per term, so the correction term moves by ~1e-3 of itself; f32 p:
+    rounding level). Also the deferred form: [bias | dgamma] partial rows summed by
+    the caller give the same dbias / dgamma."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    B, H, W, C, pool = case
+    rng = np.random.default_rng(7 * C + W)
+    tm = pool == (3, 1, 3, 1)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(cuda)   # noqa: E731
+    z = t(rng.standard_normal((B, H, W, C)) * 1.5 + 0.3).to(dtype)
+    mean, inv = t(rng.standard_normal(C) * 0.1 + 0.3), t(rng.random(C) * 0.3 + 0.5)
+    gamma, beta = t(rng.random(C) + 0.5), t(rng.standard_normal(C) * 0.2)
+    p = Kn.bn_relu_pool_fwd(z, mean, inv, gamma, beta, pool, time_major=tm)
+    dp = t(rng.standard_normal(p.shape)).to(dtype)
+    outs = []
+    for form in ("z", "pooled", "pooled-deferred"):
+        dg, db, dbias = (torch.zeros(C, device=cuda) for _ in range(3))
+        late = [] if form == "pooled-deferred" else None
+        dz = Kn.bn_relu_pool_bwd(z, dp, mean, inv, gamma, beta, pool, tm, dg, db, accumulate=False, dbias=dbias,
+                                 defer=late, pooled=None if form == "z" else p)
+        for fn, _ in late or []:
+            fn()
+        torch.cuda.synchronize()
+        outs.append((dz.double().cpu().numpy(), dg.double().cpu().numpy(), db.double().cpu().numpy(),
+                     dbias.double().cpu().numpy()))
+    rel = lambda x, r: float(np.linalg.norm(x - r) / max(np.linalg.norm(r), 1e-30))   # noqa: E731
+    ref = outs[0]
+    dz_tol = 4e-3 if dtype == torch.bfloat16 else 1e-5
+    for got in outs[1:]:
+        assert rel(got[0], ref[0]) < dz_tol
+        assert rel(got[1], ref[1]) < 1e-5                 # dgamma: from z in both forms
+        assert rel(got[2], ref[2]) < 1e-5                 # dbeta: the same terms
+        # dbias = sum dz = -gamma invstd bm sum(xhat) here (mean is not z's batch mean, so
+        # sum(xhat) != 0): it moves with bm itself; bounded like the oracle test's dbias
+        scale = np.abs(ref[0]).max()
+        assert np.abs(got[3] - ref[3]).max() <= (1e-3 if dtype == torch.bfloat16 else 1e-5) * scale * np.sqrt(B * H * W)
+    np.testing.assert_array_equal(outs[1][0], outs[2][0])   # deferral moves no dz bit
+    np.testing.assert_allclose(outs[2][1], outs[1][1], rtol=1e-6, atol=1e-6 * np.abs(outs[1][1]).max())

@@ -38,6 +38,8 @@ for name, H, W, C, pool, tm in LAYERS:
     dg, db, dbias = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     tf = timed(lambda: K.bn_relu_pool_fwd(z, mean, invstd, gamma, beta, pool, time_major=tm))
     tb = timed(lambda: K.bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, tm, dg, db, dbias=dbias))
+    tp = timed(lambda: K.bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, tm, dg, db, dbias=dbias, pooled=y))
     zb, yb = z.numel() * 2, y.numel() * 2
     print(f"{name} z {tuple(z.shape)}  fwd {tf:7.1f} us (floor {(zb + yb) / 8e6:5.1f})   "
-          f"bwd {tb:7.1f} us (floor {(2 * zb + yb) / 8e6:5.1f}; staged da image +{2 * zb / 8e6:.1f})", flush=True)
+          f"bwd {tb:7.1f} us (floor {(2 * zb + yb) / 8e6:5.1f}; staged da image +{2 * zb / 8e6:.1f})   "
+          f"bwd pooled {tp:7.1f} us", flush=True)
