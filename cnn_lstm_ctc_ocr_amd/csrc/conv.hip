@@ -327,6 +327,14 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
 int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin, int cout, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, hipStream_t s);
 bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout);
+bool conv_rows_fwd_bits_covers(int B, int H, int W, int cin, int cout);
+int conv_rows_fwd_bits(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,
+                       void* y, void* bits, hipStream_t s);
+bool conv_rows_dgrad_bits_covers(int B, int H, int W, int cin, int cout);
+int conv_rows_dgrad_bits(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                         const void* bits, float* stats, hipStream_t s);
+bool gemm_nt_enabled();
+bool nt_staged_enabled();
 int64_t conv_rows_dgrad_c1_parts(int B);
 int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
                        const void* relu_bits, const void* x, int x_is_u8, float* part, hipStream_t s);
@@ -409,7 +417,7 @@ static int64_t bwd_data_tiles(int B, int H, int W) { return ocrk::cdiv((int64_t)
 
 // dx (and, with stats, the per-tile column statistics of the masked dx)
 static int bwd_data_run(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
-                        const void* relu_mask, float* stats, int dtype, hipStream_t s) {
+                        const void* relu_mask, float* stats, int dtype, hipStream_t s, const void* relu_bits = nullptr) {
     ocrk::GemmParams p = {};
     p.M = B * H * W; p.N = cin; p.K = 9 * cout; p.batch = 1;
     p.A = dy; p.B = w_bwd; p.ldb = 9 * cout;
@@ -418,15 +426,79 @@ static int bwd_data_run(const void* dy, int B, int H, int W, int cout, const voi
     p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
     p.convH = H; p.convW = W; p.convC = cout;
     p.stats = stats;
+    if (relu_bits) {                         // the bit-mask routes only (rows kernel, else the NT engine)
+        const int sb = ocrk::conv_rows_dgrad_bits(dy, B, H, W, cout, w_bwd, cin, dx, relu_bits, stats, s);
+        if (sb >= 0) return sb;
+        p.mask = nullptr;
+        p.mask_bits = relu_bits;
+        return ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
+    }
     int st = dtype == OCRK_BF16 ? ocrk::conv_rows_dgrad(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s) : -1;
     if (st < 0 && dtype == OCRK_BF16) st = ocrk::conv_direct_bwd_data(dy, B, H, W, cout, w_bwd, cin, dx, relu_mask, stats, s);
     if (st < 0) st = ocrk::gemm(p, ocrk::A_IM2COL_FLIP, ocrk::B_NK, dtype, s);
     return st;
 }
 
+// ReLU bit masks between an odd conv's forward and the next even conv's backward-data
+// (conv3 -> conv4, conv5 -> conv6, conv7 -> conv8 in the path): the forward writes
+// relu_bits [B*H*W][cout/8] (bit c of byte c/8: y[..][c] > 0) beside y, the data gradient
+// reads them instead of the bf16 y -- 1/16 of the mask bytes. Covered: bf16 on the wide
+// row kernels (forward 32->64, 64->64, 64->128; backward-data 64<-64) or the NT engine's
+// staged epilogue (channels a multiple of 8, K = 9 Cin >= 512 or Cout <= 64).
+static bool nt_bits_ok(int cin, int cout) {
+    return ocrk::gemm_nt_enabled() && ocrk::nt_staged_enabled() && cin % 8 == 0 && cout % 8 == 0 &&
+           (9 * cin >= 512 || cout <= 64);
+}
+
+extern "C" int ocrk_conv3x3_fwd_relu_bits_supported(int B, int H, int W, int cin, int cout, int dtype) {
+    if (dtype != OCRK_BF16 || B < 1 || H < 1 || W < 1 || (int64_t)B * H * W >= (1ll << 31)) return 0;
+    return ocrk::conv_rows_fwd_bits_covers(B, H, W, cin, cout) || nt_bits_ok(cin, cout) ? 1 : 0;
+}
+
+extern "C" int ocrk_conv3x3_fwd_relu_bits(const void* x, int B, int H, int W, int cin, const void* w_nk,
+                                          const float* bias, int cout, void* y, void* relu_bits, int dtype,
+                                          void* stream) {
+    OCRK_REQUIRE(relu_bits && ocrk_conv3x3_fwd_relu_bits_supported(B, H, W, cin, cout, dtype),
+                 "ocrk_conv3x3_fwd_relu_bits: B=%d H=%d W=%d %d->%d dtype=%d not covered", B, H, W, cin, cout, dtype);
+    hipStream_t s = ocrk::as_stream(stream);
+    const int st = ocrk::conv_rows_fwd_bits(x, B, H, W, cin, w_nk, bias, cout, y, relu_bits, s);
+    if (st >= 0) return st;
+    ocrk::GemmParams p = {};
+    p.M = B * H * W; p.N = cout; p.K = 9 * cin; p.batch = 1;
+    p.A = x; p.B = w_nk; p.ldb = 9 * cin;
+    p.C = y; p.ldc = cout; p.c_bf16 = 1;
+    p.bias = bias; p.relu = 1; p.alpha = 1.f;
+    p.splits = 1; p.k_chunk = (int)ocrk::cdiv(p.K, 32) * 32;
+    p.convH = H; p.convW = W; p.convC = cin;
+    p.relu_bits = relu_bits;
+    return ocrk::gemm(p, ocrk::A_IM2COL, ocrk::B_NK, dtype, s);
+}
+
+extern "C" int ocrk_conv3x3_bwd_data_bits_supported(int B, int H, int W, int cout, int cin, int dtype) {
+    if (dtype != OCRK_BF16 || B < 1 || H < 1 || W < 1 || (int64_t)B * H * W >= (1ll << 31)) return 0;
+    return ocrk::conv_rows_dgrad_bits_covers(B, H, W, cin, cout) || nt_bits_ok(cout, cin) ? 1 : 0;
+}
+
 extern "C" size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin) {
     return ((size_t)bwd_data_tiles(B, H, W) * 2 * cin * sizeof(float) + 7) / 8 * 8 +
            (size_t)ocrk::SLAB_P * cin * sizeof(double);
+}
+
+// ocrk_conv3x3_bwd_data with the mask as the producer's bit mask (ocrk_conv3x3_fwd_relu_bits)
+extern "C" int ocrk_conv3x3_bwd_data_bits(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
+                                          void* dx, const void* relu_bits, float* dbias, int accumulate, void* ws,
+                                          size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(relu_bits && ocrk_conv3x3_bwd_data_bits_supported(B, H, W, cout, cin, dtype),
+                 "ocrk_conv3x3_bwd_data_bits: B=%d H=%d W=%d %d<-%d dtype=%d not covered", B, H, W, cin, cout, dtype);
+    hipStream_t s = ocrk::as_stream(stream);
+    if (!dbias) return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, nullptr, nullptr, dtype, s, relu_bits);
+    OCRK_REQUIRE(ws && ws_bytes >= ocrk_conv3x3_bwd_data_workspace_size(B, H, W, cin),
+                 "ocrk_conv3x3_bwd_data_bits: workspace too small for the bias gradient");
+    int st = bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, nullptr, (float*)ws, dtype, s, relu_bits);
+    if (st) return st;
+    const int tiles = (int)bwd_data_tiles(B, H, W);
+    double* part = (double*)((char*)ws + ((size_t)tiles * 2 * cin * sizeof(float) + 7) / 8 * 8);
+    return ocrk::slab_sum((const float*)ws, tiles, cin, part, nullptr, dbias, nullptr, cin, accumulate, s, 2 * cin);
 }
 
 extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd,

@@ -866,10 +866,12 @@ struct RfCfg {
     static constexpr int PH = KS >= 4 && NW > 4 ? 2 : 1;    // pixel parts per row (register budget)
 };
 
+// bits (RELU only, or NULL): the output's ReLU bit mask, [B*H*W][CO/8] bytes, bit c = channel c > 0
 template <int CI, int CO, int KPX, int CS, bool RELU>
 __global__ void __launch_bounds__((RfCfg<CI, CO, KPX, CS>::NT), (RfCfg<CI, CO, KPX, CS>::PER_CU))
 conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn, const float* __restrict__ bias,
-                           bf16* __restrict__ y, float* __restrict__ stats, int B, int H, int W) {
+                           bf16* __restrict__ y, float* __restrict__ stats, int B, int H, int W,
+                           uint16_t* __restrict__ bits) {
     using C = RfCfg<CI, CO, KPX, CS>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -973,6 +975,17 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
                     o[1] = pack_bf16x2(acc[n][2], acc[n][3]);
                     *reinterpret_cast<u32x2*>(orow + (size_t)px * CO + 16 * wave + 4 * g) = o;
                 }
+                if constexpr (RELU) {
+                    if (bits) {                            // the 4 lanes of a pixel: 16 channels -> one u16
+                        unsigned m = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) m |= (acc[n][e] > 0.f ? 1u : 0u) << (4 * g + e);
+                        m |= __shfl_xor(m, 16, 64);
+                        m |= __shfl_xor(m, 32, 64);
+                        if (g == 0 && px < W) bits[((size_t)b * H + h) * W * (CO / 16) + (size_t)px * (CO / 16) + wave] =
+                            (uint16_t)m;
+                    }
+                }
             }
             if (stats) {
                 const int p0 = 16 * PP * ph;
@@ -1028,17 +1041,17 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
 
 template <int CI, int CO, int KPX, int CS = 1>
 static int launch_fwd_co(const void* x, int B, int H, int W, const void* w_nk, const float* bias, void* y, int relu,
-                         float* stats, hipStream_t s) {
+                         float* stats, hipStream_t s, void* relu_bits = nullptr) {
     using C = RfCfg<CI, CO, KPX, CS>;
     static DeviceOnce cfg, cfg_r;
     if (relu) {
         set_dyn_lds(cfg_r, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, true>), C::LDS);
         conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, true><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
-            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W);
+            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W, (uint16_t*)relu_bits);
     } else {
         set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, false>), C::LDS);
         conv3x3_fwd_rows_co_kernel<CI, CO, KPX, CS, false><<<B * C::BANDS * CS, C::NT, C::LDS, s>>>(
-            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W);
+            (const bf16*)x, (const bf16*)w_nk, bias, (bf16*)y, stats, B, H, W, nullptr);
     }
     return launch_status("conv3x3_fwd_rows_co");
 }
@@ -1064,7 +1077,9 @@ struct RbCfg {
     static constexpr int BANDS = PER_CU;
 };
 
-template <int CI, int CO, int KPX, int CS>
+// MB: `mask` is the producer's ReLU bit mask ([B*H*W][CI/8] bytes, bit c = channel c), 2 B per
+// (pixel, wave) instead of the bf16 output's 8 B per lane
+template <int CI, int CO, int KPX, int CS, bool MB = false>
 __global__ void __launch_bounds__((RbCfg<CI, CO, KPX, CS>::NT), (RbCfg<CI, CO, KPX, CS>::PER_CU))
 conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb,
                              const bf16* __restrict__ mask, bf16* __restrict__ dx, float* __restrict__ stats,
@@ -1130,11 +1145,18 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
             rw_barrier();
             load_row(drow(min(h + 3, H - 1)), sx[1 - P]);
             u32x2 mk[C::PT];
-            const bf16* mrow = mask ? mask + ((size_t)b * H + h) * W * CI : nullptr;
-            if (mask) {
+            unsigned mbv[C::PT];
+            if constexpr (MB) {
+                const uint16_t* mrow = reinterpret_cast<const uint16_t*>(mask) + ((size_t)b * H + h) * W * (CI / 16);
 #pragma unroll
-                for (int n = 0; n < C::PT; ++n)
-                    mk[n] = *reinterpret_cast<const u32x2*>(mrow + (size_t)min(16 * n + i16, W - 1) * CI + 16 * wave + 4 * g);
+                for (int n = 0; n < C::PT; ++n) mbv[n] = mrow[(size_t)min(16 * n + i16, W - 1) * (CI / 16) + wave];
+            } else {
+                const bf16* mrow = mask ? mask + ((size_t)b * H + h) * W * CI : nullptr;
+                if (mask) {
+#pragma unroll
+                    for (int n = 0; n < C::PT; ++n)
+                        mk[n] = *reinterpret_cast<const u32x2*>(mrow + (size_t)min(16 * n + i16, W - 1) * CI + 16 * wave + 4 * g);
+                }
             }
             floatx4 acc[C::PT];
 #pragma unroll
@@ -1160,7 +1182,11 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
                 float v[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = acc[n][e];
-                if (mask) {
+                if constexpr (MB) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (!((mbv[n] >> (4 * g + e)) & 1u)) v[e] = 0.f;
+                } else if (mask) {
 #pragma unroll
                     for (int e2 = 0; e2 < 2; ++e2) {
                         const unsigned m = mk[n][e2];
@@ -1204,7 +1230,7 @@ conv3x3_dgrad_rows_co_kernel(const bf16* __restrict__ dy, const bf16* __restrict
     }
 }
 
-template <int CI, int CO, int KPX, int CS = 1>
+template <int CI, int CO, int KPX, int CS = 1, bool MB = false>
 static int launch_dgrad_co(const void* dy, int B, int H, int W, const void* w_bwd, void* dx, const void* mask,
                            float* stats, hipStream_t s) {
     using C = RbCfg<CI, CO, KPX, CS>;
@@ -1212,8 +1238,8 @@ static int launch_dgrad_co(const void* dy, int B, int H, int W, const void* w_bw
     const int64_t trows = cdiv((int64_t)B * H * W, 128);
     if (stats && trows < B * C::BANDS) return -1;  // the table has fewer rows than band workgroups
     static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS>), C::LDS);
-    conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS><<<grid, C::NT, C::LDS, s>>>(
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS, MB>), C::LDS);
+    conv3x3_dgrad_rows_co_kernel<CI, CO, KPX, CS, MB><<<grid, C::NT, C::LDS, s>>>(
         (const bf16*)dy, (const bf16*)w_bwd, (const bf16*)mask, (bf16*)dx, stats, (int)trows, B, H, W);
     return launch_status("conv3x3_dgrad_rows_co");
 }
@@ -1286,6 +1312,30 @@ int conv_rows_dgrad(const void* dy, int B, int H, int W, int cout, const void* w
                                                                    (const bf16*)relu_mask, (bf16*)dx, B, H, W,
                                                                    nullptr, nullptr);
     return launch_status("conv3x3_dgrad_rows");
+}
+
+// ReLU bit masks on the wide row kernels: the forward of conv3 / conv5 (32 -> 64, 64 -> 128;
+// 64 -> 64 too) writes its output's bits, conv4's backward-data (64 <- 64) reads them
+bool conv_rows_fwd_bits_covers(int B, int H, int W, int cin, int cout) {
+    return conv_rows_fwd_covers(B, H, W, cin, cout) && !(cin == RW_CI && cout == RW_CO);
+}
+
+int conv_rows_fwd_bits(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,
+                       void* y, void* bits, hipStream_t s) {
+    if (!conv_rows_fwd_bits_covers(B, H, W, cin, cout)) return -1;
+    if (cin == 32) return launch_fwd_co<32, 64, 128>(x, B, H, W, w_nk, bias, y, 1, nullptr, s, bits);
+    if (cout == 64) return launch_fwd_co<64, 64, 128>(x, B, H, W, w_nk, bias, y, 1, nullptr, s, bits);
+    return launch_fwd_co<64, 128, 128>(x, B, H, W, w_nk, bias, y, 1, nullptr, s, bits);
+}
+
+bool conv_rows_dgrad_bits_covers(int B, int H, int W, int cin, int cout) {
+    return rows_enabled() && rows_wide_enabled() && B >= 1 && H >= 1 && W >= 1 && W <= 128 && cin == 64 && cout == 64;
+}
+
+int conv_rows_dgrad_bits(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin, void* dx,
+                         const void* bits, float* stats, hipStream_t s) {
+    if (!conv_rows_dgrad_bits_covers(B, H, W, cin, cout)) return -1;
+    return launch_dgrad_co<64, 64, 128, 1, true>(dy, B, H, W, w_bwd, dx, bits, stats, s);
 }
 
 bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout) {

@@ -40,6 +40,11 @@ struct GemmParams {
     int k_chunk;                   // k-range per split (multiple of 32)
     int convH, convW, convC;       // im2col source geometry (NHWC) for the A_IM2COL* modes
     int epi_staged;                // gemm_nt (set by it): bf16 C (and the mask) move through an LDS tile
+    // ReLU bit masks (bit c of byte c/8 of row m: column c > 0; rows of N/8 bytes), NT engine,
+    // staged bf16 epilogue only: mask_bits replaces `mask` as C's mask; relu_bits receives
+    // the bit mask of the (ReLU) output C
+    const void* mask_bits;
+    void* relu_bits;
 };
 
 // XCD-aware tile order for a 1-D grid of 8 * ceil(tm * tn / 8) workgroups.

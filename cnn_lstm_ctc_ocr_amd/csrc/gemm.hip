@@ -596,6 +596,11 @@ int gemm(const GemmParams& p, int amode, int bmode, int dtype, hipStream_t strea
     OCRK_REQUIRE(amode < A_IM2COL || p.convC % 8 == 0, "gemm: conv channels must be a multiple of 8");
     OCRK_REQUIRE(!(p.stats && (p.splits > 1 || p.batch > 1)), "gemm: stats need splits=1, batch=1");
     OCRK_REQUIRE(!(p.accumulate && p.c_bf16), "gemm: accumulate needs an f32 C");
+    if (p.mask_bits || p.relu_bits) {                   // bit masks: the NT engine's staged epilogue only
+        const int st = gemm_nt(p, amode, bmode, dtype, stream);
+        OCRK_REQUIRE(st >= 0, "gemm: ReLU bit masks need the NT engine (bf16 C, staged epilogue) for this shape");
+        return st;
+    }
     int nt = gemm_pp(p, amode, bmode, dtype, stream);
     if (nt >= 0) return nt != OCRK_OK ? nt : splitk_finish(p, stream);
     nt = gemm_nt(p, amode, bmode, dtype, stream);

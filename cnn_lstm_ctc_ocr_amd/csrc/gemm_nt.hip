@@ -317,12 +317,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     constexpr bool TILE_FITS = T_OFF + BM * TP <= S * STAGE;
     const bool staged = TILE_FITS && p.epi_staged;
     char* tile = smem + T_OFF;
-    if (staged && mask) {
+    const uint8_t* mbits = reinterpret_cast<const uint8_t*>(p.mask_bits);
+    if (staged && (mask || mbits)) {
         for (int q = tid; q < BM * CPT; q += NW * 64) {
             const int r = q / CPT, cc = q - r * CPT;
             const int row = m0 + r, col = n0 + 8 * cc;
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (row < p.M && col < p.N) v = *reinterpret_cast<const uint4*>(mask + (int64_t)row * p.ldmask + col);
+            if (row < p.M && col < p.N) {
+                if (mbits) {                               // one byte of bits -> 8 bf16 (1.0 or 0)
+                    const unsigned m = mbits[(int64_t)row * (p.N >> 3) + (col >> 3)];
+                    unsigned w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        w[i] = ((m >> (2 * i)) & 1u ? 0x3f80u : 0u) | ((m >> (2 * i + 1)) & 1u ? 0x3f800000u : 0u);
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+                    v = *reinterpret_cast<const uint4*>(mask + (int64_t)row * p.ldmask + col);
+                }
+            }
             *reinterpret_cast<uint4*>(tile + r * TP + cc * 16) = v;
         }
         __syncthreads();
@@ -340,7 +352,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
                 if (row < p.M && col < p.N) {
                     if (staged) {
                         bf16* e = reinterpret_cast<bf16*>(tile + (row - m0) * TP + (col - n0) * 2);
-                        if (mask && !((float)*e > 0.f)) v = 0.f;
+                        if ((mask || mbits) && !((float)*e > 0.f)) v = 0.f;
                         if (p.relu) v = fmaxf(v, 0.f);
                         *e = (bf16)v;
                     } else {
@@ -364,12 +376,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     }
     if (staged) {
         __syncthreads();
+        uint8_t* rbits = reinterpret_cast<uint8_t*>(p.relu_bits);
         for (int q = tid; q < BM * CPT; q += NW * 64) {
             const int r = q / CPT, cc = q - r * CPT;
             const int row = m0 + r, col = n0 + 8 * cc;
-            if (row < p.M && col < p.N)
-                *reinterpret_cast<uint4*>(Cb + (int64_t)row * p.ldc + col) =
-                    *reinterpret_cast<const uint4*>(tile + r * TP + cc * 16);
+            if (row < p.M && col < p.N) {
+                const uint4 v = *reinterpret_cast<const uint4*>(tile + r * TP + cc * 16);
+                *reinterpret_cast<uint4*>(Cb + (int64_t)row * p.ldc + col) = v;
+                if (rbits) {                               // the 8 values' (> 0) bits: one byte
+                    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+                    unsigned m = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        m |= (__uint_as_float(w[i] << 16) > 0.f ? 1u : 0u) << (2 * i);
+                        m |= (__uint_as_float(w[i] & 0xffff0000u) > 0.f ? 1u : 0u) << (2 * i + 1);
+                    }
+                    rbits[(int64_t)row * (p.N >> 3) + (col >> 3)] = (uint8_t)m;
+                }
+            }
         }
     }
     if constexpr (!ST) return;
@@ -515,7 +539,8 @@ int dispatch_nt(const GemmParams& p, hipStream_t s) {
     // N in (64, 96] (the logits, 96 classes): 64 x 96 tiles, three stages -- twice the
     // workgroups of a 128 x 128 tile with no idle columns (19.9 vs 29.9 us at 32000 x 96 x 1024)
     if (p.N <= 96) return launch_nt<64, 96, 64, 3, 2, AM>(p, s);
-    if (p.N >= 512 && p.M >= 16384) return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
+    // (the 256 x 256 tile's C does not fit the staged epilogue: bit masks stay on 128 x 128)
+    if (p.N >= 512 && p.M >= 16384 && !p.mask_bits && !p.relu_bits) return launch_nt<256, 256, 64, 2, 2, AM, 8>(p, s);
     return launch_nt<128, 128, 64, 2, 2, AM>(p, s);
 }
 
@@ -569,6 +594,8 @@ int gemm_nt(const GemmParams& p0, int amode, int bmode, int dtype, hipStream_t s
     // wide N with short K (a few k-steps: store-bound) runs better on the
     // generic engine's three resident workgroups per CU (measured)
     if (p.K % 8 != 0 || (p.k_chunk < 512 && p.N > 64)) return -1;
+    // bit masks (mask_bits / relu_bits) live in the staged epilogue only
+    if ((p.mask_bits || p.relu_bits) && (!p.epi_staged || p.batch != 1 || p.ldc != p.N)) return -1;
     if (amode == A_ROWK) {
         if (p.lda % 8 != 0 || p.ldb % 8 != 0) return -1;          // 16-B aligned rows
         return dispatch_nt<A_ROWK>(p, stream);

@@ -120,6 +120,29 @@ def conv_stats_tiles(M):
     return _lib.lib().ocrk_conv_stats_tiles(M)
 
 
+def relu_bits_ok(x_shape, cin, cout, cout_next, dtype):
+    """The bit-mask pair covers conv_{odd} (cin -> cout, forward with ReLU) and the next
+    conv's (cout -> cout_next) backward-data into it at this [B, H, W] (bf16)."""
+    B, H, W = x_shape[:3]
+    lib = _lib.lib()
+    code = dtype_code(dtype)
+    return (bool(lib.ocrk_conv3x3_fwd_relu_bits_supported(B, H, W, cin, cout, code))
+            and bool(lib.ocrk_conv3x3_bwd_data_bits_supported(B, H, W, cout_next, cout, code)))
+
+
+def conv3x3_fwd_relu_bits(x, w_nk, bias):
+    """conv3x3_fwd(..., relu=True) and its output's ReLU bit mask, u8 [B, H, W, Cout/8]
+    (ocrk_conv3x3_fwd_relu_bits)."""
+    _chk(x, w_nk, bias)
+    B, H, W, Cin = x.shape
+    Cout = w_nk.shape[0]
+    y = torch.empty(B, H, W, Cout, dtype=x.dtype, device=x.device)
+    bits = torch.empty(B, H, W, Cout // 8, dtype=torch.uint8, device=x.device)
+    call("ocrk_conv3x3_fwd_relu_bits", ptr(x), B, H, W, Cin, ptr(w_nk), ptr(bias), Cout, ptr(y), ptr(bits),
+         dtype_code(x.dtype), _stream(x))
+    return y, bits
+
+
 def conv3x3_fwd(x, w_nk, bias, relu, stats=None, y_dtype=None):
     _chk(x, w_nk, bias, stats)
     B, H, W, Cin = x.shape
@@ -131,16 +154,28 @@ def conv3x3_fwd(x, w_nk, bias, relu, stats=None, y_dtype=None):
     return y
 
 
-def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True, defer=None):
+def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True, defer=None, relu_bits=None):
     """dx = conv3x3 backward-data (ReLU mask of the producer fused); if dbias
     is given, dbias (+)= column sums of dx (the producer's bias gradient).
     With a `defer` list, that reduction is appended to it as (fn, tensors) for
     the caller to issue later (e.g. on the side stream): same bits, off the
-    data-gradient path (ocrk_conv3x3_bwd_data_slab + ocrk_slab_sum)."""
-    _chk(dy, w_bwd, relu_mask, dbias)
+    data-gradient path (ocrk_conv3x3_bwd_data_slab + ocrk_slab_sum).
+    relu_bits (instead of relu_mask): the producer's bit mask from
+    conv3x3_fwd_relu_bits (ocrk_conv3x3_bwd_data_bits; no `defer`)."""
+    _chk(dy, w_bwd, relu_mask, dbias, relu_bits)
     B, H, W, Cout = dy.shape
     Cin = w_bwd.shape[0]
     dx = torch.empty(B, H, W, Cin, dtype=dy.dtype, device=dy.device)
+    if relu_bits is not None:
+        if relu_mask is not None or defer is not None:
+            raise ValueError("relu_bits takes neither relu_mask nor defer")
+        nb, ws = 0, None
+        if dbias is not None:
+            nb = _lib.lib().ocrk_conv3x3_bwd_data_workspace_size(B, H, W, Cin)
+            ws = _ws(nb, dy.device)
+        call("ocrk_conv3x3_bwd_data_bits", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_bits),
+             ptr(dbias), int(accumulate), ptr(ws), nb, dtype_code(dy.dtype), _stream(dy))
+        return dx
     if dbias is not None and defer is not None:
         tiles = conv_stats_tiles(B * H * W)
         slab = torch.empty(tiles, 2 * Cin, dtype=torch.float32, device=dy.device)

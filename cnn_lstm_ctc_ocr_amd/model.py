@@ -101,7 +101,13 @@ class _ConvBlock(torch.autograd.Function):
             y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
         else:
             w_nk, _ = store.conv_images(odd, dt)
-            y_odd = K.conv3x3_fwd(x, w_nk, P[f"convnet/{odd}/bias"], relu=True)
+            if (training and dt == torch.bfloat16 and not ctx.exact and options.get("RELU_BITS")
+                    and K.relu_bits_ok(x.shape, x.shape[3], w_nk.shape[0], store.conv_images(even, dt)[0].shape[0],
+                                       dt)):
+                # conv_{2k-1}'s ReLU as a bit mask for conv_{2k}'s backward-data (1/16 of the bytes)
+                y_odd, ctx.relu_bits = K.conv3x3_fwd_relu_bits(x, w_nk, P[f"convnet/{odd}/bias"])
+            else:
+                y_odd = K.conv3x3_fwd(x, w_nk, P[f"convnet/{odd}/bias"], relu=True)
         B, H, W, _ = y_odd.shape
         M = B * H * W
         w_nk, _ = store.conv_images(even, dt)
@@ -182,8 +188,11 @@ class _ConvBlock(torch.autograd.Function):
             store.join()                                   # side-stream weight gradients are in
             return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
-        dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
-                                    defer=late)
+        if k > 1 and ctx.relu_bits is not None and late is None:
+            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, dbias=G[po + "/bias"], relu_bits=ctx.relu_bits)
+        else:
+            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
+                                        defer=late)
         _issue(store, late)
         dx = None
         if k == 1:

@@ -216,6 +216,19 @@ size_t ocrk_conv3x3_bwd_data_workspace_size(int B, int H, int W, int cin);
 int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
                           void* dx, const void* relu_mask, float* dbias, int accumulate, void* ws,
                           size_t ws_bytes, int dtype, void* stream);
+/* ReLU bit masks between an odd conv's forward and the next even conv's backward-data
+ * (conv3 -> conv4, conv5 -> conv6, conv7 -> conv8): _fwd_relu_bits is ocrk_conv3x3_fwd with
+ * relu = 1 that also writes relu_bits u8 [B*H*W][cout/8] (bit c of byte c/8: y[..][c] > 0);
+ * _bwd_data_bits is ocrk_conv3x3_bwd_data with that bit mask as the ReLU mask (1/16 of the
+ * bf16 mask's bytes). bf16 only; *_supported says whether a shape is covered (the wide row
+ * kernels or the NT engine's staged epilogue). */
+int ocrk_conv3x3_fwd_relu_bits_supported(int B, int H, int W, int cin, int cout, int dtype);
+int ocrk_conv3x3_fwd_relu_bits(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias,
+                               int cout, void* y, void* relu_bits, int dtype, void* stream);
+int ocrk_conv3x3_bwd_data_bits_supported(int B, int H, int W, int cout, int cin, int dtype);
+int ocrk_conv3x3_bwd_data_bits(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
+                               void* dx, const void* relu_bits, float* dbias, int accumulate, void* ws,
+                               size_t ws_bytes, int dtype, void* stream);
 /* The same with the bias-gradient reduction left to the caller (e.g. on a side
  * stream, off the data-gradient critical path): slab [ocrk_conv_stats_tiles(B*H*W)]
  * [2*cin] f32 gets the per-tile column (sum, M2) of the masked dx; then

@@ -114,6 +114,37 @@ def test_conv1_fwd_relu_bits(cuda, x_u8):
     np.testing.assert_array_equal(bits.cpu().numpy(), _relu_bits(y.float().cpu().numpy()))
 
 
+@pytest.mark.parametrize("B,H,W,cin,cout,cnext", [(4, 15, 127, 32, 64, 64), (4, 7, 126, 64, 128, 128),
+                                                  (8, 3, 125, 128, 256, 256), (3, 5, 37, 64, 64, 64)])
+def test_relu_bit_masks_conv_pair(cuda, B, H, W, cin, cout, cnext):
+    """conv_{odd}'s forward with its ReLU bit mask (ocrk_conv3x3_fwd_relu_bits: the wide row
+    kernels for conv3 / conv5, the NT engine's staged epilogue for conv7) gives the same y
+    bits as the plain forward and the bits of y > 0; conv_{even}'s backward-data with that
+    bit mask (ocrk_conv3x3_bwd_data_bits: rows kernel for conv4, NT for conv6 / conv8) the
+    same dx and producer bias gradient as with the bf16 y as the mask."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(cin + cout + W)
+    x = torch.from_numpy(_bf(rng.standard_normal((B, H, W, cin)))).to(cuda).bfloat16()
+    w = torch.from_numpy(_bf(rng.standard_normal((3, 3, cin, cout)) / np.sqrt(9 * cin))).to(cuda)
+    b = torch.from_numpy(rng.standard_normal(cout).astype(np.float32) * 0.3).to(cuda)
+    w_nk = Kn.permute3(w, 9 * cin, cout, 1, torch.bfloat16).view(cout, 9 * cin)
+    assert Kn.relu_bits_ok((B, H, W), cin, cout, cnext, torch.bfloat16)
+    y = Kn.conv3x3_fwd(x, w_nk, b, True)
+    y2, bits = Kn.conv3x3_fwd_relu_bits(x, w_nk, b)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    np.testing.assert_array_equal(bits.cpu().numpy(), _relu_bits(y.float().cpu().numpy()))
+    w2 = torch.from_numpy(_bf(rng.standard_normal((3, 3, cout, cnext)) / np.sqrt(9 * cout))).to(cuda)
+    w_bwd = Kn.permute3(w2, 9, cout, cnext, torch.bfloat16).view(cout, 9 * cnext)
+    dz = torch.from_numpy(_bf(rng.standard_normal((B, H, W, cnext)))).to(cuda).bfloat16()
+    db1, db2 = torch.zeros(cout, device=cuda), torch.zeros(cout, device=cuda)
+    dx1 = Kn.conv3x3_bwd_data(dz, w_bwd, relu_mask=y, dbias=db1)
+    dx2 = Kn.conv3x3_bwd_data(dz, w_bwd, dbias=db2, relu_bits=bits)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2)
+    assert torch.equal(db1, db2)
+
+
 @pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70)])
 @pytest.mark.parametrize("x_u8", [True, False])
 @pytest.mark.parametrize("mask", ["bf16", "bits"])
