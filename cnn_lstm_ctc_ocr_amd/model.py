@@ -172,7 +172,8 @@ class _ConvBlock(torch.autograd.Function):
         B, H, W, C = dz.shape
         if k > 1:
             _issue(store, late)
-            with _conv_side(store, y_odd, dz):             # overlaps the data-gradient GEMM below
+            with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):   # overlaps the data gradient below
+                _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
         if k == 1 and not ctx.exact and options.get("CONV1_FUSED") and K.conv2_bwd_data_conv1_wgrad_ok(dz, x):
@@ -180,7 +181,8 @@ class _ConvBlock(torch.autograd.Function):
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
             # contracted as it is produced, never stored: its only consumer is conv1's dW)
             _issue(store, late)
-            with _conv_side(store, y_odd, dz):
+            with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):
+                _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             bits = ctx.relu_bits
             K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, None if bits is not None else y_odd, x, G[po + "/kernel"],
@@ -200,13 +202,20 @@ class _ConvBlock(torch.autograd.Function):
             # conv3's) while conv2's runs here, so the two streams end together
             # (measured against conv2's on a third stream beside the data gradient
             # and conv1's after it on this one: 6.39 vs 6.37 ms)
-            with _conv_side(store, x, dy_odd):
+            with _conv_side(store, x, dy_odd, *_conv_late_tensors(store)):
+                _conv_late_run(store)
                 K.conv1_bwd_weight(x, dy_odd, G[po + "/kernel"], G[po + "/bias"])
             _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             store.join()                                   # side-stream weight gradients are in
         else:
-            with _conv_side(store, x, dy_odd):
-                _conv_wgrad(ctx.exact, x, dy_odd, G[po + "/kernel"])
+            if options.get("CONV_SIDE_MERGE") and options.get("CONV_SIDE") and options.get("SIDE_STREAM"):
+                # the odd conv's weight gradient joins the next side-stream fork (the lower
+                # block's even-conv weight gradient): one fork per block instead of two
+                store.conv_late.append((lambda x=x, d=dy_odd, dw=G[po + "/kernel"], ex=ctx.exact:
+                                        _conv_wgrad(ex, x, d, dw), (x, dy_odd)))
+            else:
+                with _conv_side(store, x, dy_odd):
+                    _conv_wgrad(ctx.exact, x, dy_odd, G[po + "/kernel"])
             if ctx.needs_input_grad[0]:
                 _, w_bwd_odd = store.conv_images(odd, dt)
                 dx = K.conv3x3_bwd_data(dy_odd, w_bwd_odd)
@@ -345,6 +354,21 @@ def _issue(store, late):
         fn, tensors = late.pop(0)
         with side_work(store, *tensors, lane="reduce"):
             fn()
+
+
+def _conv_late_tensors(store):
+    return tuple(t for _, ts in store.conv_late for t in ts)
+
+
+def _conv_late_run(store):
+    """Issue the conv weight gradients queued for this side-stream fork (oldest first).
+    Each fork records an event on the main stream -- a ~6.4 us gap before the next
+    main-stream kernel in the step (profiles/r5e_step_timeline.txt) -- and the side
+    stream is busy past the point a queued gradient could have started, so joining
+    the next fork costs that gradient no time."""
+    late, store.conv_late = store.conv_late, []
+    for fn, _ in late:
+        fn()
 
 
 def _conv_side(store, *tensors):

@@ -140,6 +140,7 @@ class ParamStore:
         self._images = {}
         self.pending = []          # events of side-stream gradient work not yet joined
         self.deferred = []         # (launch fn, tensors) of gradient work an upper layer deferred
+        self.conv_late = []        # (launch fn, tensors): conv weight gradients queued for the next side fork
         self._img_stream = None    # the weight-image refresh's own stream (prefetch_images)
         self._img_wait = None      # its completion, awaited by the first images() consumer
         self.bn_group = None       # SyncBN: the process group TRAIN-mode BatchNorm statistics span
@@ -180,6 +181,9 @@ class ParamStore:
         (model.side_work) so flat_grad is complete in stream order."""
         while self.deferred:        # never issued (no lower layer ran): issue it here, in order
             fn, _tensors = self.deferred.pop(0)
+            fn()
+        while self.conv_late:       # queued conv weight gradients no later fork took: inline, in order
+            fn, _tensors = self.conv_late.pop(0)
             fn()
         if self.pending:
             cur = torch.cuda.current_stream(self.device)
