@@ -67,6 +67,7 @@ SIGNATURES = {
     "ocrk_conv3x3_fwd_relu_bits": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i32, _p],
     "ocrk_conv3x3_bwd_data_bits_supported": [_i32, _i32, _i32, _i32, _i32, _i32],
     "ocrk_conv3x3_bwd_data_bits": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_conv3x3_bwd_data_bits_slab": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p],
     "ocrk_conv3x3_bwd_data_slab": [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i32, _p],
     "ocrk_conv3x3_wgrad_workspace_size": [_i32, _i32, _i32, _i32, _i32],
     "ocrk_conv3x3_bwd_weight": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p],

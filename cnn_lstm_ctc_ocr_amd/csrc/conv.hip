@@ -520,6 +520,16 @@ extern "C" int ocrk_conv3x3_bwd_data(const void* dy, int B, int H, int W, int co
 // rows of 2*cin floats (sums in the first cin); ocrk_slab_sum(slab, tiles, cin,
 // 2*cin, dbias, ...) on any stream ordered after this call gives the dbias of
 // ocrk_conv3x3_bwd_data -- the same bits, off the data-gradient critical path.
+// ocrk_conv3x3_bwd_data_bits with the bias-gradient reduction left to the caller (as _slab)
+extern "C" int ocrk_conv3x3_bwd_data_bits_slab(const void* dy, int B, int H, int W, int cout, const void* w_bwd,
+                                               int cin, void* dx, const void* relu_bits, float* slab, int dtype,
+                                               void* stream) {
+    OCRK_REQUIRE(slab && relu_bits && ocrk_conv3x3_bwd_data_bits_supported(B, H, W, cout, cin, dtype),
+                 "ocrk_conv3x3_bwd_data_bits_slab: B=%d H=%d W=%d %d<-%d dtype=%d not covered (or no slab)", B, H, W,
+                 cin, cout, dtype);
+    return bwd_data_run(dy, B, H, W, cout, w_bwd, cin, dx, nullptr, slab, dtype, ocrk::as_stream(stream), relu_bits);
+}
+
 extern "C" int ocrk_conv3x3_bwd_data_slab(const void* dy, int B, int H, int W, int cout, const void* w_bwd,
                                           int cin, void* dx, const void* relu_mask, float* slab, int dtype,
                                           void* stream) {

@@ -167,8 +167,15 @@ def conv3x3_bwd_data(dy, w_bwd, relu_mask=None, dbias=None, accumulate=True, def
     Cin = w_bwd.shape[0]
     dx = torch.empty(B, H, W, Cin, dtype=dy.dtype, device=dy.device)
     if relu_bits is not None:
-        if relu_mask is not None or defer is not None:
-            raise ValueError("relu_bits takes neither relu_mask nor defer")
+        if relu_mask is not None:
+            raise ValueError("relu_bits replaces relu_mask")
+        if dbias is not None and defer is not None:
+            tiles = conv_stats_tiles(B * H * W)
+            slab = torch.empty(tiles, 2 * Cin, dtype=torch.float32, device=dy.device)
+            call("ocrk_conv3x3_bwd_data_bits_slab", ptr(dy), B, H, W, Cout, ptr(w_bwd), Cin, ptr(dx), ptr(relu_bits),
+                 ptr(slab), dtype_code(dy.dtype), _stream(dy))
+            defer.append((lambda: slab_sum(slab, tiles, Cin, 2 * Cin, dbias, accumulate), (slab,)))
+            return dx
         nb, ws = 0, None
         if dbias is not None:
             nb = _lib.lib().ocrk_conv3x3_bwd_data_workspace_size(B, H, W, Cin)

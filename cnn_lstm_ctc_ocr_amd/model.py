@@ -158,10 +158,21 @@ class _ConvBlock(torch.autograd.Function):
         dp = dp.contiguous()
         if dp.dtype != dt:
             dp = K.cast(dp, dt)
-        # bias-gradient reductions (conv bias in front of the BN, and the odd conv's
-        # bias from the data-gradient GEMM's tile column sums) go to the side stream
-        # with the weight gradients, off the main stream's dependent chain
-        late = [] if _side_enabled("CONV_SIDE") else None
+        # bias-gradient reductions (conv bias in front of the BN with the BN's dgamma, and
+        # the odd conv's bias from the data-gradient GEMM's tile column sums) go to the side
+        # stream with the weight gradients, off the main stream's dependent chain: queued for
+        # the next conv side fork (option CONV_BIAS_SIDE, no fork of their own), or on the
+        # "reduce" lane (DEFER_BIAS=1)
+        bias_side = bool(options.get("CONV_BIAS_SIDE") and options.get("CONV_SIDE_MERGE")
+                         and options.get("CONV_SIDE") and options.get("SIDE_STREAM"))
+        late = [] if (bias_side or _side_enabled("CONV_SIDE")) else None
+
+        def flush_late():
+            if bias_side:
+                store.conv_late.extend(late)
+                late.clear()
+            else:
+                _issue(store, late)
         dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                 POOLS[even], dp_time_major=(k == 4),
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
@@ -171,7 +182,7 @@ class _ConvBlock(torch.autograd.Function):
                                 pooled=pooled if ctx.bn_sync is None and options.get("POOLED_BN") else None)
         B, H, W, C = dz.shape
         if k > 1:
-            _issue(store, late)
+            flush_late()
             with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):   # overlaps the data gradient below
                 _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
@@ -180,7 +191,7 @@ class _ConvBlock(torch.autograd.Function):
             # the step's tail: conv2's weight gradient (y1, dz) on the side stream beside one
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
             # contracted as it is produced, never stored: its only consumer is conv1's dW)
-            _issue(store, late)
+            flush_late()
             with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):
                 _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
@@ -190,12 +201,12 @@ class _ConvBlock(torch.autograd.Function):
             store.join()                                   # side-stream weight gradients are in
             return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
-        if k > 1 and ctx.relu_bits is not None and late is None:
-            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, dbias=G[po + "/bias"], relu_bits=ctx.relu_bits)
+        if k > 1 and ctx.relu_bits is not None:
+            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, dbias=G[po + "/bias"], relu_bits=ctx.relu_bits, defer=late)
         else:
             dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
                                         defer=late)
-        _issue(store, late)
+        flush_late()
         dx = None
         if k == 1:
             # the step's tail: conv1's weight gradient joins the side stream (behind

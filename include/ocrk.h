@@ -229,6 +229,9 @@ int ocrk_conv3x3_bwd_data_bits_supported(int B, int H, int W, int cout, int cin,
 int ocrk_conv3x3_bwd_data_bits(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
                                void* dx, const void* relu_bits, float* dbias, int accumulate, void* ws,
                                size_t ws_bytes, int dtype, void* stream);
+/* The same with the bias-gradient partials left to the caller (as ocrk_conv3x3_bwd_data_slab). */
+int ocrk_conv3x3_bwd_data_bits_slab(const void* dy, int B, int H, int W, int cout, const void* w_bwd, int cin,
+                                    void* dx, const void* relu_bits, float* slab, int dtype, void* stream);
 /* The same with the bias-gradient reduction left to the caller (e.g. on a side
  * stream, off the data-gradient critical path): slab [ocrk_conv_stats_tiles(B*H*W)]
  * [2*cin] f32 gets the per-tile column (sum, M2) of the masked dx; then
