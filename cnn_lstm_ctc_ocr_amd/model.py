@@ -219,9 +219,12 @@ class _ConvBlock(torch.autograd.Function):
             _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             store.join()                                   # side-stream weight gradients are in
         else:
-            if options.get("CONV_SIDE_MERGE") and options.get("CONV_SIDE") and options.get("SIDE_STREAM"):
+            if (k > options.get("CONV_SIDE_MERGE_FROM") and options.get("CONV_SIDE_MERGE") and options.get("CONV_SIDE")
+                    and options.get("SIDE_STREAM")):
                 # the odd conv's weight gradient joins the next side-stream fork (the lower
-                # block's even-conv weight gradient): one fork per block instead of two
+                # block's even-conv weight gradient): one fork per block instead of two. Not
+                # conv3's (k = 2, CONV_SIDE_MERGE_FROM): deferred to conv2's fork it queued
+                # in front of conv2's weight gradient at the step's tail
                 store.conv_late.append((lambda x=x, d=dy_odd, dw=G[po + "/kernel"], ex=ctx.exact:
                                         _conv_wgrad(ex, x, d, dw), (x, dy_odd)))
             else:

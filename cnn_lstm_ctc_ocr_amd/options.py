@@ -25,6 +25,7 @@ _HOST_DEFAULTS = {
     "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
     "PREFETCH_IMAGES": 0,     # 1: the weight-image refresh on its own stream beside conv1 (measured slower)
     "CONV_BIAS_SIDE": 0,      # 1: conv / BN bias-gradient reductions ride the next conv side fork (measured slower)
+    "CONV_SIDE_MERGE_FROM": 2,  # blocks k > this merge their odd weight gradient into the next fork
     "CONV_SIDE_MERGE": 1,     # 0: a side-stream fork for each conv weight gradient (two per block)
     "RELU_BITS": 1,           # 0: conv3/5/7's ReLU masks for conv4/6/8's backward-data as their bf16 outputs
     "POOLED_BN": 1,           # 0: the BN backward's dgamma / dbeta pass walks z instead of the pooled output
