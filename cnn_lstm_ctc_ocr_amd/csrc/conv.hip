@@ -328,6 +328,9 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
                     void* ws, size_t ws_bytes, hipStream_t s);
 bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout);
 bool conv_rows_fwd_bits_covers(int B, int H, int W, int cin, int cout);
+bool conv12_fwd_covers(int B, int H, int W);
+int conv12_fwd(const void* img, int x_is_u8, int B, int H, int W, const float* w1, const float* b1,
+               const void* w_nk2, const float* b2, void* y1, void* bits, void* z, float* stats, hipStream_t s);
 int conv_rows_fwd_bits(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,
                        void* y, void* bits, hipStream_t s);
 bool conv_rows_dgrad_bits_covers(int B, int H, int W, int cin, int cout);
@@ -338,6 +341,27 @@ bool nt_staged_enabled();
 int64_t conv_rows_dgrad_c1_parts(int B);
 int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
                        const void* relu_bits, const void* x, int x_is_u8, float* part, hipStream_t s);
+}
+
+// conv1 -> conv2 forward as one row walk (bf16 training): conv1's output rows are produced
+// into conv2's ring from the image (conv1 on the MFMA, hi + lo split operands) instead of
+// being written and re-read. x [B,IH,IW] u8 (x_is_u8: the fused preprocess) or bf16; w1 f32
+// [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32]; outputs y1 [B,IH-2,IW-2,32]
+// bf16 (conv1's ReLU output), relu_bits u8 [B,IH-2,IW-2][4] (its bit mask), z (conv2's
+// pre-BN output, same shape) and stats [B*(IH-2)][2][32] (conv2's per-row BN partials,
+// ocrk_bn_finalize_tiles with tile_rows = IW-2).
+extern "C" int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype) {
+    return dtype == OCRK_BF16 && IH >= 3 && IW >= 3 && ocrk::conv12_fwd_covers(B, IH - 2, IW - 2) ? 1 : 0;
+}
+
+extern "C" int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
+                               const void* w_nk2, const float* b2, void* y1, void* relu_bits, void* z, float* stats,
+                               int dtype, void* stream) {
+    OCRK_REQUIRE(ocrk_conv12_fwd_supported(B, IH, IW, dtype), "ocrk_conv12_fwd: B=%d IH=%d IW=%d dtype=%d not covered",
+                 B, IH, IW, dtype);
+    OCRK_REQUIRE(x && w1 && b1 && w_nk2 && y1 && relu_bits && z && stats, "ocrk_conv12_fwd: null pointer");
+    return ocrk::conv12_fwd(x, x_is_u8, B, IH - 2, IW - 2, w1, b1, w_nk2, b2, y1, relu_bits, z, stats,
+                            ocrk::as_stream(stream));
 }
 
 // conv2's backward-data and conv1's weight gradient as one pass (bf16): the data

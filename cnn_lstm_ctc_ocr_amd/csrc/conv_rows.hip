@@ -853,6 +853,273 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
 // ds_read_b128 = 8 ci of one pixel). Per-row BatchNorm partials are wave-local
 // (a wave owns its channels): DPP row sums over the 16 pixels of a tile, the
 // tiles in order, M2 about the row mean in a second pass.
+// conv1 -> conv2 forward in one row walk (bf16 training, conv2's 32 -> 32 with the BN row
+// statistics): conv2's x ring rows (conv1's output y1 = relu(conv1(image)), 'valid' on the
+// [H+2][W+2] single-channel image) are PRODUCED here from an 8-row f32 ring of preprocessed
+// image rows instead of being loaded -- conv1's separate pass and conv2's re-read of y1
+// (125 MB at C3) are gone. conv1 itself runs on the MFMA: per 16-pixel tile and 16-channel
+// tile, D[ch][px] = b1 + W1^T[ch][tap] . X[tap][px] over K = 9 taps (padded to 32), the
+// operands split hi + lo in bf16 (3 products: ~2^-16 per product against fp32's conv1,
+// whose output is rounded to bf16 anyway). The produced rows also leave as y1 (the
+// weight gradient's operand) and as the ReLU bit mask (the backward-data's mask), owned
+// rows only. y1 row r is produced at the end of step r - 2 (the ring slot of row r - 4),
+// image row r + 3 put at the end of step r - 2 (the ring slot of row r - 5).
+constexpr int C12_XSLOTS = 8;
+constexpr int C12_LDS = RD_LDS + C12_XSLOTS * RD_XROW * 4;
+
+template <int XIN>   // 1: u8 image (the fused preprocess), 2: bf16 preprocessed image
+__global__ void __launch_bounds__(256, 2)
+conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w1, const float* __restrict__ b1,
+                       const bf16* __restrict__ wn, const float* __restrict__ bias, bf16* __restrict__ y1,
+                       unsigned* __restrict__ bits, bf16* __restrict__ y, float* __restrict__ stats, int B, int H,
+                       int W) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float s_red[2][4][RW_CO];           // [sum | M2][wave][channel]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x / RD_BANDS, band = blockIdx.x - b * RD_BANDS;
+    const int rows = (H + RD_BANDS - 1) / RD_BANDS;
+    const int h0 = band * rows, h1 = min(H, h0 + rows);
+    if (h0 >= h1) return;
+
+    for (int i = tid; i < C12_LDS / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+    float* ximg = reinterpret_cast<float*>(smem + RD_LDS);          // [8][RD_XROW] preprocessed image rows
+
+    // conv2's resident A fragments: co tile j, tap t -> w_nk[16 j + i16][t][8 g .. 8 g + 7]
+    bf16x8 wa[9][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            wa[t][j] = *reinterpret_cast<const bf16x8*>(wn + ((size_t)(16 * j + i16) * 9 + t) * RW_CI + 8 * g);
+    float bco[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bco[j][e] = bias ? bias[16 * j + 4 * g + e] : 0.f;
+    // conv1's A fragments (hi, lo): channel tile j, lane row = channel 16 j + i16, k = taps 8 g .. 8 g + 7
+    u32x4 w1h[2], w1l[2];
+    float b1v[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int t0 = 8 * g + 2 * p, t1 = t0 + 1;
+            const float v0 = t0 < 9 ? w1[t0 * RW_CO + 16 * j + i16] : 0.f;
+            const float v1 = t1 < 9 ? w1[t1 * RW_CO + 16 * j + i16] : 0.f;
+            unsigned hh, ll;
+            split2_bf16(v0, v1, hh, ll);
+            w1h[j][p] = hh;
+            w1l[j][p] = ll;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b1v[j][e] = b1[16 * j + 4 * g + e];
+    }
+
+    const int XW = W + 2;
+    unsigned xraw = 0;
+    auto x_fetch = [&](int r) {                      // this thread's pixel of image row r (clamped)
+        const size_t o = ((size_t)b * (H + 2) + min(max(r, 0), H + 1)) * XW + min(tid, XW - 1);
+        if constexpr (XIN == 1) xraw = reinterpret_cast<const uint8_t*>(img)[o];
+        else xraw = reinterpret_cast<const unsigned short*>(img)[o];
+    };
+    auto x_put = [&](int r) {
+        if (tid < XW) ximg[(r & (C12_XSLOTS - 1)) * RD_XROW + tid] = XIN == 1 ? conv1_pre_u8(xraw) : __uint_as_float(xraw << 16);
+    };
+    auto zero_row = [&](int row) {                   // a y1 row outside the image ('same' padding of conv2)
+        char* slot = smem + (row & 3) * RW_XSLOT;
+        for (int i = tid; i < RW_XSLOT / 16; i += 256) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+    };
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    // y1 row r (0 <= r < H) into conv2's ring slot r & 3 (pixels past W stay zero), and to
+    // y1 / bits when the band owns row r. Image rows r .. r + 2 are in the image ring.
+    auto make_y1 = [&](int r) {
+        char* slot = smem + (r & 3) * RW_XSLOT;
+        const bool own = r >= h0 && r < h1;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int px = 64 * wave + 16 * n + i16;
+            // B: X[tap][px] for taps 8 g .. 8 g + 7 (taps >= 9: zero)
+            float xv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int t = 8 * g + e;
+                const int kh = t / 3, kw = t - 3 * (t / 3);
+                xv[e] = t < 9 ? ximg[((r + kh) & (C12_XSLOTS - 1)) * RD_XROW + px + kw] : 0.f;
+            }
+            u32x4 bh, bl;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                unsigned hh, ll;
+                split2_bf16(xv[2 * p], xv[2 * p + 1], hh, ll);
+                bh[p] = hh;
+                bl[p] = ll;
+            }
+            unsigned mword = 0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                floatx4 d = floatx4{b1v[j][0], b1v[j][1], b1v[j][2], b1v[j][3]};
+                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1h[j]),
+                                                            __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1l[j]),
+                                                            __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+                if constexpr (XIN == 1)                  // a bf16 image is exact in hi
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1h[j]),
+                                                                __builtin_bit_cast(bf16x8, bl), d, 0, 0, 0);
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = fmaxf(d[e], 0.f);
+                    mword |= (v[e] > 0.f ? 1u : 0u) << (16 * j + 4 * g + e);
+                }
+                u32x2 o;
+                o[0] = pack_bf16x2(v[0], v[1]);
+                o[1] = pack_bf16x2(v[2], v[3]);
+                if (px < W) {
+                    *reinterpret_cast<u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o;
+                    if (own) *reinterpret_cast<u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o;
+                }
+            }
+            mword |= __shfl_xor(mword, 16, 64);
+            mword |= __shfl_xor(mword, 32, 64);
+            if (own && g == 0 && px < W) bits[((size_t)b * H + r) * W + px] = mword;
+        }
+    };
+
+    __syncthreads();
+    // prologue: image rows h0-1 .. h0+4 into the image ring, then y1 rows h0-1 .. h0+1 into the ring
+    for (int r = h0 - 1; r <= h0 + 4; ++r) {
+        if (r >= 0 && r < H + 2) {
+            x_fetch(r);
+            x_put(r);
+        }
+    }
+    __syncthreads();
+    for (int r = h0 - 1; r <= h0 + 1; ++r) {
+        if (r < 0 || r >= H) zero_row(r);
+        else make_y1(r);
+    }
+    const float inv_w = 1.f / (float)W;
+    float inrow[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) inrow[n] = 64 * wave + 16 * n + i16 < W ? 1.f : 0.f;
+
+    for (int h = h0; h < h1; ++h) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        x_fetch(h + 5);                              // image row h + 5, put at the end of this step
+        floatx4 acc[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[n][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const char* slot = smem + ((h + kh - 1) & 3) * RW_XSLOT;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const int r = 64 * wave + 16 * n + i16 + kw;
+                    const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rw_off(r, g));
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][j], bf, acc[n][j], 0, 0, 0);
+                }
+            }
+        }
+        float sum[2][4] = {};
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[n][j][e] + bco[j][e];
+                    acc[n][j][e] = v;
+                    sum[j][e] = __builtin_fmaf(v, inrow[n], sum[j][e]);
+                }
+        bf16* orow = y + ((size_t)b * H + h) * W * RW_CO;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int px = 64 * wave + 16 * n + i16;
+            if (px >= W) continue;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                u32x2 o;
+                o[0] = pack_bf16x2(acc[n][j][0], acc[n][j][1]);
+                o[1] = pack_bf16x2(acc[n][j][2], acc[n][j][3]);
+                *reinterpret_cast<u32x2*>(orow + (size_t)px * RW_CO + 16 * j + 4 * g) = o;
+            }
+        }
+        // the row's (sum, M2) as conv3x3_fwd_rows_kernel
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = sum[j][e];
+                v += dpp_row<0x128>(v);
+                v += dpp_row<0x124>(v);
+                v += dpp_row<0x122>(v);
+                v += dpp_row<0x121>(v);
+                sum[j][e] = v;
+            }
+        if (i16 == 0)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s_red[0][wave][16 * j + 4 * g + e] = sum[j][e];
+        rw_barrier();
+        float mean[2][4], q2[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 16 * j + 4 * g + e;
+                mean[j][e] = (((s_red[0][0][c] + s_red[0][1][c]) + s_red[0][2][c]) + s_red[0][3][c]) * inv_w;
+                q2[j][e] = 0.f;
+            }
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float d = (acc[n][j][e] - mean[j][e]) * inrow[n];
+                    q2[j][e] = __builtin_fmaf(d, d, q2[j][e]);
+                }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = q2[j][e];
+                v += dpp_row<0x128>(v);
+                v += dpp_row<0x124>(v);
+                v += dpp_row<0x122>(v);
+                v += dpp_row<0x121>(v);
+                q2[j][e] = v;
+            }
+        if (i16 == 0)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s_red[1][wave][16 * j + 4 * g + e] = q2[j][e];
+        rw_barrier();
+        if (tid < 2 * RW_CO) {
+            const int k = tid / RW_CO, c = tid - k * RW_CO;
+            stats[((size_t)b * H + h) * 2 * RW_CO + tid] =
+                ((s_red[k][0][c] + s_red[k][1][c]) + s_red[k][2][c]) + s_red[k][3][c];
+        }
+        // y1 row h+2 into the slot of row h-2 (zeros past the image); image row h+5 into the
+        // image slot of row h-3 (rows h+2 .. h+4, read by make_y1, are in other slots)
+        if (h + 2 < H) make_y1(h + 2);
+        else if (h + 2 == H) zero_row(h + 2);
+        if (h + 5 < H + 2) x_put(h + 5);
+    }
+}
+
 template <int CI, int CO, int KPX, int CS = 1>
 struct RfCfg {
     // CS workgroups split the output channels of a row band (CO / CS per workgroup)
@@ -1336,6 +1603,28 @@ int conv_rows_dgrad_bits(const void* dy, int B, int H, int W, int cout, const vo
                          const void* bits, float* stats, hipStream_t s) {
     if (!conv_rows_dgrad_bits_covers(B, H, W, cin, cout)) return -1;
     return launch_dgrad_co<64, 64, 128, 1, true>(dy, B, H, W, w_bwd, dx, bits, stats, s);
+}
+
+bool conv12_fwd_covers(int B, int H, int W) {
+    return rows_enabled() && B >= 1 && H >= 1 && W >= 1 && W <= RW_MAXW;
+}
+
+// conv1 -> conv2 forward (conv12_fwd_rows_kernel): y1 [B,H,W,32] bf16, bits [B,H,W] u32, z [B,H,W,32]
+// bf16, stats [B*H][2][32] (conv2's per-row BN partials, tile_rows = W)
+int conv12_fwd(const void* img, int x_is_u8, int B, int H, int W, const float* w1, const float* b1,
+               const void* w_nk2, const float* b2, void* y1, void* bits, void* z, float* stats, hipStream_t s) {
+    if (!conv12_fwd_covers(B, H, W)) return -1;
+    static DeviceOnce cfg_u8, cfg_bf;
+    if (x_is_u8) {
+        set_dyn_lds(cfg_u8, reinterpret_cast<const void*>(&conv12_fwd_rows_kernel<1>), C12_LDS);
+        conv12_fwd_rows_kernel<1><<<B * RD_BANDS, 256, C12_LDS, s>>>(img, w1, b1, (const bf16*)w_nk2, b2, (bf16*)y1,
+                                                                     (unsigned*)bits, (bf16*)z, stats, B, H, W);
+    } else {
+        set_dyn_lds(cfg_bf, reinterpret_cast<const void*>(&conv12_fwd_rows_kernel<2>), C12_LDS);
+        conv12_fwd_rows_kernel<2><<<B * RD_BANDS, 256, C12_LDS, s>>>(img, w1, b1, (const bf16*)w_nk2, b2, (bf16*)y1,
+                                                                     (unsigned*)bits, (bf16*)z, stats, B, H, W);
+    }
+    return launch_status("conv12_fwd_rows");
 }
 
 bool conv_rows_dgrad_c1_covers(int B, int H, int W, int cin, int cout) {

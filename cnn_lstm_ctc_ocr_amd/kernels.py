@@ -80,6 +80,30 @@ def conv1_fwd(x, w, b, dtype, relu_bits=False):
     return y
 
 
+def conv12_fwd_ok(x, dtype):
+    """The fused conv1 -> conv2 forward covers this image batch [B, IH, IW] (bf16)."""
+    B, IH, IW = x.shape[:3]
+    return (x.dtype in (torch.uint8, torch.bfloat16) and (x.dtype == torch.uint8 or x.dtype == dtype)
+            and bool(_lib.lib().ocrk_conv12_fwd_supported(B, IH, IW, dtype_code(dtype))))
+
+
+def conv12_fwd(x, w1, b1, w_nk2, b2):
+    """conv1 (fused preprocess, ReLU) -> conv2 (no activation) with conv2's per-row BN
+    partials (ocrk_conv12_fwd). Returns y1 [B,IH-2,IW-2,32] bf16, its ReLU bit mask
+    u8 [.., 4], z [B,IH-2,IW-2,32] bf16, stats [B*(IH-2), 2, 32]."""
+    _chk(x, w1, b1, w_nk2, b2)
+    B, IH, IW = x.shape[:3]
+    H, W = IH - 2, IW - 2
+    dev = x.device
+    y1 = torch.empty(B, H, W, 32, dtype=torch.bfloat16, device=dev)
+    bits = torch.empty(B, H, W, 4, dtype=torch.uint8, device=dev)
+    z = torch.empty(B, H, W, 32, dtype=torch.bfloat16, device=dev)
+    stats = torch.empty(B * H, 2, 32, dtype=torch.float32, device=dev)
+    call("ocrk_conv12_fwd", ptr(x), int(x.dtype == torch.uint8), B, IH, IW, ptr(w1), ptr(b1), ptr(w_nk2), ptr(b2),
+         ptr(y1), ptr(bits), ptr(z), ptr(stats), BF16, _stream(x))
+    return y1, bits, z, stats
+
+
 def conv1_bwd_weight(x, dz, dw, db, accumulate=True):
     _chk(x, dz, dw, db)
     B, H, W = x.shape[0], x.shape[1], x.shape[2]

@@ -92,7 +92,17 @@ class _ConvBlock(torch.autograd.Function):
         pe = f"convnet/{even}"
         ctx.bn_sync = None
         ctx.relu_bits = None
-        if k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
+        zs = None
+        if (k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED")
+                and options.get("CONV12_FUSED") and K.conv12_fwd_ok(x, dt)):
+            # conv1 -> conv2 in one row walk: conv1's rows produced into conv2's ring (never
+            # re-read from HBM), y1 and its ReLU bit mask written for the backward
+            w_nk2, _ = store.conv_images(even, dt)
+            y_odd, bits, z12, st12 = K.conv12_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], w_nk2,
+                                                  P[pe + "/bias"])
+            ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(y_odd, x) else None
+            zs = (z12, st12)
+        elif k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
             # the ReLU's bit mask for the fused conv2 backward-data + conv1 weight gradient
             # (it reads 4 B per pixel instead of y1's 64)
             y_odd, bits = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt, relu_bits=True)
@@ -113,7 +123,10 @@ class _ConvBlock(torch.autograd.Function):
         w_nk, _ = store.conv_images(even, dt)
         C = w_nk.shape[0]
         if training:
-            if K.conv3x3_fwd_rowstats_ok(y_odd, C):
+            if zs is not None:                             # conv2 already ran inside conv12_fwd
+                z, stats = zs
+                trows = W
+            elif K.conv3x3_fwd_rowstats_ok(y_odd, C):
                 # conv2 on the row-walking kernel: BN partials per output row
                 z, stats = K.conv3x3_fwd_rowstats(y_odd, w_nk, P[pe + "/bias"])
                 trows = W

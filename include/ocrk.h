@@ -171,6 +171,17 @@ int ocrk_conv1_fwd(const void* x, int x_is_u8, int B, int H, int W, const float*
  * backward (ocrk_conv2_bwd_data_conv1_wgrad), 1/16 of y's bf16 bytes. */
 int ocrk_conv1_fwd_relu_bits(const void* x, int x_is_u8, int B, int H, int W, const float* w, const float* bias,
                              int cout, void* y, void* relu_bits, int dtype, void* stream);
+/* conv1 -> conv2 forward as one row walk (bf16 training; conv_layer 1 and 2, model.py:84-109,
+ * 134-137): conv1's output rows are produced into conv2's LDS ring from the image (conv1 on
+ * the MFMA with hi + lo bf16 operands) instead of being written and re-read by conv2. Replaces
+ * ocrk_conv1_fwd_relu_bits + ocrk_conv3x3_fwd_rowstats of the first block. x [B,IH,IW] u8
+ * (x_is_u8) or bf16; w1 f32 [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32];
+ * y1, z bf16 [B,IH-2,IW-2,32]; relu_bits u8 [B,IH-2,IW-2][4]; stats [B*(IH-2)][2][32]
+ * (tile_rows = IW-2). */
+int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype);
+int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
+                    const void* w_nk2, const float* b2, void* y1, void* relu_bits, void* z, float* stats, int dtype,
+                    void* stream);
 /* conv1 weight/bias gradient from dz = dL/d(pre-ReLU conv1), f32 outputs. */
 size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
 int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,

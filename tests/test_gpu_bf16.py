@@ -114,6 +114,45 @@ def test_conv1_fwd_relu_bits(cuda, x_u8):
     np.testing.assert_array_equal(bits.cpu().numpy(), _relu_bits(y.float().cpu().numpy()))
 
 
+@pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70)])
+@pytest.mark.parametrize("x_u8", [True, False])
+def test_conv12_fused_forward(cuda, B, IH, IW, x_u8):
+    """conv1 -> conv2 in one row walk (ocrk_conv12_fwd, the bench's first block): y1 (conv1
+    on the MFMA, hi + lo operands) against the float64 conv1 and the fp32 VALU conv1 kernel
+    (bf16 rounding level); its bit mask = y1 > 0; z and the per-row BN partials bit-identical
+    to the conv2 row kernel run on the same y1 (the same MFMA sequence)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(IH * 100 + IW + 7 * x_u8)
+    img = rng.integers(0, 256, (B, IH, IW)).astype(np.uint8)
+    w1 = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
+    b1 = (rng.standard_normal(32) * 0.3).astype(np.float32)
+    w2 = _bf(rng.standard_normal((3, 3, 32, 32)) / np.sqrt(288))
+    b2 = rng.standard_normal(32).astype(np.float32)
+    if x_u8:
+        xd = torch.from_numpy(img).to(cuda)
+        x64 = G.preprocess(img).astype(np.float64)
+    else:
+        xf = _bf(rng.standard_normal((B, IH, IW)))
+        xd = torch.from_numpy(xf).to(cuda).bfloat16()
+        x64 = xf.astype(np.float64)
+    w1d, b1d = torch.from_numpy(w1).to(cuda), torch.from_numpy(b1).to(cuda)
+    w_nk = Kn.permute3(torch.from_numpy(w2).to(cuda), 9 * 32, 32, 1, torch.bfloat16).view(32, 9 * 32)
+    b2d = torch.from_numpy(b2).to(cuda)
+    assert Kn.conv12_fwd_ok(xd, torch.bfloat16)
+    y1, bits, z, stats = Kn.conv12_fwd(xd, w1d, b1d, w_nk, b2d)
+    y1_ref = G.relu(G.conv2d(x64[..., None], w1.astype(np.float64), b1.astype(np.float64), "valid"))
+    y1f = y1.float().cpu().numpy()
+    assert _rel(y1f, y1_ref) < BF16_OUT
+    y1_valu = Kn.conv1_fwd(xd, w1d, b1d, torch.bfloat16).float().cpu().numpy()
+    differ = np.abs(y1f - y1_valu) > 2 ** -7 * np.abs(y1_valu) + 1e-6
+    assert differ.mean() < 1e-3, differ.mean()              # at most a last-bit rounding apart
+    np.testing.assert_array_equal(bits.cpu().numpy(), _relu_bits(y1f))
+    z2, st2 = Kn.conv3x3_fwd_rowstats(y1, w_nk, b2d)
+    torch.cuda.synchronize()
+    assert torch.equal(z, z2)
+    assert torch.equal(stats, st2)
+
+
 @pytest.mark.parametrize("B,H,W,cin,cout,cnext", [(4, 15, 127, 32, 64, 64), (4, 7, 126, 64, 128, 128),
                                                   (8, 3, 125, 128, 256, 256), (3, 5, 37, 64, 64, 64)])
 def test_relu_bit_masks_conv_pair(cuda, B, H, W, cin, cout, cnext):
