@@ -24,7 +24,7 @@ _HOST_DEFAULTS = {
     "DEFER_DWX": 0,           # 1: an upper layer's dW_x behind the lower BPTT (measured no gain)
     "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
     "PREFETCH_IMAGES": 0,     # 1: the weight-image refresh on its own stream beside conv1 (measured slower)
-    "CONV12_FUSED": 0,        # 1: conv1 -> conv2 forward as one row walk (conv1 rows never re-read)
+    "CONV12_FUSED": 1,        # 0: conv1 and conv2 forward as two passes (y1 written, then re-read)
     "CONV_BIAS_SIDE": 0,      # 1: conv / BN bias-gradient reductions ride the next conv side fork (measured slower)
     "CONV_SIDE_MERGE_FROM": 2,  # blocks k > this merge their odd weight gradient into the next fork
     "CONV_SIDE_MERGE": 1,     # 0: a side-stream fork for each conv weight gradient (two per block)
