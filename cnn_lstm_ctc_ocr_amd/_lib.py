@@ -60,6 +60,8 @@ SIGNATURES = {
                                         _p],
     "ocrk_conv12_fwd_supported": [_i32, _i32, _i32, _i32],
     "ocrk_conv12_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p],
+    "ocrk_conv2_bwd_weight_c1x_supported": [_i32, _i32, _i32, _i32],
+    "ocrk_conv2_bwd_weight_c1x": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv1_fwd_relu_bits": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i32, _p],
     "ocrk_conv_stats_tiles": [_i64],
     "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],

@@ -331,6 +331,8 @@ bool conv_rows_fwd_bits_covers(int B, int H, int W, int cin, int cout);
 bool conv12_fwd_covers(int B, int H, int W);
 int conv12_fwd(const void* img, int x_is_u8, int B, int H, int W, const float* w1, const float* b1,
                const void* w_nk2, const float* b2, void* y1, void* bits, void* z, float* stats, hipStream_t s);
+int conv_rows_wgrad_c1x(const void* img, int x_is_u8, const float* w1, const float* b1, const void* dy, int B, int H,
+                        int W, float* dw, int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
 int conv_rows_fwd_bits(const void* x, int B, int H, int W, int cin, const void* w_nk, const float* bias, int cout,
                        void* y, void* bits, hipStream_t s);
 bool conv_rows_dgrad_bits_covers(int B, int H, int W, int cin, int cout);
@@ -349,7 +351,8 @@ int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, c
 // [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32]; outputs y1 [B,IH-2,IW-2,32]
 // bf16 (conv1's ReLU output), relu_bits u8 [B,IH-2,IW-2][4] (its bit mask), z (conv2's
 // pre-BN output, same shape) and stats [B*(IH-2)][2][32] (conv2's per-row BN partials,
-// ocrk_bn_finalize_tiles with tile_rows = IW-2).
+// ocrk_bn_finalize_tiles with tile_rows = IW-2). y1 may be NULL: not written (the backward
+// then recomputes it, ocrk_conv2_bwd_weight_c1x).
 extern "C" int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype) {
     return dtype == OCRK_BF16 && IH >= 3 && IW >= 3 && ocrk::conv12_fwd_covers(B, IH - 2, IW - 2) ? 1 : 0;
 }
@@ -359,9 +362,29 @@ extern "C" int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW
                                int dtype, void* stream) {
     OCRK_REQUIRE(ocrk_conv12_fwd_supported(B, IH, IW, dtype), "ocrk_conv12_fwd: B=%d IH=%d IW=%d dtype=%d not covered",
                  B, IH, IW, dtype);
-    OCRK_REQUIRE(x && w1 && b1 && w_nk2 && y1 && relu_bits && z && stats, "ocrk_conv12_fwd: null pointer");
+    OCRK_REQUIRE(x && w1 && b1 && w_nk2 && relu_bits && z && stats, "ocrk_conv12_fwd: null pointer");
     return ocrk::conv12_fwd(x, x_is_u8, B, IH - 2, IW - 2, w1, b1, w_nk2, b2, y1, relu_bits, z, stats,
                             ocrk::as_stream(stream));
+}
+
+// conv2's weight gradient with its input y1 = relu(conv1(x)) recomputed per row from the
+// image instead of read (bf16): dw [3][3][32][32] f32 (+)= sum y1 (x) dz over the batch,
+// y1 bit-identical to ocrk_conv12_fwd's. x, w1, b1 as ocrk_conv12_fwd; dz [B,IH-2,IW-2,32]
+// bf16; ws per ocrk_conv3x3_wgrad_workspace_size(B, IH-2, IW-2, 32, 32).
+extern "C" int ocrk_conv2_bwd_weight_c1x_supported(int B, int IH, int IW, int dtype) {
+    return ocrk_conv12_fwd_supported(B, IH, IW, dtype);
+}
+
+extern "C" int ocrk_conv2_bwd_weight_c1x(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1,
+                                         const float* b1, const void* dz, float* dw, int accumulate, void* ws,
+                                         size_t ws_bytes, int dtype, void* stream) {
+    OCRK_REQUIRE(ocrk_conv2_bwd_weight_c1x_supported(B, IH, IW, dtype),
+                 "ocrk_conv2_bwd_weight_c1x: B=%d IH=%d IW=%d dtype=%d not covered", B, IH, IW, dtype);
+    OCRK_REQUIRE(x && w1 && b1 && dz && dw && ws, "ocrk_conv2_bwd_weight_c1x: null pointer");
+    int st = ocrk::conv_rows_wgrad_c1x(x, x_is_u8, w1, b1, dz, B, IH - 2, IW - 2, dw, accumulate, ws, ws_bytes,
+                                       ocrk::as_stream(stream));
+    OCRK_REQUIRE(st >= 0, "ocrk_conv2_bwd_weight_c1x: workspace too small or path disabled");
+    return st;
 }
 
 // conv2's backward-data and conv1's weight gradient as one pass (bf16): the data

@@ -64,9 +64,109 @@ __device__ __forceinline__ void rw_barrier() {
     asm volatile("" ::: "memory");
 }
 
+constexpr int RD_XROW = 260;                       // floats per image ring row (pixels 0 .. 257, zero past W + 1)
+constexpr int C12_XSLOTS = 8;                      // image ring rows of the conv1 producers
+
+// validate.py:61-62 (the preprocess conv.hip's conv1 kernels apply, same rounding)
+__device__ __forceinline__ float conv1_pre_u8(unsigned v) {
+#pragma clang fp contract(off)
+    return (float)v * (1.0f / 255.0f) - 0.5f;
+}
+
+// conv1's weights as MFMA A fragments (hi, lo) and its bias in the D layout: channel
+// tile j, lane row = channel 16 j + i16, k = taps 8 g .. 8 g + 7 (taps >= 9: zero)
+struct C1Frags {
+    u32x4 wh[2], wl[2];
+    const float* b1;              // read at use (4 floats per tile: fewer live registers)
+};
+__device__ __forceinline__ void c1_frags(C1Frags& f, const float* __restrict__ w1, const float* __restrict__ b1,
+                                         int i16, int g) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int t0 = 8 * g + 2 * p, t1 = t0 + 1;
+            const float v0 = t0 < 9 ? w1[t0 * RW_CO + 16 * j + i16] : 0.f;
+            const float v1 = t1 < 9 ? w1[t1 * RW_CO + 16 * j + i16] : 0.f;
+            unsigned hh, ll;
+            split2_bf16(v0, v1, hh, ll);
+            f.wh[j][p] = hh;
+            f.wl[j][p] = ll;
+        }
+    }
+    f.b1 = b1;
+}
+
+// conv1's output row r (relu(b1 + 3x3 'valid' conv of image rows r .. r + 2, held
+// preprocessed in the 8-row f32 image ring `ximg`)) into a conv row ring slot ([pixel + 1]
+// [32 channels], rw_off layout; pixels past W untouched) on the MFMA: per 16-pixel tile
+// and 16-channel tile D[ch][px] = b1 + W1^T[ch][tap] . X[tap][px], K = 9 taps padded to 32,
+// hi + lo bf16 operands (3 products; XIN 2 = a bf16 image, exact in hi: 2). Wave w covers
+// pixels 64 w .. 64 w + 63. y1row / bitsrow (or NULL): the row's bf16 values and its
+// ReLU bit mask (u32 per pixel) to global memory. The same bits wherever it runs.
+template <int XIN>
+__device__ __forceinline__ void c1_make_row(char* slot, const float* ximg, int r, int W, int wave, int i16, int g,
+                                            const C1Frags& f, bf16* y1row, unsigned* bitsrow) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int px = 64 * wave + 16 * n + i16;
+        float xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int t = 8 * g + e;
+            const int kh = t / 3, kw = t - 3 * (t / 3);
+            xv[e] = t < 9 ? ximg[((r + kh) & (C12_XSLOTS - 1)) * RD_XROW + px + kw] : 0.f;
+        }
+        u32x4 bh, bl;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            unsigned hh, ll;
+            split2_bf16(xv[2 * p], xv[2 * p + 1], hh, ll);
+            bh[p] = hh;
+            bl[p] = ll;
+        }
+        unsigned mword = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            floatx4 d = *reinterpret_cast<const floatx4*>(f.b1 + 16 * j + 4 * g);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
+                                                        __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wl[j]),
+                                                        __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+            if constexpr (XIN == 1)
+                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
+                                                            __builtin_bit_cast(bf16x8, bl), d, 0, 0, 0);
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = fmaxf(d[e], 0.f);
+                mword |= (v[e] > 0.f ? 1u : 0u) << (16 * j + 4 * g + e);
+            }
+            u32x2 o;
+            o[0] = pack_bf16x2(v[0], v[1]);
+            o[1] = pack_bf16x2(v[2], v[3]);
+            if (px < W) {
+                *reinterpret_cast<u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o;
+                if (y1row) *reinterpret_cast<u32x2*>(y1row + (size_t)px * RW_CI + 16 * j + 4 * g) = o;
+            }
+        }
+        if (bitsrow) {
+            mword |= __shfl_xor(mword, 16, 64);
+            mword |= __shfl_xor(mword, 32, 64);
+            if (g == 0 && px < W) bitsrow[px] = mword;
+        }
+    }
+}
+
+// C1X (1: u8, 2: bf16 image): conv2's x = y1 is not read but recomputed per row from the
+// image (c1_make_row: the same bits conv12_fwd_rows_kernel produced), so the fused forward
+// need not write y1 at all -- 125 MB written and 125 MB read less per step at C3
+template <int C1X = 0>
 __global__ void __launch_bounds__(256, 1)
 conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part,
-                          int B, int H, int W) {
+                          int B, int H, int W, const void* __restrict__ img = nullptr,
+                          const float* __restrict__ w1 = nullptr, const float* __restrict__ b1 = nullptr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -76,6 +176,21 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
 
     // zero both rings once: the pad pixels (x rows 0 and W+1.., dy rows W..255) stay zero
     for (int i = tid; i < RW_RING / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+    float* ximg = reinterpret_cast<float*>(smem + RW_LDS);           // C1X: [8][RD_XROW] image rows
+    if constexpr (C1X != 0)
+        for (int i = tid; i < C12_XSLOTS * RD_XROW; i += 256) ximg[i] = 0.f;
+    C1Frags f1;
+    if constexpr (C1X != 0) c1_frags(f1, w1, b1, i16, g);
+    const int XW = W + 2;
+    unsigned xraw = 0;
+    auto x_fetch = [&](int bb, int r) {
+        const size_t o = ((size_t)bb * (H + 2) + min(max(r, 0), H + 1)) * XW + min(tid, XW - 1);
+        if constexpr (C1X == 1) xraw = reinterpret_cast<const uint8_t*>(img)[o];
+        else if constexpr (C1X == 2) xraw = reinterpret_cast<const unsigned short*>(img)[o];
+    };
+    auto x_put = [&](int r) {
+        if (tid < XW) ximg[(r & (C12_XSLOTS - 1)) * RD_XROW + tid] = C1X == 1 ? conv1_pre_u8(xraw) : __uint_as_float(xraw << 16);
+    };
 
     floatx4 acc[9][2][2];
 #pragma unroll
@@ -120,17 +235,31 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
         auto xrow = [&](int r) { return xb + (size_t)r * W * RW_CI; };
         auto drow = [&](int r) { return db + (size_t)r * W * RW_CO; };
         __syncthreads();                            // the previous image's last reads are done
-        // prologue: x rows 0, 1 and dy row 0 into the ring; x row 2 / dy row 1 into set 0
-        load_row(xrow(0), sx[1]);
-        load_row(drow(0), sd[1]);
-        store_row(xslot(0), 1, sx[1]);
-        store_row(dslot(0), 0, sd[1]);
-        if (H > 1) {
-            load_row(xrow(1), sx[1]);
-            store_row(xslot(1), 1, sx[1]);
-            load_row(drow(1), sd[0]);
+        if constexpr (C1X != 0) {
+            // prologue: image rows 0 .. 4 into the image ring, then x rows 0, 1 produced
+            for (int r = 0; r <= 4 && r < H + 2; ++r) {
+                x_fetch(b, r);
+                x_put(r);
+            }
+            __syncthreads();
+            c1_make_row<C1X>(smem + xslot(0), ximg, 0, W, wave, i16, g, f1, nullptr, nullptr);
+            if (H > 1) c1_make_row<C1X>(smem + xslot(1), ximg, 1, W, wave, i16, g, f1, nullptr, nullptr);
+            load_row(drow(0), sd[1]);
+            store_row(dslot(0), 0, sd[1]);
+            if (H > 1) load_row(drow(1), sd[0]);
+        } else {
+            // prologue: x rows 0, 1 and dy row 0 into the ring; x row 2 / dy row 1 into set 0
+            load_row(xrow(0), sx[1]);
+            load_row(drow(0), sd[1]);
+            store_row(xslot(0), 1, sx[1]);
+            store_row(dslot(0), 0, sd[1]);
+            if (H > 1) {
+                load_row(xrow(1), sx[1]);
+                store_row(xslot(1), 1, sx[1]);
+                load_row(drow(1), sd[0]);
+            }
+            if (H > 2) load_row(xrow(2), sx[0]);
         }
-        if (H > 2) load_row(xrow(2), sx[0]);
         // step h: rows h-1..h+1 of x and row h of dy are in the ring; set P holds
         // x row h+2 / dy row h+1 (loaded during step h-1); set 1-P receives x row
         // h+3 / dy row h+2 now
@@ -139,7 +268,8 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
             __syncthreads();
             // unconditional (a clamped row past the image): a fixed count of loads in
             // flight lets the stores below wait for the older set only
-            load_row(xrow(min(h + 3, H - 1)), sx[1 - P]);
+            if constexpr (C1X != 0) x_fetch(b, h + 5);
+            else load_row(xrow(min(h + 3, H - 1)), sx[1 - P]);
             load_row(drow(min(h + 2, H - 1)), sd[1 - P]);
             const char* dsl = smem + dslot(h);
 #pragma unroll
@@ -175,7 +305,13 @@ conv3x3_wgrad_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ d
                 }
             }
             // rows h+2 / h+1 into the slots nobody reads this step (x row h-2's, dy row h-1's)
-            if (h + 2 < H) store_row(xslot(h + 2), 1, sx[P]);
+            if constexpr (C1X != 0) {
+                // x row h+2 produced from image rows h+2 .. h+4; image row h+5 into the slot of h-3
+                if (h + 2 < H) c1_make_row<C1X>(smem + xslot(h + 2), ximg, h + 2, W, wave, i16, g, f1, nullptr, nullptr);
+                if (h + 5 < H + 2) x_put(h + 5);
+            } else {
+                if (h + 2 < H) store_row(xslot(h + 2), 1, sx[P]);
+            }
             if (h + 1 < H) store_row(dslot(h + 1), 0, sd[P]);
         };
         for (int h = 0; h < H; h += 2) {
@@ -234,17 +370,10 @@ constexpr int RD_LDS = 4 * RW_XSLOT;               // 64.5 KB
 // 4-row f32 ring (preprocessed once per row), split hi + lo into bf16 (the u8
 // path's x = v/255 - 0.5 is not a bf16 value; |x - hi - lo| <= 2^-17 |x|).
 // 8 MFMAs per row beside the data gradient's 72; one [10][32] partial per workgroup.
-constexpr int RD_XROW = 260;                       // floats per x ring row (pixels 0 .. 257, zero past W + 1)
 constexpr int RD_XRING = 4 * RD_XROW * 4;          // 4.1 KB
 constexpr int RD_TSLOT = 32 * RW_ROWB;             // 2 KB: one wave's 32-pixel block of dy1
 constexpr int RD_LDS_C1 = RD_LDS + RD_XRING + 4 * RD_TSLOT;   // 76.6 KB (2 workgroups per CU)
 constexpr int RD_C1_PART = 10 * RW_CI;             // floats per workgroup partial: [tap 0-8 | bias][ci]
-
-// validate.py:61-62 (the preprocess conv.hip's conv1 kernels apply, same rounding)
-__device__ __forceinline__ float conv1_pre_u8(unsigned v) {
-#pragma clang fp contract(off)
-    return (float)v * (1.0f / 255.0f) - 0.5f;
-}
 
 // BITS: the ReLU mask as conv1's bit mask (u32 per pixel, bit c = channel c: ocrk_conv1_fwd_relu_bits)
 // instead of its bf16 output -- 4 B per pixel read instead of 64
@@ -864,10 +993,9 @@ conv3x3_wgrad_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict_
 // weight gradient's operand) and as the ReLU bit mask (the backward-data's mask), owned
 // rows only. y1 row r is produced at the end of step r - 2 (the ring slot of row r - 4),
 // image row r + 3 put at the end of step r - 2 (the ring slot of row r - 5).
-constexpr int C12_XSLOTS = 8;
 constexpr int C12_LDS = RD_LDS + C12_XSLOTS * RD_XROW * 4;
 
-template <int XIN>   // 1: u8 image (the fused preprocess), 2: bf16 preprocessed image
+template <int XIN, bool WY1>   // XIN 1: u8 image (the fused preprocess), 2: bf16 preprocessed image; WY1: y1 out
 __global__ void __launch_bounds__(256, 2)
 conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w1, const float* __restrict__ b1,
                        const bf16* __restrict__ wn, const float* __restrict__ bias, bf16* __restrict__ y1,
@@ -900,7 +1028,6 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
         for (int e = 0; e < 4; ++e) bco[j][e] = bias ? bias[16 * j + 4 * g + e] : 0.f;
     // conv1's A fragments (hi, lo): channel tile j, lane row = channel 16 j + i16, k = taps 8 g .. 8 g + 7
     u32x4 w1h[2], w1l[2];
-    float b1v[2][4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
 #pragma unroll
@@ -913,8 +1040,6 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
             w1h[j][p] = hh;
             w1l[j][p] = ll;
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) b1v[j][e] = b1[16 * j + 4 * g + e];
     }
 
     const int XW = W + 2;
@@ -933,7 +1058,7 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
     };
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     // y1 row r (0 <= r < H) into conv2's ring slot r & 3 (pixels past W stay zero), and to
-    // y1 / bits when the band owns row r. Image rows r .. r + 2 are in the image ring.
+    // y1 (WY1) / bits when the band owns row r. Image rows r .. r + 2 are in the image ring.
     auto make_y1 = [&](int r) {
         char* slot = smem + (r & 3) * RW_XSLOT;
         const bool own = r >= h0 && r < h1;
@@ -959,7 +1084,7 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
             unsigned mword = 0;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                floatx4 d = floatx4{b1v[j][0], b1v[j][1], b1v[j][2], b1v[j][3]};
+                floatx4 d = *reinterpret_cast<const floatx4*>(b1 + 16 * j + 4 * g);   // at use: fewer live registers
                 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1h[j]),
                                                             __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
                 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1l[j]),
@@ -978,7 +1103,7 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
                 o[1] = pack_bf16x2(v[2], v[3]);
                 if (px < W) {
                     *reinterpret_cast<u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o;
-                    if (own) *reinterpret_cast<u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o;
+                    if (WY1 && own) *reinterpret_cast<u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o;
                 }
             }
             mword |= __shfl_xor(mword, 16, 64);
@@ -1605,24 +1730,56 @@ int conv_rows_dgrad_bits(const void* dy, int B, int H, int W, int cout, const vo
     return launch_dgrad_co<64, 64, 128, 1, true>(dy, B, H, W, w_bwd, dx, bits, stats, s);
 }
 
+// conv2's weight gradient with conv1's output recomputed from the image (no y1 tensor):
+// dw [3][3][32][32] (+)= sum y1 (x) dz, y1 = relu(conv1(img)) produced per row by
+// c1_make_row -- the bits conv12_fwd_rows_kernel made in the forward
+constexpr int RW_LDS_C1X = RW_LDS + C12_XSLOTS * RD_XROW * 4;     // 155.6 KB (one workgroup per CU)
+
+int conv_rows_wgrad_c1x(const void* img, int x_is_u8, const float* w1, const float* b1, const void* dy, int B, int H,
+                        int W, float* dw, int accumulate, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (!rows_enabled() || W < 1 || H < 1 || B < 1 || W > RW_MAXW) return -1;
+    if (ws_bytes < conv_rows_wgrad_ws_bytes(B, RW_CI, RW_CO) || (uintptr_t)ws % 16 != 0) return -1;
+    const int grid = std::min(B, std::max(cu_count(), 1));
+    static DeviceOnce cfg_u8, cfg_bf;
+    if (x_is_u8) {
+        set_dyn_lds(cfg_u8, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel<1>), RW_LDS_C1X);
+        conv3x3_wgrad_rows_kernel<1><<<grid, 256, RW_LDS_C1X, s>>>(nullptr, (const bf16*)dy, (float*)ws, B, H, W, img,
+                                                                   w1, b1);
+    } else {
+        set_dyn_lds(cfg_bf, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel<2>), RW_LDS_C1X);
+        conv3x3_wgrad_rows_kernel<2><<<grid, 256, RW_LDS_C1X, s>>>(nullptr, (const bf16*)dy, (float*)ws, B, H, W, img,
+                                                                   w1, b1);
+    }
+    int st = launch_status("conv3x3_wgrad_rows_c1x");
+    if (st) return st;
+    GemmParams p = {};
+    p.M = 9 * RW_CI; p.N = RW_CO; p.K = B * H * W; p.batch = 1;
+    p.C = dw; p.ldc = RW_CO; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+    p.splits = grid; p.splitk_ws = (float*)ws;
+    return splitk_finish(p, s);
+}
+
 bool conv12_fwd_covers(int B, int H, int W) {
     return rows_enabled() && B >= 1 && H >= 1 && W >= 1 && W <= RW_MAXW;
 }
 
-// conv1 -> conv2 forward (conv12_fwd_rows_kernel): y1 [B,H,W,32] bf16, bits [B,H,W] u32, z [B,H,W,32]
+// conv1 -> conv2 forward (conv12_fwd_rows_kernel): y1 [B,H,W,32] bf16 (or NULL: not written), bits [B,H,W] u32, z [B,H,W,32]
 // bf16, stats [B*H][2][32] (conv2's per-row BN partials, tile_rows = W)
 int conv12_fwd(const void* img, int x_is_u8, int B, int H, int W, const float* w1, const float* b1,
                const void* w_nk2, const float* b2, void* y1, void* bits, void* z, float* stats, hipStream_t s) {
     if (!conv12_fwd_covers(B, H, W)) return -1;
-    static DeviceOnce cfg_u8, cfg_bf;
+    auto go = [&](auto kern, DeviceOnce& cfg) {
+        set_dyn_lds(cfg, reinterpret_cast<const void*>(kern), C12_LDS);
+        kern<<<B * RD_BANDS, 256, C12_LDS, s>>>(img, w1, b1, (const bf16*)w_nk2, b2, (bf16*)y1, (unsigned*)bits,
+                                                (bf16*)z, stats, B, H, W);
+    };
+    static DeviceOnce cfg[4];
     if (x_is_u8) {
-        set_dyn_lds(cfg_u8, reinterpret_cast<const void*>(&conv12_fwd_rows_kernel<1>), C12_LDS);
-        conv12_fwd_rows_kernel<1><<<B * RD_BANDS, 256, C12_LDS, s>>>(img, w1, b1, (const bf16*)w_nk2, b2, (bf16*)y1,
-                                                                     (unsigned*)bits, (bf16*)z, stats, B, H, W);
+        if (y1) go(conv12_fwd_rows_kernel<1, true>, cfg[0]);
+        else go(conv12_fwd_rows_kernel<1, false>, cfg[1]);
     } else {
-        set_dyn_lds(cfg_bf, reinterpret_cast<const void*>(&conv12_fwd_rows_kernel<2>), C12_LDS);
-        conv12_fwd_rows_kernel<2><<<B * RD_BANDS, 256, C12_LDS, s>>>(img, w1, b1, (const bf16*)w_nk2, b2, (bf16*)y1,
-                                                                     (unsigned*)bits, (bf16*)z, stats, B, H, W);
+        if (y1) go(conv12_fwd_rows_kernel<2, true>, cfg[2]);
+        else go(conv12_fwd_rows_kernel<2, false>, cfg[3]);
     }
     return launch_status("conv12_fwd_rows");
 }
@@ -1708,8 +1865,8 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
     const int grid = std::min(B, std::max(cu_count(), 1));
     static DeviceOnce cfg;
-    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel), RW_LDS);
-    conv3x3_wgrad_rows_kernel<<<grid, 256, RW_LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel<0>), RW_LDS);
+    conv3x3_wgrad_rows_kernel<0><<<grid, 256, RW_LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);
     int st = launch_status("conv3x3_wgrad_rows");
     if (st) return st;
     GemmParams p = {};

@@ -87,21 +87,33 @@ def conv12_fwd_ok(x, dtype):
             and bool(_lib.lib().ocrk_conv12_fwd_supported(B, IH, IW, dtype_code(dtype))))
 
 
-def conv12_fwd(x, w1, b1, w_nk2, b2):
+def conv12_fwd(x, w1, b1, w_nk2, b2, want_y1=True):
     """conv1 (fused preprocess, ReLU) -> conv2 (no activation) with conv2's per-row BN
-    partials (ocrk_conv12_fwd). Returns y1 [B,IH-2,IW-2,32] bf16, its ReLU bit mask
-    u8 [.., 4], z [B,IH-2,IW-2,32] bf16, stats [B*(IH-2), 2, 32]."""
+    partials (ocrk_conv12_fwd). Returns y1 [B,IH-2,IW-2,32] bf16 (None unless want_y1:
+    the backward recomputes it, conv2_bwd_weight_c1x), its ReLU bit mask u8 [.., 4],
+    z [B,IH-2,IW-2,32] bf16, stats [B*(IH-2), 2, 32]."""
     _chk(x, w1, b1, w_nk2, b2)
     B, IH, IW = x.shape[:3]
     H, W = IH - 2, IW - 2
     dev = x.device
-    y1 = torch.empty(B, H, W, 32, dtype=torch.bfloat16, device=dev)
+    y1 = torch.empty(B, H, W, 32, dtype=torch.bfloat16, device=dev) if want_y1 else None
     bits = torch.empty(B, H, W, 4, dtype=torch.uint8, device=dev)
     z = torch.empty(B, H, W, 32, dtype=torch.bfloat16, device=dev)
     stats = torch.empty(B * H, 2, 32, dtype=torch.float32, device=dev)
     call("ocrk_conv12_fwd", ptr(x), int(x.dtype == torch.uint8), B, IH, IW, ptr(w1), ptr(b1), ptr(w_nk2), ptr(b2),
          ptr(y1), ptr(bits), ptr(z), ptr(stats), BF16, _stream(x))
     return y1, bits, z, stats
+
+
+def conv2_bwd_weight_c1x(x, w1, b1, dz, dw, accumulate=True):
+    """conv2's weight gradient with y1 = relu(conv1(x)) recomputed from the image x [B,IH,IW]
+    (u8 or bf16) instead of read (ocrk_conv2_bwd_weight_c1x); dz [B,IH-2,IW-2,32] bf16."""
+    _chk(x, w1, b1, dz, dw)
+    B, IH, IW = x.shape[:3]
+    nb = _lib.lib().ocrk_conv3x3_wgrad_workspace_size(B, IH - 2, IW - 2, 32, 32)
+    ws = _ws(nb, x.device)
+    call("ocrk_conv2_bwd_weight_c1x", ptr(x), int(x.dtype == torch.uint8), B, IH, IW, ptr(w1), ptr(b1), ptr(dz),
+         ptr(dw), int(accumulate), ptr(ws), nb, BF16, _stream(x))
 
 
 def conv1_bwd_weight(x, dz, dw, db, accumulate=True):

@@ -97,10 +97,15 @@ class _ConvBlock(torch.autograd.Function):
                 and options.get("CONV12_FUSED") and K.conv12_fwd_ok(x, dt)):
             # conv1 -> conv2 in one row walk: conv1's rows produced into conv2's ring (never
             # re-read from HBM), y1 and its ReLU bit mask written for the backward
+            # (or, CONV12_RECOMPUTE, only the bit mask: conv2's weight gradient recomputes y1
+            # from the image, conv2_bwd_weight_c1x)
             w_nk2, _ = store.conv_images(even, dt)
+            want_y1 = not options.get("CONV12_RECOMPUTE")
             y_odd, bits, z12, st12 = K.conv12_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], w_nk2,
-                                                  P[pe + "/bias"])
-            ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(y_odd, x) else None
+                                                  P[pe + "/bias"], want_y1=want_y1)
+            ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(z12, x) else None
+            if y_odd is None and ctx.relu_bits is None:    # the fused backward is what needs no y1
+                y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
             zs = (z12, st12)
         elif k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
             # the ReLU's bit mask for the fused conv2 backward-data + conv1 weight gradient
@@ -118,7 +123,7 @@ class _ConvBlock(torch.autograd.Function):
                 y_odd, ctx.relu_bits = K.conv3x3_fwd_relu_bits(x, w_nk, P[f"convnet/{odd}/bias"])
             else:
                 y_odd = K.conv3x3_fwd(x, w_nk, P[f"convnet/{odd}/bias"], relu=True)
-        B, H, W, _ = y_odd.shape
+        B, H, W, _ = (y_odd if zs is None else zs[0]).shape
         M = B * H * W
         w_nk, _ = store.conv_images(even, dt)
         C = w_nk.shape[0]
@@ -205,9 +210,13 @@ class _ConvBlock(torch.autograd.Function):
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
             # contracted as it is produced, never stored: its only consumer is conv1's dW)
             flush_late()
-            with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):
+            with _conv_side(store, x if y_odd is None else y_odd, dz, *_conv_late_tensors(store)):
                 _conv_late_run(store)
-                _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
+                if y_odd is None:                          # conv12 wrote no y1: recomputed per row
+                    K.conv2_bwd_weight_c1x(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dz,
+                                           G[pe + "/kernel"])
+                else:
+                    _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             bits = ctx.relu_bits
             K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, None if bits is not None else y_odd, x, G[po + "/kernel"],
                                          G[po + "/bias"], relu_bits=bits)

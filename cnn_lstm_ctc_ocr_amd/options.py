@@ -25,6 +25,7 @@ _HOST_DEFAULTS = {
     "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
     "PREFETCH_IMAGES": 0,     # 1: the weight-image refresh on its own stream beside conv1 (measured slower)
     "CONV12_FUSED": 1,        # 0: conv1 and conv2 forward as two passes (y1 written, then re-read)
+    "CONV12_RECOMPUTE": 0,    # 1: conv12 writes no y1, conv2's weight gradient recomputes it (measured +55 us)
     "CONV_BIAS_SIDE": 0,      # 1: conv / BN bias-gradient reductions ride the next conv side fork (measured slower)
     "CONV_SIDE_MERGE_FROM": 2,  # blocks k > this merge their odd weight gradient into the next fork
     "CONV_SIDE_MERGE": 1,     # 0: a side-stream fork for each conv weight gradient (two per block)

@@ -176,12 +176,21 @@ int ocrk_conv1_fwd_relu_bits(const void* x, int x_is_u8, int B, int H, int W, co
  * the MFMA with hi + lo bf16 operands) instead of being written and re-read by conv2. Replaces
  * ocrk_conv1_fwd_relu_bits + ocrk_conv3x3_fwd_rowstats of the first block. x [B,IH,IW] u8
  * (x_is_u8) or bf16; w1 f32 [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32];
- * y1, z bf16 [B,IH-2,IW-2,32]; relu_bits u8 [B,IH-2,IW-2][4]; stats [B*(IH-2)][2][32]
- * (tile_rows = IW-2). */
+ * y1, z bf16 [B,IH-2,IW-2,32] (y1 may be NULL: not written); relu_bits u8 [B,IH-2,IW-2][4];
+ * stats [B*(IH-2)][2][32] (tile_rows = IW-2). */
 int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype);
 int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
                     const void* w_nk2, const float* b2, void* y1, void* relu_bits, void* z, float* stats, int dtype,
                     void* stream);
+/* conv2's weight gradient (conv_layer 2's backward, model.py:84-109) with its input
+ * y1 = relu(conv1(x)) recomputed per row from the image instead of read: the partner of
+ * ocrk_conv12_fwd with y1 = NULL, bit-identical to ocrk_conv3x3_bwd_weight on the y1 that
+ * ocrk_conv12_fwd writes. dz bf16 [B,IH-2,IW-2,32]; dw f32 [3][3][32][32] (+)=; ws per
+ * ocrk_conv3x3_wgrad_workspace_size(B, IH-2, IW-2, 32, 32). */
+int ocrk_conv2_bwd_weight_c1x_supported(int B, int IH, int IW, int dtype);
+int ocrk_conv2_bwd_weight_c1x(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
+                              const void* dz, float* dw, int accumulate, void* ws, size_t ws_bytes, int dtype,
+                              void* stream);
 /* conv1 weight/bias gradient from dz = dL/d(pre-ReLU conv1), f32 outputs. */
 size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
 int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,
