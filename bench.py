@@ -53,7 +53,14 @@ def synthetic_batch(rng, B, W, T, device):
 
 def work_conv_fwd(args):
     # (x, B, H, W, cin, w_nk, bias, cout, ...): 2 * pixels * 9 * cin * cout FLOP
+    # (ocrk_conv3x3_fwd, _rowstats, _relu_bits)
     return 2.0 * args[1] * args[2] * args[3] * 9 * args[4] * args[7]
+
+
+def work_conv12_fwd(args):
+    # (x, x_is_u8, B, IH, IW, ...): conv1 (1 -> 32, 'valid') and conv2 (32 -> 32) over the
+    # same B x (IH-2) x (IW-2) pixels in one launch
+    return 2.0 * args[2] * (args[3] - 2) * (args[4] - 2) * 9 * (1 * 32 + 32 * 32)
 
 
 def work_lstm_fwd(args):
@@ -78,8 +85,11 @@ def work_dw(args):
 
 ROOFLINE_OPS = {
     # conv2-conv5 run on the row-walking kernels (ocrk_conv3x3_fwd_rowstats for the BN layers)
-    "conv": (("ocrk_conv3x3_fwd", "ocrk_conv3x3_fwd_rowstats"), work_conv_fwd,
-             "conv2-conv8 forward launches (row-walking conv2-conv5, implicit GEMM conv6-conv8; MFMA bf16)"),
+    "conv": (("ocrk_conv12_fwd", "ocrk_conv3x3_fwd", "ocrk_conv3x3_fwd_rowstats", "ocrk_conv3x3_fwd_relu_bits"),
+             {"ocrk_conv12_fwd": work_conv12_fwd, "ocrk_conv3x3_fwd": work_conv_fwd,
+              "ocrk_conv3x3_fwd_rowstats": work_conv_fwd, "ocrk_conv3x3_fwd_relu_bits": work_conv_fwd},
+             "conv1-conv8 forward launches (conv1 -> conv2 as one row walk, row-walking conv3-conv5, implicit "
+             "GEMM conv6-conv8; MFMA bf16)"),
     "lstm": ("ocrk_lstm_fwd", work_lstm_fwd, "recurrent h.W_h time loop, both directions (MFMA bf16)"),
     "gemm": ("ocrk_gemm", work_gemm, "dense GEMM launches"),
     "dw": ("ocrk_gemm", work_dw, "recurrent weight-gradient GEMMs dW = [x, h_prev]^T dG, both directions batched "
@@ -656,7 +666,8 @@ def main():
 
     def arm_probes():
         for name, k in armed.items():
-            _lib.PROBES[name] = (ROOFLINE_OPS[k][1], probes[k])
+            fn = ROOFLINE_OPS[k][1]
+            _lib.PROBES[name] = (fn[name] if isinstance(fn, dict) else fn, probes[k])
         if args.breakdown:
             for name in _lib.SIGNATURES:
                 if name not in op_names and not name.endswith(("_size", "version", "last_error", "tiles")) \

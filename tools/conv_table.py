@@ -1,4 +1,5 @@
-"""Per-layer table of the conv2-conv8 forward launches of the bench step:
+"""Per-layer table of the conv1/conv2-conv8 forward launches of the bench step (conv1 -> conv2
+as one launch, conv12_fwd_rows_kernel, when the bf16 step fuses them):
 duration (rocprofv3 --kernel-trace), TFLOP/s and MFMA fraction, and HBM
 bytes from the PMC passes (FETCH_SIZE x2 per the gfx950 correction +
 WRITE_SIZE) against the algorithmic bytes (input + output activations +
@@ -14,7 +15,8 @@ import os
 import re
 from collections import defaultdict
 
-FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, false)*>|conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel")
+FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, false)*>|"
+                 r"conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel|conv12_fwd_rows_kernel")
 B = 256
 LAYERS = [("conv2", 30, 254, 32, 32), ("conv3", 15, 127, 32, 64), ("conv4", 15, 127, 64, 64),
           ("conv5", 7, 126, 64, 128), ("conv6", 7, 126, 128, 128), ("conv7", 3, 125, 128, 256),
@@ -77,6 +79,14 @@ def main():
         M = B * H * W
         fl = 2.0 * M * 9 * cin * cout
         alg = (M * cin + M * cout + 9 * cin * cout) * 2
+        if name == "conv2" and "conv12" in names.get(name, ""):
+            # conv1 -> conv2 in one launch: the u8 image in; y1 (bf16), its ReLU bit mask
+            # (4 B per pixel) and z (bf16) out; both layers' weights
+            fl = 2.0 * M * 9 * (1 * 32 + cin * cout)
+            alg = B * (H + 2) * (W + 2) + M * (2 * cin + 4 + 2 * cout) + 9 * 32 * 4 + 9 * cin * cout * 2
+            name_shown = "conv1+2 1->32->32"
+        else:
+            name_shown = f"{name} {cin}->{cout}"
         us = sum(dur[name]) / max(len(dur[name]), 1)
         rd = 2 * sum(fetch[name]) / max(len(fetch[name]), 1)
         wr = sum(write[name]) / max(len(write[name]), 1)
@@ -85,7 +95,7 @@ def main():
         roof = min(PEAK, ai * HBM)
         tot_us += us
         tot_fl += fl
-        lines.append(f"| {name} {cin}->{cout} | `{names.get(name, '?')}` | {us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | "
+        lines.append(f"| {name_shown} | `{names.get(name, '?')}` | {us:.1f} | {tf:.0f} | {tf / PEAK:.3f} | "
                      f"{ai:.0f} | {roof:.0f} | {tf / roof:.3f} | {alg / 1e6:.1f} | {(rd + wr) / 1e6:.1f} | "
                      f"{(rd + wr) / alg:.2f} |")
     tf = tot_fl / tot_us / 1e6
