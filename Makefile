@@ -5,10 +5,16 @@ CSRC  := cnn_lstm_ctc_ocr_amd/csrc
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 SRC   := $(wildcard $(CSRC)/*.hip)
 OBJ   := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRC))
-HDR   := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
+HDR   := $(wildcard $(CSRC)/*.h) $(filter-out include/ocrk_comm.h,$(wildcard include/*.h))
 LIB   := cnn_lstm_ctc_ocr_amd/libocrk.so
+# the optional RCCL gradient all-reduce (include/ocrk_comm.h): its own object, so
+# libocrk.so does not link RCCL
+COMMLIB := cnn_lstm_ctc_ocr_amd/libocrk_comm.so
 
-all: $(LIB)
+all: $(LIB) $(COMMLIB)
+
+$(COMMLIB): cnn_lstm_ctc_ocr_amd/comm/ocrk_comm.cpp include/ocrk_comm.h
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude -Wall -o $@ $< -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
@@ -32,6 +38,6 @@ build/exp/%.o: $(CSRC)/%.hip $(HDR)
 	$(HIPCC) $(HIPFLAGS) -DOCRK_EXPERIMENTS -c $< -o $@
 
 clean:
-	rm -rf build $(LIB) $(EXPLIB)
+	rm -rf build $(LIB) $(COMMLIB) $(EXPLIB)
 
 .PHONY: all exp clean
