@@ -13,7 +13,7 @@ COMMLIB := cnn_lstm_ctc_ocr_amd/libocrk_comm.so
 
 all: $(LIB) $(COMMLIB)
 
-$(COMMLIB): cnn_lstm_ctc_ocr_amd/comm/ocrk_comm.cpp include/ocrk_comm.h
+$(COMMLIB): $(CSRC)/ocrk_comm.cpp include/ocrk_comm.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude -Wall -o $@ $< -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(LIB): $(OBJ)
