@@ -11,7 +11,16 @@ LIB   := cnn_lstm_ctc_ocr_amd/libocrk.so
 # libocrk.so does not link RCCL
 COMMLIB := cnn_lstm_ctc_ocr_amd/libocrk_comm.so
 
+# built only where RCCL's header is present: libocrk.so never depends on it
+RCCL_H := $(firstword $(wildcard /opt/rocm/include/rccl/rccl.h /opt/rocm/include/rccl.h))
+ifeq ($(RCCL_H),)
+all: $(LIB)
+	@echo "rccl.h not found: $(COMMLIB) (optional all-reduce C ABI) not built"
+else
 all: $(LIB) $(COMMLIB)
+endif
+
+comm: $(COMMLIB)
 
 $(COMMLIB): $(CSRC)/ocrk_comm.cpp include/ocrk_comm.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude -Wall -o $@ $< -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
@@ -40,4 +49,4 @@ build/exp/%.o: $(CSRC)/%.hip $(HDR)
 clean:
 	rm -rf build $(LIB) $(COMMLIB) $(EXPLIB)
 
-.PHONY: all exp clean
+.PHONY: all comm exp clean

@@ -574,45 +574,102 @@ bn_bwd_route_kernel(const T* __restrict__ z, const T* __restrict__ dp, int B, in
 //   sum da = sum_{p > 0} dp,   sum da * xhat = sum_{p > 0} dp * (p - beta) / gamma
 // over the POOLED elements -- a stream over p and dp (1/4 of z's bytes for the 2x2
 // pools, 1/2 and 1/3 for the others) instead of the window walk over z. xhat is
-// recovered from the stored p (bf16 in the bf16 path: the same 2^-9 class of error
-// as the bf16 z the walk reads); where |gamma| is tiny the recovery is not used
-// (ocrk_bn_relu_pool_bwd_pooled falls back to the walk). Per-block [s1 | s2] rows of
-// 2C, the window walk's slab format. Thread = 8 channels, 4 items in flight.
+// recovered from the stored p to |p| ulp / |gamma| ~ (|beta| / |gamma| + |xhat|) ulp,
+// where the walk's (z - mean) * invstd carries (|mean| * invstd + |xhat|) ulp: a
+// channel whose |beta| / |gamma| exceeds max(4, |mean| * invstd) (gamma = 0 included)
+// is ill-conditioned for the recovery, and the 8-channel group holding it evaluates its
+// windows from z instead ([TF1] first max of relu(bn(z)), row-major scan, exactly the
+// walk's per-window terms) -- decided per channel on the device, no host sync.
+// Per-block [s1 | s2] rows of 2C, the window walk's slab format. Thread = 8
+// channels, 4 items in flight.
 template <typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_pooled_sums_kernel(const T* __restrict__ p, const T* __restrict__ dp, int64_t items, int C,
-                          const float* __restrict__ gamma, const float* __restrict__ beta, int items_per_block,
+                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                          const float* __restrict__ mean, const float* __restrict__ invstd, const T* __restrict__ z,
+                          int B, int H, int W, int kh, int kw, int sh, int sw, int time_major, int items_per_block,
                           float* __restrict__ slab) {
     __shared__ float red[256][17];
     const int G = C / 8;
     const int g = threadIdx.x % G, c0 = 8 * g;     // fixed: items_per_block % 256 == 0, 256 % G == 0
     float rg[8], bt[8], s1[8], s2[8];
+    bool from_z = false;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        rg[i] = gamma[c0 + i] != 0.f ? 1.f / gamma[c0 + i] : 0.f;   // gamma = 0: xhat unrecoverable (term dropped)
-        bt[i] = beta[c0 + i];
+        const float ga = gamma[c0 + i], be = beta[c0 + i];
+        const float cz = fabsf(mean[c0 + i]) * invstd[c0 + i];
+        from_z |= !(fabsf(be) <= fmaxf(4.f, cz) * fabsf(ga));       // gamma = 0 or NaN: z
+        rg[i] = ga != 0.f ? 1.f / ga : 0.f;
+        bt[i] = be;
         s1[i] = s2[i] = 0.f;
     }
     const int64_t i0 = (int64_t)blockIdx.x * items_per_block;
     const int64_t i1 = min(items, i0 + items_per_block);
-    constexpr int U = 4;
-    for (int64_t it = i0 + threadIdx.x; it < i1; it += 256 * U) {
-        Pend8<T> pr[U], dr[U];
+    if (from_z) {
+        // the z form for this channel group: each pooled element's window re-evaluated
+        const int Ho = (H - kh) / sh + 1, Wo = (W - kw) / sw + 1;
+        float sc[8], sf[8], mu[8], is[8];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t q = min(it + 256 * u, i1 - 1);       // clamped (a fixed load count)
-            pr[u] = load_pend8(p + q * 8);
-            dr[u] = load_pend8(dp + q * 8);
+        for (int i = 0; i < 8; ++i) {
+            is[i] = invstd[c0 + i];
+            mu[i] = mean[c0 + i];
+            sc[i] = gamma[c0 + i] * is[i];
+            sf[i] = beta[c0 + i] - mu[i] * sc[i];
         }
+        for (int64_t it = i0 + threadIdx.x; it < i1; it += 256) {
+            const int64_t pix = it / G;
+            int b, ho, wo;
+            if (time_major) {                       // [Wo][B][Ho][C]
+                ho = (int)(pix % Ho);
+                const int64_t r = pix / Ho;
+                b = (int)(r % B);
+                wo = (int)(r / B);
+            } else {                                // [B][Ho][Wo][C]
+                wo = (int)(pix % Wo);
+                const int64_t r = pix / Wo;
+                ho = (int)(r % Ho);
+                b = (int)(r / Ho);
+            }
+            float best[8], zb[8];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (it + 256 * u >= i1) break;
-            const F8 pv = cvt8(pr[u]), dv = cvt8(dr[u]);
+            for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; zb[i] = 0.f; }
+            for (int dh = 0; dh < kh; ++dh)
+                for (int dw = 0; dw < kw; ++dw) {
+                    const F8 v = load8(z + (((int64_t)b * H + ho * sh + dh) * W + wo * sw + dw) * C + c0);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float y = fmaxf(fmaf(v.v[i], sc[i], sf[i]), 0.f);
+                        if (y > best[i]) { best[i] = y; zb[i] = v.v[i]; }
+                    }
+                }
+            const F8 dv = load8(dp + it * 8);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const float d = pv.v[i] > 0.f ? dv.v[i] : 0.f;
+                const float d = best[i] > 0.f ? dv.v[i] : 0.f;
                 s1[i] += d;
-                s2[i] += d * ((pv.v[i] - bt[i]) * rg[i]);
+                s2[i] += d * ((zb[i] - mu[i]) * is[i]);
+            }
+        }
+    } else {
+        constexpr int U = 4;
+        for (int64_t it = i0 + threadIdx.x; it < i1; it += 256 * U) {
+            Pend8<T> pr[U], dr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = min(it + 256 * u, i1 - 1);       // clamped (a fixed load count)
+                pr[u] = load_pend8(p + q * 8);
+                dr[u] = load_pend8(dp + q * 8);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (it + 256 * u >= i1) break;
+                const F8 pv = cvt8(pr[u]), dv = cvt8(dr[u]);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float d = pv.v[i] > 0.f ? dv.v[i] : 0.f;
+                    s1[i] += d;
+                    s2[i] += d * ((pv.v[i] - bt[i]) * rg[i]);
+                }
             }
         }
     }
@@ -853,7 +910,10 @@ extern "C" size_t ocrk_bn_bwd_bias_slab_rows(int B, int H, int W, int C, int kh,
     return (size_t)bn_bwd_bias_rows(B, H, W, C, kh, kw, sh, sw);
 }
 
+// 0 = the pooled-output form is not taken for this shape / pool (or option BN_ROUTE=0):
+// ocrk_bn_relu_pool_bwd_pooled then refuses a bias_slab (callers take the z form)
 extern "C" size_t ocrk_bn_bwd_pooled_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw) {
+    if (!bn_route_variant(kh, kw, sh, sw, H, W)) return 0;
     if (C < 8 || C % 8 != 0 || (int64_t)B * H * W == 0) return 1;
     return (size_t)bn_bwd_bias_rows(B, H, W, C, kh, kw, sh, sw, true);
 }
@@ -905,10 +965,12 @@ static int bn_bwd_impl(const void* z, const void* dp, int B, int H, int W, int C
         nr = (int)ocrk::cdiv(pitems, ipb2);
         if (dtype == OCRK_BF16)
             bn_bwd_pooled_sums_kernel<bf16><<<nr, 256, 0, s>>>((const bf16*)pooled, (const bf16*)dp, pitems, C, gamma,
-                                                               beta, ipb2, slab);
+                                                               beta, mean, invstd, (const bf16*)z, B, H, W, kh, kw,
+                                                               sh, sw, dp_time_major, ipb2, slab);
         else
             bn_bwd_pooled_sums_kernel<float><<<nr, 256, 0, s>>>((const float*)pooled, (const float*)dp, pitems, C,
-                                                                gamma, beta, ipb2, slab);
+                                                                gamma, beta, mean, invstd, (const float*)z, B, H, W,
+                                                                kh, kw, sh, sw, dp_time_major, ipb2, slab);
     } else if (rk) {
         const int Ho = (H - kh) / kh + 1, Wo = (W - kw) / sw + 1;
         const int nseg = (int)ocrk::cdiv(Wo, seg);
@@ -1019,6 +1081,10 @@ extern "C" int ocrk_bn_relu_pool_bwd_pooled(const void* z, const void* pooled, c
                                             void* dz, float* dgamma, float* dbeta, float* dbias, int accumulate,
                                             float* bias_slab, void* ws, size_t ws_bytes, int dtype, void* stream) {
     OCRK_REQUIRE(pooled, "ocrk_bn_relu_pool_bwd_pooled: pooled is required");
+    // a [bias | dgamma] slab exists only for the pooled form; the z form would write C-wide rows
+    OCRK_REQUIRE(!bias_slab || bn_route_variant(kh, kw, sh, sw, H, W),
+                 "ocrk_bn_relu_pool_bwd_pooled: bias_slab given but the pooled form is off for this pool "
+                 "(ocrk_bn_bwd_pooled_bias_slab_rows() == 0)");
     return bn_bwd_impl(z, dp, B, H, W, C, mean, invstd, gamma, beta, kh, kw, sh, sw, dp_time_major, dz, dgamma,
                        dbeta, bias_slab ? nullptr : dbias, accumulate, bias_slab, ws, ws_bytes, dtype, stream, 0,
                        nullptr, nullptr, nullptr, pooled);

@@ -50,12 +50,21 @@ int ocrk_comm_init(void** comm, int world, int rank, const void* id, int device)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return fail(OCRK_COMM_ERR_INVALID_ARG, "ocrk_comm_init: device %d of %d", device, ndev);
+    // the communicator binds the CURRENT device: switch to `device` for the init and
+    // give the calling thread its previous device back afterwards
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return fail(OCRK_COMM_ERR_HIP, "ocrk_comm_init: hipGetDevice");
     if (hipSetDevice(device) != hipSuccess) return fail(OCRK_COMM_ERR_HIP, "ocrk_comm_init: hipSetDevice(%d)", device);
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
     ncclComm_t c = nullptr;
     const int st = rccl_status(ncclCommInitRank(&c, world, uid, rank), "ocrk_comm_init");
     if (st == OCRK_COMM_OK) *comm = c;
+    if (prev != device && hipSetDevice(prev) != hipSuccess) {
+        if (c) ncclCommDestroy(c);
+        *comm = nullptr;
+        return fail(OCRK_COMM_ERR_HIP, "ocrk_comm_init: restoring device %d", prev);
+    }
     return st;
 }
 

@@ -348,10 +348,15 @@ def bn_relu_pool_bwd(z, dp, mean, invstd, gamma, beta, pool, dp_time_major, dgam
     if pooled is not None:
         if pooled.shape != dp.shape or pooled.dtype != dp.dtype:
             raise ValueError("pooled must have dp's shape and dtype")
+        # 0 rows: the library takes the z form for this pool (or BN_ROUTE=0) -- use it here too,
+        # so a deferred bias slab has the z form's C-wide rows
+        rows = _lib.lib().ocrk_bn_bwd_pooled_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
+        if rows == 0:
+            pooled = None
+    if pooled is not None:
         slab = None
         if dbias is not None and defer is not None:
             # [bias | dgamma] partial rows: both reductions deferred
-            rows = _lib.lib().ocrk_bn_bwd_pooled_bias_slab_rows(B, H, W, C, kh, kw, sh, sw)
             slab = torch.empty(rows, 2 * C, dtype=torch.float32, device=z.device)
         call("ocrk_bn_relu_pool_bwd_pooled", ptr(z), ptr(pooled), ptr(dp), B, H, W, C, ptr(mean), ptr(invstd),
              ptr(gamma), ptr(beta), kh, kw, sh, sw, int(dp_time_major), ptr(dz), ptr(dgamma), ptr(dbeta),

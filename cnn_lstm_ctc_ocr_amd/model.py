@@ -92,6 +92,10 @@ class _ConvBlock(torch.autograd.Function):
         pe = f"convnet/{even}"
         ctx.bn_sync = None
         ctx.relu_bits = None
+        # route decisions the backward must follow are taken here, once (an options.override
+        # block may end between the forward and the backward)
+        ctx.c1_fused = bool(k == 1 and not ctx.exact and options.get("CONV1_FUSED"))
+        ctx.pooled_bn = bool(options.get("POOLED_BN"))
         zs = None
         if (k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED")
                 and options.get("CONV12_FUSED") and K.conv12_fwd_ok(x, dt)):
@@ -197,7 +201,7 @@ class _ConvBlock(torch.autograd.Function):
                                 dbias=G[pe + "/bias"], defer=late,      # conv bias grad fused
                                 sync=ctx.bn_sync,
                                 # dgamma / dbeta from the saved pooled output instead of a walk over z
-                                pooled=pooled if ctx.bn_sync is None and options.get("POOLED_BN") else None)
+                                pooled=pooled if ctx.bn_sync is None and ctx.pooled_bn else None)
         B, H, W, C = dz.shape
         if k > 1:
             flush_late()
@@ -205,7 +209,7 @@ class _ConvBlock(torch.autograd.Function):
                 _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
-        if k == 1 and not ctx.exact and options.get("CONV1_FUSED") and K.conv2_bwd_data_conv1_wgrad_ok(dz, x):
+        if ctx.c1_fused and K.conv2_bwd_data_conv1_wgrad_ok(dz, x):
             # the step's tail: conv2's weight gradient (y1, dz) on the side stream beside one
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
             # contracted as it is produced, never stored: its only consumer is conv1's dW)

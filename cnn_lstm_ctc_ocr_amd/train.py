@@ -44,22 +44,44 @@ class GradBuckets:
     (one bucketed all-reduce after backward, overlapped with the
     conv backward; RCCL over xGMI with backend "nccl".)"""
 
-    def __init__(self, store, group=None):
-        self.store, self.group = store, group
+    def __init__(self, store, group=None, comm=None, force=False):
+        """comm: a comm.Communicator (libocrk_comm.so, include/ocrk_comm.h) that
+        carries the exchange instead of torch.distributed -- the C-ABI
+        all-reduce a host without PyTorch would bind. force: run the whole
+        exchange even with one rank (the sum over one rank is the identity), so
+        the collective really executes on the comm stream beside the conv
+        backward -- the C4 path's ordering, exercised on a one-GPU box."""
+        self.store, self.group, self.comm, self.force = store, group, comm, bool(force)
         rnn = [off for name, (tr, off, _s) in store.offsets.items() if tr and name.startswith("rnn/")]
         self.split = min(rnn) if rnn else store.flat_grad.numel()
         self.work = None
         self._stream = None
+        self._comm_world = comm.info()[0] if comm is not None else None
 
     def world(self):
+        if self.comm is not None:
+            return self._comm_world
         if not (dist.is_available() and dist.is_initialized()):
             return 1
         return dist.get_world_size(self.group)
 
+    def active(self):
+        """True when the step exchanges gradients (several ranks, or forced)."""
+        return self.world() > 1 or (self.force and (self.comm is not None or
+                                                    (dist.is_available() and dist.is_initialized())))
+
+    def _sum_(self, t, async_op=False):
+        """SUM all-reduce of t in place on the current stream (RCCL through
+        torch.distributed or through the C ABI)."""
+        if self.comm is not None:
+            self.comm.allreduce_(t)
+            return None
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
     def rnn_ready(self, *_):
         """Start the recurrent bucket's all-reduce (called by the hook on the
         conv tower's output gradient, i.e. after the recurrent backward)."""
-        if self.world() <= 1 or self.work is not None:
+        if not self.active() or self.work is not None:
             return
         g = self.store.flat_grad
         if g.is_cuda:
@@ -69,49 +91,58 @@ class GradBuckets:
             for ev in self.store.pending:                   # the side-stream weight gradients
                 K.wait_mark(self._stream, ev)
             with torch.cuda.stream(self._stream):
-                self.work = dist.all_reduce(g[self.split:], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                self.work = self._sum_(g[self.split:], async_op=True)
+                if self.work is None:                       # the C ABI: stream-ordered, joined in finish()
+                    self.work = "stream"
                 g.record_stream(self._stream)
         else:
-            self.work = dist.all_reduce(g[self.split:], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.work = self._sum_(g[self.split:], async_op=True)
 
     def finish(self):
         """After the whole backward (and store.join()): reduce the rest, wait
         for both; returns 1/world (the mean-of-equal-shards factor)."""
-        world = self.world()
-        if world <= 1:
+        if not self.active():
             return 1.0
+        world = self.world()
         g = self.store.flat_grad
         if self.work is None:                               # no hook fired: one flat all-reduce
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+            self._sum_(g)
         else:
-            dist.all_reduce(g[:self.split], op=dist.ReduceOp.SUM, group=self.group)
-            self.work.wait()
+            self._sum_(g[:self.split])
+            if self.work == "stream":
+                torch.cuda.current_stream(g.device).wait_stream(self._stream)
+            else:
+                self.work.wait()
             self.work = None
         if g.is_cuda:
             # every rank gets the same device status word (the OR over ranks) for
             # this step, so a device error raises on all ranks at the same step
             # (Trainer.poll_status) instead of one rank raising while its peers
             # block in the next collective
-            or_allreduce_status(K.status_word(g.device), self.group)
+            or_allreduce_status(K.status_word(g.device), self.group, comm=self.comm)
         return 1.0 / world
 
 
 _STATUS_BITS = {}
 
 
-def or_allreduce_status(word, group=None):
+def or_allreduce_status(word, group=None, comm=None):
     """OR the int32 status word `word` ([1], a bitmask) over the ranks, in place.
     A MAX all-reduce of the word itself would keep only the numerically largest
     rank's word; instead its 31 bits are spread into a one-hot vector, that is
-    MAX-reduced in a separate buffer, and the result is OR-ed back into the word,
-    so every rank's bits -- its own included -- survive. Stream-ordered (no host
-    sync)."""
+    MAX-reduced in a separate buffer (comm: the C ABI's SUM, then > 0 -- the same
+    OR), and the result is OR-ed back into the word, so every rank's bits -- its
+    own included -- survive. Stream-ordered (no host sync)."""
     key = word.device
     if key not in _STATUS_BITS:
         _STATUS_BITS[key] = torch.arange(31, dtype=torch.int32, device=word.device)
     bits = _STATUS_BITS[key]
     vec = torch.bitwise_and(torch.bitwise_right_shift(word, bits), 1)
-    dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=group)
+    if comm is not None:
+        comm.allreduce_(vec)
+        vec = (vec > 0).to(torch.int32)
+    else:
+        dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=group)
     word.bitwise_or_(torch.bitwise_left_shift(vec, bits).sum(dtype=torch.int32).view(1))
     return word
 
@@ -146,7 +177,7 @@ class Trainer:
 
     def __init__(self, store, learning_rate=1e-4, momentum=0.9, decay_rate=0.9, decay_steps=2 ** 16,
                  decay_staircase=False, beta2=0.999, epsilon=1e-8, process_group=None, global_step=0,
-                 summary=None, summary_every=100, sync_bn=False):
+                 summary=None, summary_every=100, sync_bn=False, comm=None, force_exchange=False):
         """summary: a summary.SummaryWriter; every `summary_every` steps it gets
         learning_rate (train.py:139's tf.summary.scalar), the step's loss and
         the global crops/s since the previous record (no sync: device values
@@ -154,7 +185,8 @@ class Trainer:
         TRAIN-mode BatchNorm statistics (and the backward's two sums) span all
         ranks' batches -- one small SUM all-reduce per BN layer each way -- so N
         ranks compute the single-device reference's step on the union of their
-        batches; off (the default) they stay per rank."""
+        batches; off (the default) they stay per rank. comm / force_exchange:
+        GradBuckets' C-ABI communicator and its one-rank forced exchange."""
         self.store = store
         self.sync_bn = bool(sync_bn)               # the group is resolved at each step (_bn_group)
         self.summary = summary
@@ -177,7 +209,7 @@ class Trainer:
         self._status_stream = None
         self._status_ring = collections.deque()     # data parallel: (event, pinned copy) per step
         self.status_lag = 2
-        self.buckets = GradBuckets(store, process_group)
+        self.buckets = GradBuckets(store, process_group, comm=comm, force=force_exchange)
         self.overlap_allreduce = True          # start the recurrent bucket mid-backward (GradBuckets)
 
     def learning_rate(self, step=None):
@@ -197,6 +229,8 @@ class Trainer:
         return self.group if self.group is not None else dist.group.WORLD
 
     def world_size(self):
+        if self.buckets.comm is not None:
+            return self.buckets.world()
         if dist.is_available() and dist.is_initialized():
             return dist.get_world_size(self.group)
         return 1
@@ -241,7 +275,7 @@ class Trainer:
             store.zero_grad()
         self._grads_zeroed = False
         features, seq_len = convnet_layers(image, width, TRAIN, store)
-        if self.overlap_allreduce and features.requires_grad and self.buckets.world() > 1 and \
+        if self.overlap_allreduce and features.requires_grad and self.buckets.active() and \
                 not (features.is_cuda and torch.cuda.is_current_stream_capturing()):
             features.register_hook(self.buckets.rnn_ready)
         logits = rnn_layers(features, seq_len, store.cfg.num_classes, store)
@@ -324,7 +358,7 @@ class Trainer:
     def post_status(self):
         """Queue a non-blocking copy of the device status word (after the step's work)."""
         dev = self.store.device
-        if dev.type == "cuda" and self.world_size() > 1:
+        if dev.type == "cuda" and self.buckets.active():
             buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             buf.copy_(K.status_word(dev), non_blocking=True)
             ev = torch.cuda.Event()

@@ -314,12 +314,16 @@ int ocrk_bn_relu_pool_bwd_slab(const void* z, const void* dp, int B, int H, int 
 /* The same with pass 1 (the dgamma / dbeta sums) read from the forward's pooled
  * output `pooled` (ocrk_bn_relu_pool_fwd's result, laid out as dp) instead of walking
  * z: sum dy = sum_{pooled > 0} dp, sum dy * xhat = sum_{pooled > 0} dp (pooled - beta) / gamma
- * (xhat recovered at each window's max; gamma = 0 drops that channel's xhat terms).
+ * (xhat recovered at each window's max). A channel where |beta| / |gamma| exceeds
+ * max(4, |mean| * invstd) (gamma = 0 included) is ill-conditioned for that recovery:
+ * its 8-channel group re-evaluates its windows from z instead (decided on the device).
  * Window-walk pools only (2x2/[2,2], 2x2/[2,1], [3,1]/[3,1]); others take the z form.
  * dgamma itself is summed from z in the apply walk (xhat as the z form computes it).
  * bias_slab: NULL (dbias (+)= the conv-bias gradient) or the caller's
  * [ocrk_bn_bwd_pooled_bias_slab_rows(...)][2C] partial rows [bias | dgamma] -- both
- * reductions are then the caller's (ocrk_slab_sum over each half; dbias ignored). */
+ * reductions are then the caller's (ocrk_slab_sum over each half; dbias ignored).
+ * ocrk_bn_bwd_pooled_bias_slab_rows() == 0: this pool takes the z form (or option
+ * BN_ROUTE is 0), and a bias_slab is refused (OCRK_ERR_INVALID_ARG). */
 size_t ocrk_bn_bwd_pooled_bias_slab_rows(int B, int H, int W, int C, int kh, int kw, int sh, int sw);
 int ocrk_bn_relu_pool_bwd_pooled(const void* z, const void* pooled, const void* dp, int B, int H, int W, int C,
                                  const float* mean, const float* invstd, const float* gamma, const float* beta,

@@ -112,3 +112,82 @@ def test_bn_bwd_pooled_matches_z_form(cuda, case, dtype):
         assert np.abs(got[3] - ref[3]).max() <= (1e-3 if dtype == torch.bfloat16 else 1e-5) * scale * np.sqrt(B * H * W)
     np.testing.assert_array_equal(outs[1][0], outs[2][0])   # deferral moves no dz bit
     np.testing.assert_allclose(outs[2][1], outs[1][1], rtol=1e-6, atol=1e-6 * np.abs(outs[1][1]).max())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", CASES[:4], ids=lambda c: "x".join(map(str, c[:4])))
+def test_bn_bwd_pooled_ill_conditioned_channels(cuda, case, dtype):
+    """Channels where xhat = (p - beta) / gamma is ill-conditioned (|gamma| 1e-3..1e-2
+    beside |beta| 0.5..2, gamma = 0, negative gamma) take the z walk's per-window terms
+    inside the pooled pass (the stored output's rounding is amplified by
+    |beta| / |gamma|, ~10 % at gamma = 0.01, beta = 0.5 in bf16). Those channels' dz
+    must match the z form to summation order; the well-conditioned ones as before."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    B, H, W, C, pool = case
+    rng = np.random.default_rng(11 * C + W)
+    tm = pool == (3, 1, 3, 1)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(cuda)   # noqa: E731
+    z = t(rng.standard_normal((B, H, W, C)) * 1.5 + 0.3).to(dtype)
+    mean, inv = t(rng.standard_normal(C) * 0.1 + 0.3), t(rng.random(C) * 0.3 + 0.5)
+    gamma = rng.random(C) + 0.5
+    beta = rng.standard_normal(C) * 0.2
+    ill = np.zeros(C, bool)
+    ill[1::4] = True                                  # every 8-channel group holds some
+    gamma[ill] = rng.uniform(1e-3, 1e-2, ill.sum()) * rng.choice([-1, 1], ill.sum())
+    beta[ill] = rng.uniform(0.5, 2.0, ill.sum())
+    gamma[5] = 0.0
+    ill[5] = True
+    gamma[2] = -gamma[2]                              # negative, well-conditioned
+    gamma, beta = t(gamma), t(beta)
+    p = Kn.bn_relu_pool_fwd(z, mean, inv, gamma, beta, pool, time_major=tm)
+    dp = t(rng.standard_normal(p.shape)).to(dtype)
+    outs = []
+    for pooled in (None, p):
+        dg, db, dbias = (torch.zeros(C, device=cuda) for _ in range(3))
+        dz = Kn.bn_relu_pool_bwd(z, dp, mean, inv, gamma, beta, pool, tm, dg, db, accumulate=False, dbias=dbias,
+                                 pooled=pooled)
+        torch.cuda.synchronize()
+        outs.append((dz.double().cpu().numpy().reshape(-1, C), dg.double().cpu().numpy(), db.double().cpu().numpy()))
+    (zr, gr, br), (zp, gp, bp) = outs
+    per = np.linalg.norm(zp - zr, axis=0) / np.maximum(np.linalg.norm(zr, axis=0), 1e-30)
+    assert per[ill].max() < 1e-4, per[ill]             # the z form's terms, another summation order
+    assert per[~ill].max() < (4e-3 if dtype == torch.bfloat16 else 1e-5), per[~ill]
+    np.testing.assert_allclose(gp, gr, rtol=1e-5, atol=1e-5 * np.abs(gr).max())
+    np.testing.assert_allclose(bp, br, rtol=1e-5, atol=1e-5 * np.abs(br).max())
+
+
+def test_bn_bwd_pooled_defer_without_route(cuda):
+    """with the window walk off (BN_ROUTE=0) the library takes the z form
+    for a pooled call; the deferred bias slab must then have the z form's rows, and
+    dbias / dgamma equal the undeferred z form's (ocrk_bn_bwd_pooled_bias_slab_rows
+    == 0 tells the wrapper so; a pooled bias slab is refused by the C entry)."""
+    from cnn_lstm_ctc_ocr_amd import _lib, options
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    B, H, W, C, pool = CASES[1]
+    rng = np.random.default_rng(3)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(cuda)   # noqa: E731
+    z = t(rng.standard_normal((B, H, W, C))).bfloat16()
+    mean, inv = t(rng.standard_normal(C) * 0.1), t(rng.random(C) * 0.3 + 0.5)
+    gamma, beta = t(rng.random(C) + 0.5), t(rng.standard_normal(C) * 0.2)
+    p = Kn.bn_relu_pool_fwd(z, mean, inv, gamma, beta, pool)
+    dp = t(rng.standard_normal(p.shape)).bfloat16()
+    with options.override(BN_ROUTE=0):
+        assert _lib.lib().ocrk_bn_bwd_pooled_bias_slab_rows(B, H, W, C, *pool) == 0
+        res = []
+        for pooled, late in ((None, None), (p, [])):
+            dg, db, dbias = (torch.zeros(C, device=cuda) for _ in range(3))
+            dz = Kn.bn_relu_pool_bwd(z, dp, mean, inv, gamma, beta, pool, False, dg, db, accumulate=False,
+                                     dbias=dbias, defer=late, pooled=pooled)
+            for fn, _ in late or []:
+                fn()
+            torch.cuda.synchronize()
+            res.append([v.double().cpu().numpy() for v in (dz, dg, db, dbias)])
+        slab = torch.empty(64, 2 * C, device=cuda)
+        with pytest.raises(RuntimeError, match="pooled form is off"):
+            Kn.call("ocrk_bn_relu_pool_bwd_pooled", Kn.ptr(z), Kn.ptr(p), Kn.ptr(dp), B, H, W, C, Kn.ptr(mean),
+                    Kn.ptr(inv), Kn.ptr(gamma), Kn.ptr(beta), *pool, 0, Kn.ptr(torch.empty_like(z)),
+                    Kn.ptr(torch.zeros(C, device=cuda)), Kn.ptr(torch.zeros(C, device=cuda)), None, 0,
+                    Kn.ptr(slab), Kn.ptr(torch.empty(1 << 24, dtype=torch.uint8, device=cuda)), 1 << 24,
+                    Kn.dtype_code(z.dtype), Kn._stream(z))
+    for a, b in zip(*res):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * max(np.abs(b).max(), 1e-30))

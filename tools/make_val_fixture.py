@@ -1,10 +1,11 @@
-"""Build tests/golden/mjsynth_val_words000.npz: every crop of the reference's
-data/val/words-000.tfrecord (803 MJSynth word crops) as DATA -- decoded uint8
-pixels, widths, labels and texts -- for the bf16-vs-fp32 training test
-(tests/test_gpu_train_curves.py). No reference source is stored; the GPU box
-has no /root/reference, so this is how the shard travels.
+"""Build tests/golden/mjsynth_{val,test}_words000.npz: every crop of the
+reference's data/val/words-000.tfrecord (803 MJSynth word crops: the training
+shard of tests/test_gpu_trained.py) and data/test/words-000.tfrecord (the
+held-out shard: trained-weight decode parity and held-out CER) as DATA --
+decoded uint8 pixels, widths, labels and texts. No reference source is stored;
+the GPU box has no /root/reference, so this is how the shards travel.
 
-    python tools/make_val_fixture.py     (needs /root/reference/data; run here)
+    python tools/make_val_fixture.py [val|test]    (needs /root/reference/data; run here)
 
 Decode: input_pipeline.decode_jpeg_gray (libjpeg grayscale via PIL; TF's
 decode_jpeg is unavailable, so bit-parity of the JPEG decode is unpinned --
@@ -26,11 +27,11 @@ from cnn_lstm_ctc_ocr_amd import input_pipeline as P  # noqa: E402
 from cnn_lstm_ctc_ocr_amd.tfrecord import read_word_records  # noqa: E402
 from oracle import ref_graph as G  # noqa: E402
 
-SRC = "/root/reference/data/val/words-000.tfrecord"
+SRC = "/root/reference/data/{}/words-000.tfrecord"
 
 
-def main():
-    recs = list(read_word_records(SRC))
+def main(split="val"):
+    recs = list(read_word_records(SRC.format(split)))
     crops = [P.decode_jpeg_gray(r["image"])[:, :, 0] for r in recs]
     heights = np.array([c.shape[0] for c in crops], np.int32)
     assert heights.max() <= 32
@@ -49,10 +50,10 @@ def main():
     out = {"pixels": pixels, "offsets": offsets, "widths": widths, "heights": heights, "labels": labels,
            "label_len": np.array([int(r["length"]) for r in recs], np.int32),
            "texts": np.array([r["text"] for r in recs])}
-    path = os.path.join(ROOT, "tests", "golden", "mjsynth_val_words000.npz")
+    path = os.path.join(ROOT, "tests", "golden", f"mjsynth_{split}_words000.npz")
     np.savez_compressed(path, **out)
     print(path, os.path.getsize(path), "bytes;", {k: getattr(v, "shape", v) for k, v in out.items()})
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:2])
