@@ -130,14 +130,15 @@ def _cpu_batch(rng, B, W):
 RNN_SIZES = {"lstm": (512, 512), "gru": (512, 256)}     # model_bu.py (bench default) / model.py
 
 
-def cpu_baseline(sample, warmup=1, steps=2, cell="lstm"):
+def cpu_baseline(sample, warmup=3, steps=6, cell="lstm"):
     """BASELINE.md CPU-baseline plan: the reference graph's train step (conv ->
     BiLSTM 512/512 -> CTC -> TF1 Adam) as the PyTorch-CPU restatement
     (oracle/torch_ref.py, checked against the NumPy oracle in
     tests/test_oracle.py; TensorFlow 1.x is unavailable), with every host
     thread this process may use, on `sample` synthetic 32x256 crops -- by
-    default the GPU step's own shape (B = 256), 1 warm-up + 2 timed steps
-    (~15 s of host time, bounded so the default run stays within minutes)."""
+    default the GPU step's own shape (B = 256), 3 warm-up + 6 timed steps
+    (~30 s of host time, bounded so the default run stays within minutes); the
+    per-step times' spread is reported beside the mean rate."""
     from oracle import ref_model as M
     from oracle.torch_ref import TorchRef
     threads, model = host_cpu()
@@ -150,15 +151,20 @@ def cpu_baseline(sample, warmup=1, steps=2, cell="lstm"):
         for _ in range(warmup):
             ref.train_step(img, lab, ln)
         print(f"# cpu baseline: {warmup} warm-up steps done", file=sys.stderr, flush=True)
-        t0 = time.perf_counter()
+        per = []
         for i in range(steps):
+            t0 = time.perf_counter()
             ref.train_step(img, lab, ln)
+            per.append(time.perf_counter() - t0)
             print(f"# cpu baseline: step {i + 1}/{steps}", file=sys.stderr, flush=True)
-        dt = time.perf_counter() - t0
+        dt = sum(per)
     finally:
         torch.set_num_threads(prev)
+    rates = sorted(sample / t for t in per)
     return {"value": round(sample * steps / dt, 3), "unit": "line-crops/sec", "cores": threads, "kind": "port",
-            "cpu": model,
+            "cpu": model, "per_step_s": [round(t, 3) for t in per],
+            "spread": {"min": round(rates[0], 3), "median": round(float(np.median(rates)), 3),
+                       "max": round(rates[-1], 3), "cv": round(float(np.std(per) / np.mean(per)), 4)},
             "sample": f"reference graph on CPU (PyTorch restatement oracle/torch_ref.py; TF1 unavailable): "
                       f"{warmup} warm-up + {steps} timed train steps (fp32, {cell.upper()} {sizes[0]}/{sizes[1]}, Adam) on {sample} "
                       f"synthetic 32x256 crops, {threads} threads, {dt:.1f} s"}
@@ -592,7 +598,7 @@ def main():
                          "Nth timed step (each probe event costs ~6 us of queue idle; 1 = every step)")
     ap.add_argument("--cpu-sample", type=int, default=256,
                     help="crops per CPU-baseline train step (default: the GPU step's B = 256)")
-    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline train steps (after 1 warm-up)")
+    ap.add_argument("--cpu-steps", type=int, default=6, help="timed CPU-baseline train steps (after 3 warm-up)")
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
                     help="c3: the headline train step (default); c2: B=64 fp32 fwd+CTC+greedy; "
                          "c5: bucketed 32x{64..512} crops, beam-16 decode")

@@ -523,26 +523,40 @@ class _BeamEntry:
 
 
 def _lse(a, b):
+    """[TF1] ctc_loss_util.h LogSumExp: the smaller added to the larger (in the
+    operands' own precision: float64, or float32 as TF computes it)."""
     if a == -np.inf:
         return b
     if b == -np.inf:
         return a
-    m = max(a, b)
-    return m + np.log1p(np.exp(-abs(a - b)))
+    return a + np.log1p(np.exp(b - a)) if a > b else b + np.log1p(np.exp(a - b))
 
 
-def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True, blank=None):
+def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True, blank=None, margins=None,
+                           dtype=np.float64):
     """One sequence of [TF1] CTCBeamSearchDecoder with the default scorer
     (test.py:84-88 beam 128; client.py:227-231 merge_repeated=False).
     logits [T, C] (already cut to seq_len). Each frame is normalised to
     log-softmax (row max subtracted, then the log-sum-exp), as SURVEY a11
     states for the TF1 decoder's input; leaves are a bounded top-N by
     newp.total with strict '>' against the bottom; ties keep the earlier
-    insertion. Returns (paths, log_probs)."""
+    insertion. Returns (paths, log_probs). dtype: the arithmetic -- float64
+    (exact-as-possible) or float32 (TF1's own: BeamProbability and LogSumExp
+    are float).
+
+    margins: a list that receives every NONZERO decision margin of the search
+    (test infrastructure): a branch's oldp.total against the bottom when it is
+    gated, an offered child's total against the bottom, and the gaps between
+    consecutive leaves at each step's end (their order is the next step's
+    processing order). Exact ties (ReLU-zero logits give many) are decided by
+    insertion order identically in any precision; a search whose smallest
+    nonzero margin is below float32's resolution may legitimately take
+    another branch in a float32 implementation (TF's, the GPU kernel's)."""
     T, C = logits.shape
     blank = C - 1 if blank is None else blank
+    ninf = dtype(-np.inf)
     root = _BeamEntry(None, -1)
-    root.newp = [0.0, 0.0, -np.inf]
+    root.newp = [dtype(0.0), dtype(0.0), ninf]
     leaves = [root]                        # kept sorted by newp.total desc (stable)
 
     def bottom():
@@ -557,9 +571,9 @@ def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True,
             leaves.pop()
 
     for t in range(T):
-        x = logits[t].astype(np.float64)
+        x = logits[t].astype(dtype)
         x = x - x.max()
-        x = x - np.log(np.exp(x).sum())
+        x = x - np.log(np.exp(x).sum(dtype=dtype))
         branches = list(leaves)            # Extract(): descending newp.total
         leaves = []
         for b in branches:
@@ -575,6 +589,10 @@ def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True,
             push(b)
 
         def is_candidate(p):
+            if margins is not None and p[0] > -np.inf and len(leaves) >= beam_width:
+                m = abs(p[0] - bottom().newp[0])
+                if m > 0:
+                    margins.append(m)
             return p[0] > -np.inf and (len(leaves) < beam_width or p[0] > bottom().newp[0])
 
         for b in branches:
@@ -585,29 +603,42 @@ def ctc_beam_search_single(logits, beam_width, top_paths=1, merge_repeated=True,
             for c in b.children:
                 if c.active():
                     continue
-                c.newp[1] = -np.inf
+                c.newp[1] = ninf
                 prev = b.oldp[1] if c.label == b.label else b.oldp[0]
                 c.newp[2] = x[c.label] + prev
                 c.newp[0] = c.newp[2]
                 if is_candidate(c.newp):
                     if len(leaves) == beam_width:
-                        bottom().newp = [-np.inf, -np.inf, -np.inf]
+                        bottom().newp = [ninf, ninf, ninf]
                     push(c)
                 else:
-                    c.oldp = [-np.inf, -np.inf, -np.inf]
-                    c.newp = [-np.inf, -np.inf, -np.inf]
+                    c.oldp = [ninf, ninf, ninf]
+                    c.newp = [ninf, ninf, ninf]
+        if margins is not None:
+            margins += [m for m in (a.newp[0] - b.newp[0] for a, b in zip(leaves, leaves[1:])) if m > 0]
     top = leaves[:top_paths]
     return [e.label_seq(merge_repeated) for e in top], [e.newp[0] for e in top]
 
 
-def ctc_beam_search_decode(logits, seq_len, beam_width=100, top_paths=1, merge_repeated=True):
+def ctc_beam_search_min_margin(logits, seq_len, beam_width, merge_repeated=True, dtype=np.float64):
+    """Smallest nonzero decision margin (log-prob units) of the search over one
+    sequence (logits [T, 1, C] or [T, C]); +inf when every decision is exact."""
+    lg = logits[:, 0] if logits.ndim == 3 else logits
+    margins = []
+    ctc_beam_search_single(lg[:int(np.asarray(seq_len).reshape(-1)[0])], beam_width, 1, merge_repeated,
+                           margins=margins, dtype=dtype)
+    return float(min(margins)) if margins else np.inf
+
+
+def ctc_beam_search_decode(logits, seq_len, beam_width=100, top_paths=1, merge_repeated=True, dtype=np.float64):
     """Batched tf.nn.ctc_beam_search_decoder: per path k a list of B label
     sequences, and log_probabilities [B, top_paths]."""
     T, B, C = logits.shape
     paths = [[None] * B for _ in range(top_paths)]
     logp = np.full((B, top_paths), -np.inf)
     for b in range(B):
-        ps, lps = ctc_beam_search_single(logits[:int(seq_len[b]), b], beam_width, top_paths, merge_repeated)
+        ps, lps = ctc_beam_search_single(logits[:int(seq_len[b]), b], beam_width, top_paths, merge_repeated,
+                                         dtype=dtype)
         for k in range(top_paths):
             paths[k][b] = ps[k] if k < len(ps) else []
             logp[b, k] = lps[k] if k < len(lps) else -np.inf

@@ -53,3 +53,31 @@ def ocrk_opts():
     o = _Opts()
     yield o
     o.restore()
+
+
+@pytest.fixture(scope="session")
+def trained_fp32(cuda):
+    """The LSTM 512/512 model trained in fp32 on the reference's data/val shard
+    (tests/trained_model.py REGIME), once per session: shared by the trained-weight
+    parity tests (test_gpu_trained*.py). Returns dict(store, losses, curves, state)."""
+    import torch
+    import trained_model as TM
+    batches = TM.shard_batches(TM.TRAIN_SHARD)
+    dev = TM.to_device(batches, cuda, torch.float32)
+    from cnn_lstm_ctc_ocr_amd import model
+    store, losses, curves = TM.train_on_shard(
+        torch.float32, batches, cuda, evals={"infer": lambda s: TM.shard_cer(s, dev),
+                                             "train_mode": lambda s: TM.shard_cer(s, dev, model.TRAIN)})
+    return {"store": store, "losses": losses, "curves": curves, "state": store.state_dict(), "batches": batches}
+
+
+@pytest.fixture(scope="session")
+def trained_bf16(cuda, trained_fp32):
+    """The same run in bf16 (the benched precision)."""
+    import torch
+    import trained_model as TM
+    batches = trained_fp32["batches"]
+    dev = TM.to_device(batches, cuda, torch.bfloat16)
+    store, losses, curves = TM.train_on_shard(torch.bfloat16, batches, cuda,
+                                              evals={"infer": lambda s: TM.shard_cer(s, dev)})
+    return {"store": store, "losses": losses, "curves": curves}

@@ -150,8 +150,12 @@ def test_bn_bwd_pooled_ill_conditioned_channels(cuda, case, dtype):
         outs.append((dz.double().cpu().numpy().reshape(-1, C), dg.double().cpu().numpy(), db.double().cpu().numpy()))
     (zr, gr, br), (zp, gp, bp) = outs
     per = np.linalg.norm(zp - zr, axis=0) / np.maximum(np.linalg.norm(zr, axis=0), 1e-30)
-    assert per[ill].max() < 1e-4, per[ill]             # the z form's terms, another summation order
-    assert per[~ill].max() < (4e-3 if dtype == torch.bfloat16 else 1e-5), per[~ill]
+    # the z form's own terms (another summation order; for the overlapping 2x2/[2,1] pool the
+    # z form stages da in bf16 for its streaming apply, 2^-9 per routed sum -- hence bf16's 4e-3);
+    # the (p - beta) / gamma recovery would be off by ~|beta| / |gamma| * 2^-9 = 10-200 % here
+    tol = 4e-3 if dtype == torch.bfloat16 else 1e-5
+    assert per[ill].max() < tol, per[ill]
+    assert per[~ill].max() < tol, per[~ill]
     np.testing.assert_allclose(gp, gr, rtol=1e-5, atol=1e-5 * np.abs(gr).max())
     np.testing.assert_allclose(bp, br, rtol=1e-5, atol=1e-5 * np.abs(br).max())
 
