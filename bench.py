@@ -270,6 +270,64 @@ def cer_vs_ref(device):
     return res
 
 
+def cer_vs_ref_trained(device):
+    """"CER vs ref" at TRAINED weights, outside the timed
+    region: the LSTM 512/512 model trained in fp32 on the reference's data/val
+    shard (tests/trained_model.py REGIME: 4,000 Trainer.steps, ~20 s), then every
+    crop of the held-out data/test shard (892) through server.Bucket's 32-px uint8
+    buckets, greedy and beam-16. The reference strings are the fp32 HIP path's --
+    equal to the float64 reference graph's on all 932 served rows at these
+    weights but one beam near-tie (tests/test_gpu_trained_serving.py,
+    profiles/r6d_trained.json); the benched precision (bf16, the same weights)
+    is scored against them: CER = sum(edit distance) / sum(len(reference
+    string)) (test.py:90-99). Plus the fp32 model's greedy CER against the shard's
+    own labels (generalisation from 800 training crops: context, not parity)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import trained_model as TM
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, decode, model
+    t0 = time.perf_counter()
+    store, _losses, _c = TM.train_on_shard(torch.float32, TM.shard_batches(TM.TRAIN_SHARD), device)
+    train_s = time.perf_counter() - t0
+    print(f"# trained CER: fp32 model trained in {train_s:.1f} s", file=sys.stderr, flush=True)
+    bf = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.bfloat16), device=device,
+                    values=store.state_dict())
+    tally = {k: [0, 0, 0] for k in ("greedy", "beam16")}      # sum edit, sum ref length, rows differing
+    truth = [0, 0]
+    rows = 0
+    for _name, batch, widths, labels in TM.bucketed(TM.rows32(TM.shard_items(TM.HELD_OUT_SHARD))):
+        x = torch.from_numpy(batch).to(device)
+        w = torch.from_numpy(widths).to(device)
+        out = {}
+        with torch.no_grad():
+            for tag, st in (("ref", store), ("bf16", bf)):
+                feats, seq = model.convnet_layers(x, w, model.INFER, st)
+                logits = model.rnn_layers(feats, seq, 95, st).float()
+                out[tag] = {"greedy": decode.ctc_greedy_decoder(logits, seq)[0][0],
+                            "beam16": decode.ctc_beam_search_decoder(logits, seq, beam_width=16)[0][0]}
+        for kind in tally:
+            ref, hyp = out["ref"][kind], out["bf16"][kind]
+            ref_len, hyp_len = (ref >= 0).sum(1).to(torch.int32), (hyp >= 0).sum(1).to(torch.int32)
+            d = decode.edit_distance(hyp, hyp_len, ref.to(torch.int32), ref_len).cpu().numpy()
+            tally[kind][0] += float(d.sum())
+            tally[kind][1] += int(ref_len.sum().item())
+            tally[kind][2] += int((d > 0).sum())
+        lab, ln = model.dense_labels(labels, len(labels), device)
+        g = out["ref"]["greedy"]
+        d = decode.edit_distance(g, (g >= 0).sum(1).to(torch.int32), lab, ln).cpu().numpy()
+        truth[0] += float(d.sum())
+        truth[1] += int(ln.sum().item())
+        rows += len(labels)
+    res = {"data": f"tests/golden/mjsynth_test_words000.npz (data/test shard, {rows} crops, server buckets, uint8); "
+                   "weights: fp32 training on data/val (tests/trained_model.py REGIME, "
+                   f"{TM.REGIME['steps']} steps, {train_s:.0f} s)",
+           "reference": "the fp32 HIP path's strings (= the float64 graph's on all 932 served rows but one beam "
+                        "near-tie: tests/test_gpu_trained_serving.py)",
+           "fp32_greedy_cer_vs_labels": round(truth[0] / max(truth[1], 1), 4)}
+    for kind, (e, n, diff) in tally.items():
+        res[f"bf16_{kind}"] = {"cer": round(e / max(n, 1), 5), "rows_differing": diff, "rows": rows}
+    return res
+
+
 def run_c2(args, world, rank, device):
     """BASELINE configs[1] (C2): B=64 synthetic 32x256 crops, INFER forward +
     CTC loss + greedy decode, fp32 (test.py:75-104's evaluation graph with the
@@ -610,6 +668,8 @@ def main():
                     help="C3 with N > 1: BatchNorm statistics over all ranks' batches (Trainer(sync_bn=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
+    ap.add_argument("--no-trained-cer", action="store_true",
+                    help="skip the trained-weight CER leg (~25 s: trains the model on data/val first)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_conv.json"),
                     help="PMC summary (tools/pmc_traffic.py) for roofline.traffic of the conv roofline kernel")
     ap.add_argument("--selftest", action="store_true",
@@ -827,6 +887,8 @@ def main():
                                                   f"({str(pmc.get('libocrk_sha256'))[:12]} vs {lib_sha[:12]}): not reported")
     if rank == 0 and not args.no_cer and args.cell == "lstm":      # the golden decodes are of the LSTM model
         result["cer_vs_ref"] = cer_vs_ref(device)
+        if world == 1 and not args.no_trained_cer:
+            result["cer_vs_ref_trained"] = cer_vs_ref_trained(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, steps=args.cpu_steps, cell=args.cell)
         if args.cell == "lstm":

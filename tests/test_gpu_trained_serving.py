@@ -55,46 +55,6 @@ def _ref(state):
     return TorchRef({k: v.astype(np.float64) for k, v in state.items()}, (512, 512), torch.float64)
 
 
-def _bucketed(items, bs=64):
-    """server.Bucket batches (uint8 [n, 32, hi, 1] zero-padded to the bucket's upper
-    width, server.py:29-34) of (32-row) crops, with their labels."""
-    from cnn_lstm_ctc_ocr_amd.server import BUCKET_STEP, Bucket
-    by = {}
-    for it in items:
-        hi = -(-it["width"] // BUCKET_STEP) * BUCKET_STEP
-        by.setdefault(hi, []).append(it)
-    out = []
-    for hi, its in sorted(by.items()):
-        bucket = Bucket(0.0, bs, (hi - BUCKET_STEP, hi))
-        lab = {}
-        for it in its:
-            assert bucket.addImgToBucket("c", it["filename"], 0.0, it["u8"])
-            lab[it["filename"]] = it["labels"]
-        now = 1e9
-        while True:
-            # getBatch resets the bucket's oldest time to `now` (server.py:52): a later clock
-            # releases the remainder
-            now += 1.0
-            got = bucket.getBatch(now=now)
-            if got is None:
-                break
-            infos, batch, widths = got
-            out.append((f"b{hi}", batch, widths, [lab[i] for _c, i in infos]))
-    return out
-
-
-def _rows32(items):
-    """Crops as served: 32 rows (a shorter crop zero-padded below, as the bucket pads
-    on the right)."""
-    out = []
-    for it in items:
-        h, w = it["u8"].shape[:2]
-        full = np.zeros((32, w, 1), np.uint8)
-        full[:h] = it["u8"]
-        out.append(dict(it, u8=full))
-    return out
-
-
 def _lines(items, n=40, seed=11):
     """n synthetic text lines: 2-4 held-out words side by side (16-px gaps), total
     width in (512, 992] -- the server's widest buckets."""
@@ -118,7 +78,7 @@ def _lines(items, n=40, seed=11):
 
 @pytest.fixture(scope="module")
 def held_out_items():
-    return _rows32(TM.shard_items(TM.HELD_OUT_SHARD))
+    return TM.rows32(TM.shard_items(TM.HELD_OUT_SHARD))
 
 
 @pytest.fixture(scope="module")
@@ -128,8 +88,8 @@ def served(cuda, trained_fp32, held_out_items):
     from cnn_lstm_ctc_ocr_amd import model
     store, ref = _store(cuda, trained_fp32["state"]), _ref(trained_fp32["state"])
     out = []
-    cases = [("held",) + c for c in _bucketed(held_out_items)]
-    cases += [("line",) + c for c in _bucketed(_lines(held_out_items), bs=16)]
+    cases = [("held",) + c for c in TM.bucketed(held_out_items)]
+    cases += [("line",) + c for c in TM.bucketed(_lines(held_out_items), bs=16)]
     for kind, name, batch, widths, labels in cases:
         name = f"{kind}_{name}"
         with torch.no_grad():

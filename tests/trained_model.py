@@ -238,3 +238,43 @@ def compare_rows(rows, beam_width=16, gap=1e-3, procs=16, refs=None):
             out["beam_edits_vs_ref"] += edit(r["beam"], p_ref)
             out["ref_beam_len"] += len(p_ref)
     return out
+
+
+def bucketed(items, bs=64):
+    """server.Bucket batches (uint8 [n, 32, hi, 1] zero-padded to the bucket's upper
+    width, server.py:29-34) of (32-row) crops, with their labels."""
+    from cnn_lstm_ctc_ocr_amd.server import BUCKET_STEP, Bucket
+    by = {}
+    for it in items:
+        hi = -(-it["width"] // BUCKET_STEP) * BUCKET_STEP
+        by.setdefault(hi, []).append(it)
+    out = []
+    for hi, its in sorted(by.items()):
+        bucket = Bucket(0.0, bs, (hi - BUCKET_STEP, hi))
+        lab = {}
+        for it in its:
+            assert bucket.addImgToBucket("c", it["filename"], 0.0, it["u8"])
+            lab[it["filename"]] = it["labels"]
+        now = 1e9
+        while True:
+            # getBatch resets the bucket's oldest time to `now` (server.py:52): a later clock
+            # releases the remainder
+            now += 1.0
+            got = bucket.getBatch(now=now)
+            if got is None:
+                break
+            infos, batch, widths = got
+            out.append((f"b{hi}", batch, widths, [lab[i] for _c, i in infos]))
+    return out
+
+
+def rows32(items):
+    """Crops as served: 32 rows (a shorter crop zero-padded below, as the bucket pads
+    on the right)."""
+    out = []
+    for it in items:
+        h, w = it["u8"].shape[:2]
+        full = np.zeros((32, w, 1), np.uint8)
+        full[:h] = it["u8"]
+        out.append(dict(it, u8=full))
+    return out
