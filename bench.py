@@ -666,6 +666,8 @@ def main():
                     help="lstm: model_bu.py's BiLSTM 512/512 (BASELINE.json's config); gru: model.py's BiGRU 512/256")
     ap.add_argument("--sync-bn", action="store_true",
                     help="C3 with N > 1: BatchNorm statistics over all ranks' batches (Trainer(sync_bn=True))")
+    ap.add_argument("--main-stream", choices=("default", "own"), default="default",
+                    help="run the train step on torch's default (NULL) stream or on a non-blocking stream of its own")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cer", action="store_true", help="skip the CER-vs-oracle decode check (outside the timing)")
     ap.add_argument("--no-trained-cer", action="store_true",
@@ -756,6 +758,17 @@ def main():
         run_step = graphed.step
     else:
         run_step = lambda: trainer.step(img, widths, labels)  # noqa: E731
+    if args.main_stream == "own":
+        # the step on a non-blocking stream of its own instead of the legacy NULL stream:
+        # a stream created without hipStreamNonBlocking (a CU-masked one, hipExtStreamCreateWithCUMask)
+        # synchronises with the NULL stream, so the step's side work would serialise behind it
+        own = torch.cuda.Stream(device)
+        own.wait_stream(torch.cuda.current_stream(device))
+        step_on_default = run_step
+
+        def run_step():
+            with torch.cuda.stream(own):
+                return step_on_default()
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()

@@ -96,6 +96,7 @@ enum Option : int {
     OPT_LSTM_DMA,             // 1 (default): LDS-DMA staging in the per-step LSTM forward kernels
     OPT_LSTM_BWD_DMA,         // 1 (default): LDS-DMA staging in the per-step LSTM backward kernels
     OPT_LSTM_FWD_R16,         // 1 (default): 16-row / 64-unit members for the bf16 forward loop at H = 512
+    OPT_NT_TAP_UNIFORM,       // 1 (default): the NT ring's tap-uniform im2col addressing where C % BK == 0
     OPT_COUNT
 };
 int64_t opt(Option o);

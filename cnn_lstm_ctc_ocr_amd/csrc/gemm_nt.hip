@@ -40,8 +40,14 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // EXACT (with F32): exact fp32 products on v_mfma_f32_16x16x4_f32 instead of the split --
 // the fp32 Trainer's conv tower (kernels.f32_exact); lane group g supplies k = 8g + e to
 // the e-th of 8 MFMAs per 32-deep step (any k order sums the same products).
+// TU (tap-uniform im2col, C % BK == 0 and every K slice a multiple of BK): a k-tile of
+// BK channels never crosses a 3x3 tap, so the tap, its (dh, dw) shift and the channel
+// offset are wave-uniform per k-step -- carried as scalars from one k-step to the next
+// instead of a per-lane k / C division -- and each A row's border test is one bit of a
+// 9-bit valid-tap mask built in the prologue (the generic path spent ~85 VALU per
+// 32 MFMAs on this address arithmetic; profiles/r6_nt_sq.txt).
 template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false,
-          bool X6 = false>
+          bool X6 = false, bool TU = false>
 __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     // 8-wave tiles hold 128 accumulators per lane: no BN-statistics epilogue
     // (its second pass over the accumulators would spill); launch_nt routes
@@ -116,7 +122,59 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
         boff[i] = n < p.N ? (unsigned)((int64_t)n * p.ldb * ESZ) : NT_BADROW;
     }
 
+    // TU: valid-tap masks of this lane's A rows (bit t: tap t = 3 kh + kw keeps the
+    // shifted pixel inside the image) and the k-step's tap / channel offset as scalars
+    unsigned tmask[NA];
+    int tu_tap = 0, tu_cc = 0;
+    if constexpr (TU) {
+        static_assert(AM != A_ROWK, "TU is the im2col form");
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            tmask[i] = 0;
+            if (aoff[i] == NT_BADROW) continue;
+            const int h = (int)(ahw[i] >> 16), w = (int)(ahw[i] & 0xffff);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int kh = t / 3, kw = t % 3;
+                const int dh = AM == A_IM2COL_FLIP ? 1 - kh : kh - 1, dw = AM == A_IM2COL_FLIP ? 1 - kw : kw - 1;
+                const int hh = h + dh, ww = w + dw;
+                if (hh >= 0 && hh < p.convH && ww >= 0 && ww < p.convW) tmask[i] |= 1u << t;
+            }
+        }
+        tu_tap = __builtin_amdgcn_readfirstlane(kbeg / p.convC);
+        tu_cc = __builtin_amdgcn_readfirstlane(kbeg - tu_tap * p.convC);
+    }
+    const unsigned lane_koff = (unsigned)(EPC * chunk * ESZ);
+
+    // TU: k-steps are issued in order (kt = 0, 1, 2, ...), each advancing the tap state by BK
+    auto issue_tu = [&](int kt, int stage) {
+        const int kg = kbeg + kt * BK;                    // wave-uniform
+        const bool kok = kg < kend;
+        char* sa = smem + stage * STAGE;
+        char* sb = sa + A_BYTES;
+        const int kh = tu_tap / 3, kw = tu_tap - 3 * (tu_tap / 3);
+        const int dh = AM == A_IM2COL_FLIP ? 1 - kh : kh - 1, dw = AM == A_IM2COL_FLIP ? 1 - kw : kw - 1;
+        const unsigned toff = (unsigned)(((dh * p.convW + dw) * p.convC + tu_cc) * ESZ) + lane_koff;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const bool ok = kok && ((tmask[i] >> tu_tap) & 1u);
+            lds_dma16(ra, sa + ((i * NW + wave) * RPI) * ROWB, ok ? aoff[i] + toff : NT_OOB);
+        }
+        const unsigned kb = (unsigned)(kg * ESZ) + lane_koff;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const bool ok = kok && boff[i] != NT_BADROW;
+            lds_dma16(rb, sb + (((i * NW + wave) % BBLK) * RPI) * ROWB, ok ? boff[i] + kb : NT_OOB);
+        }
+        tu_cc += BK;
+        if (tu_cc >= p.convC) { tu_cc = 0; ++tu_tap; }
+    };
+
     auto issue = [&](int kt, int stage) {
+        if constexpr (TU) {
+            issue_tu(kt, stage);
+            return;
+        }
         const int k = kbeg + kt * BK + EPC * chunk;
         const bool kok = k < kend;
         char* sa = smem + stage * STAGE;
@@ -462,19 +520,36 @@ __global__ void __launch_bounds__(NW * 64) gemm_nt_kernel(const GemmParams p) {
     }
 }
 
+template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW, bool F32, bool EXACT, bool X6, bool TU>
+int launch_nt_k(const GemmParams& p, hipStream_t stream) {
+    constexpr int LDS = S * (BM + BN) * BK * (F32 ? 4 : 2);
+    static DeviceOnce configured;
+    set_dyn_lds(configured,
+                reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6, TU>),
+                LDS);
+    dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
+    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6, TU><<<grid, NW * 64, LDS, stream>>>(p);
+    return launch_status("gemm_nt");
+}
+
+// the tap-uniform im2col form where it applies (option NT_TAP_UNIFORM, default on)
+template <int BK, int AM>
+bool nt_tap_uniform(const GemmParams& p) {
+    return AM != A_ROWK && opt(OPT_NT_TAP_UNIFORM) != 0 && p.convC % BK == 0 &&
+           (p.splits == 1 || p.k_chunk % BK == 0);
+}
+
 template <int BM, int BN, int BK, int S, int WAVES_M, int AM, int NW = 4, bool F32 = false, bool EXACT = false,
           bool X6 = false>
 int launch_nt(const GemmParams& p, hipStream_t stream) {
     if constexpr (NW == 8 && !F32) {
         if (p.stats) return launch_nt<128, 128, 64, 2, 2, AM, 4>(p, stream);
     }
-    constexpr int LDS = S * (BM + BN) * BK * (F32 ? 4 : 2);
-    static DeviceOnce configured;
-    set_dyn_lds(configured,
-                reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6>), LDS);
-    dim3 grid(xcd_grid((int)cdiv(p.M, BM), (int)cdiv(p.N, BN)), 1u, (unsigned)(p.batch * p.splits));
-    gemm_nt_kernel<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6><<<grid, NW * 64, LDS, stream>>>(p);
-    return launch_status("gemm_nt");
+    if constexpr (AM != A_ROWK) {
+        if (nt_tap_uniform<BK, AM>(p))
+            return launch_nt_k<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6, true>(p, stream);
+    }
+    return launch_nt_k<BM, BN, BK, S, WAVES_M, AM, NW, F32, EXACT, X6, false>(p, stream);
 }
 
 // fp32 operands (BK = 32: 128-B fp32 rows) on the bf16x3 split, or with EXACT products

@@ -41,7 +41,7 @@ constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"CONV_TN_ITEMS", 192},
     {"CONV_TN4_ITEMS", 512}, {"CONV_WGRAD_CUS", 192}, {"F32_MFMA", 0}, {"GEMM_NT", 1}, {"GEMM_NT_STAGED", 1},
     {"GEMM_PP", 1}, {"GEMM_PPTN", 1}, {"PP_MIN_N", 512}, {"GEMM_TN", 1}, {"LSTM_DMA", 1}, {"LSTM_BWD_DMA", 1},
-    {"LSTM_FWD_R16", 1},
+    {"LSTM_FWD_R16", 1}, {"NT_TAP_UNIFORM", 1},
 };
 std::atomic<int64_t> g_opts[OPT_COUNT];
 std::once_flag g_opts_once;

@@ -47,7 +47,7 @@ KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOC
                   "PP_PERSIST_NK", "PP_DEEP", "NT_F32_EXACT", "NT_F32_MASK",
                   "NT_F32_X6", "BEAM_WAVE", "BN_BWD_BLOCKS", "BN_ROUTE", "BN_ROUTE_SEG", "BN_ROUTE_NCH", "CONV_TN_ITEMS", "CONV_TN4_ITEMS",
                   "CONV_WGRAD_CUS", "F32_MFMA", "GEMM_NT", "GEMM_NT_STAGED", "GEMM_PP", "GEMM_PPTN", "PP_MIN_N", "GEMM_TN",
-                  "LSTM_DMA", "LSTM_BWD_DMA", "LSTM_FWD_R16")
+                  "LSTM_DMA", "LSTM_BWD_DMA", "LSTM_FWD_R16", "NT_TAP_UNIFORM")
 
 
 def _env_int(name, default):

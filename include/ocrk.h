@@ -93,7 +93,8 @@ const char* ocrk_last_error(void);
  * NT_F32_MASK, NT_F32_X6, BEAM_WAVE, BN_BWD_BLOCKS, BN_ROUTE, BN_ROUTE_SEG,
  * BN_ROUTE_NCH, CONV_TN_ITEMS, CONV_TN4_ITEMS,
  * CONV_WGRAD_CUS, F32_MFMA, GEMM_NT, GEMM_NT_STAGED, GEMM_PP, GEMM_PPTN, PP_MIN_N, GEMM_TN, LSTM_DMA,
- * LSTM_BWD_DMA, LSTM_FWD_R16 (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG. `prev` may be NULL. */
+ * LSTM_BWD_DMA, LSTM_FWD_R16, NT_TAP_UNIFORM (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG.
+ * `prev` may be NULL. */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
 
 /* A stream on the current device whose kernels run on only n_cus of its CUs
