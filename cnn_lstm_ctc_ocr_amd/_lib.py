@@ -60,8 +60,6 @@ SIGNATURES = {
                                         _p],
     "ocrk_conv12_fwd_supported": [_i32, _i32, _i32, _i32],
     "ocrk_conv12_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p],
-    "ocrk_conv2_bwd_weight_c1x_supported": [_i32, _i32, _i32, _i32],
-    "ocrk_conv2_bwd_weight_c1x": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv1_fwd_relu_bits": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i32, _p],
     "ocrk_conv_stats_tiles": [_i64],
     "ocrk_conv3x3_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p, _i32, _p],
@@ -100,9 +98,6 @@ SIGNATURES = {
                                    _i32, _p, _p, _p, _i32, _p, _p, _sz, _i32, _p],
     "ocrk_lstm_fwd_step": [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
     "ocrk_lstm_bwd_step": [_p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p],
-    "ocrk_stream_wait": [_p, _p, _i32],
-    "ocrk_stream_create_cu_limited": [_i32, _p],
-    "ocrk_stream_destroy": [_p],
     "ocrk_copy_batch": [_p, _i32, _i64, _p],
     "ocrk_gru_fwd_persistent_supported": [_i32, _i32],
     "ocrk_gru_fwd_persistent_workspace_size": [_i32, _i32],
@@ -113,8 +108,6 @@ SIGNATURES = {
     "ocrk_persistent_flags_size": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_supported": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_workspace_size": [_i32, _i32],
-    "ocrk_lstm_fwd_persistent_x_supported": [_i32, _i32, _i32],
-    "ocrk_lstm_fwd_persistent_x": [_p, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_fwd_persistent": [_p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
     "ocrk_lstm_fwd_persistent_f32_supported": [_i32, _i32],
     "ocrk_lstm_fwd_persistent_f32_workspace_size": [_i32, _i32],
@@ -217,7 +210,17 @@ def raise_for_status(word):
 
 
 # include/ocrk_debug.h (exported only by tools/libocrk_exp.so, `make exp`)
-DEBUG_SIGNATURES = {"ocrk_lstm_debug_stamps": [_p]}
+DEBUG_SIGNATURES = {
+    "ocrk_lstm_debug_stamps": [_p],
+    # routes measured slower and kept out of the product library (round 6)
+    "ocrk_conv2_bwd_weight_c1x_supported": [_i32, _i32, _i32, _i32],
+    "ocrk_conv2_bwd_weight_c1x": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
+    "ocrk_stream_wait": [_p, _p, _i32],
+    "ocrk_stream_create_cu_limited": [_i32, _p],
+    "ocrk_stream_destroy": [_p],
+    "ocrk_lstm_fwd_persistent_x_supported": [_i32, _i32, _i32],
+    "ocrk_lstm_fwd_persistent_x": [_p, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _sz, _p],
+}
 
 _lib = None
 

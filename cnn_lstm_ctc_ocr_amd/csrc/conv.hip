@@ -351,8 +351,8 @@ int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, c
 // [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32]; outputs y1 [B,IH-2,IW-2,32]
 // bf16 (conv1's ReLU output), relu_bits u8 [B,IH-2,IW-2][4] (its bit mask), z (conv2's
 // pre-BN output, same shape) and stats [B*(IH-2)][2][32] (conv2's per-row BN partials,
-// ocrk_bn_finalize_tiles with tile_rows = IW-2). y1 may be NULL: not written (the backward
-// then recomputes it, ocrk_conv2_bwd_weight_c1x).
+// ocrk_bn_finalize_tiles with tile_rows = IW-2). y1 may be NULL: not written (the tools
+// build's ocrk_conv2_bwd_weight_c1x recomputes it).
 extern "C" int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype) {
     return dtype == OCRK_BF16 && IH >= 3 && IW >= 3 && ocrk::conv12_fwd_covers(B, IH - 2, IW - 2) ? 1 : 0;
 }
@@ -367,6 +367,8 @@ extern "C" int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW
                             ocrk::as_stream(stream));
 }
 
+#ifdef OCRK_EXPERIMENTS
+// (tools build, include/ocrk_debug.h: measured +55 us in the step, it lands on the tail)
 // conv2's weight gradient with its input y1 = relu(conv1(x)) recomputed per row from the
 // image instead of read (bf16): dw [3][3][32][32] f32 (+)= sum y1 (x) dz over the batch,
 // y1 bit-identical to ocrk_conv12_fwd's. x, w1, b1 as ocrk_conv12_fwd; dz [B,IH-2,IW-2,32]
@@ -386,6 +388,7 @@ extern "C" int ocrk_conv2_bwd_weight_c1x(const void* x, int x_is_u8, int B, int 
     OCRK_REQUIRE(st >= 0, "ocrk_conv2_bwd_weight_c1x: workspace too small or path disabled");
     return st;
 }
+#endif  // OCRK_EXPERIMENTS
 
 // conv2's backward-data and conv1's weight gradient as one pass (bf16): the data
 // gradient dy1 = relu'(y1) . conv2^T(dz2) is contracted against conv1's input as

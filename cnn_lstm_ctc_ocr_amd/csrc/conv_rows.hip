@@ -1730,6 +1730,7 @@ int conv_rows_dgrad_bits(const void* dy, int B, int H, int W, int cout, const vo
     return launch_dgrad_co<64, 64, 128, 1, true>(dy, B, H, W, w_bwd, dx, bits, stats, s);
 }
 
+#ifdef OCRK_EXPERIMENTS
 // conv2's weight gradient with conv1's output recomputed from the image (no y1 tensor):
 // dw [3][3][32][32] (+)= sum y1 (x) dz, y1 = relu(conv1(img)) produced per row by
 // c1_make_row -- the bits conv12_fwd_rows_kernel made in the forward
@@ -1758,6 +1759,7 @@ int conv_rows_wgrad_c1x(const void* img, int x_is_u8, const float* w1, const flo
     p.splits = grid; p.splitk_ws = (float*)ws;
     return splitk_finish(p, s);
 }
+#endif  // OCRK_EXPERIMENTS
 
 bool conv12_fwd_covers(int B, int H, int W) {
     return rows_enabled() && B >= 1 && H >= 1 && W >= 1 && W <= RW_MAXW;

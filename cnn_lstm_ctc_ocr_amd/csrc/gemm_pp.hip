@@ -855,7 +855,11 @@ int launch_pp(const GemmParams& p, hipStream_t stream) {
         return launch_pp_k<AM, BN, false, true>(p, stream);
     }
     if (p.mask) return -1;
+#ifdef OCRK_EXPERIMENTS
+    // the deep-lead schedule (tools build: measured no gain, its wait fraction 0.404 vs 0.415,
+    // profiles/r6_pp_deep_counters.txt)
     if (AM == A_ROWK && !p.stats && opt(OPT_PP_DEEP)) return launch_pp_deep<BN>(p, stream);
+#endif
     if (p.stats) return launch_pp_k<AM, BN, true, false>(p, stream);
     return launch_pp_k<AM, BN, false, false>(p, stream);
 }

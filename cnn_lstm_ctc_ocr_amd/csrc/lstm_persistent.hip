@@ -1460,6 +1460,9 @@ extern "C" int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const i
     return ocrk::launch_status("ocrk_lstm_fwd_persistent");
 }
 
+#ifdef OCRK_EXPERIMENTS
+// (tools build, include/ocrk_debug.h: measured no gain -- every step 0.7 us longer,
+// profiles/r3_fused_projection.txt)
 // Fused first layer: x [T][B][n_in] (time-major features), wxT [2][4H][n_in] (per
 // direction W_x^T, gate-major rows), bias f32 [2][4H]; everything else as above.
 extern "C" int ocrk_lstm_fwd_persistent_x_supported(int B, int H, int n_in) {
@@ -1495,6 +1498,7 @@ extern "C" int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* w
         lstm_spin_limit(), g_lstm_dbg, (const bf16*)x, (const bf16*)wxT, bias);
     return ocrk::launch_status("ocrk_lstm_fwd_persistent_x");
 }
+#endif  // OCRK_EXPERIMENTS
 
 // ---------------------------------------------------------- backward C ABI
 // OCRK_LSTM_BWD_KSPLIT=1: the K-split form (read per launch). Off by default:
@@ -1538,11 +1542,16 @@ extern "C" int ocrk_lstm_bwd_persistent_supported(int B, int H) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+#ifdef OCRK_EXPERIMENTS
     hipError_t e = lstm_bwd_ksplit()
         ? (H == 512 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_ksplit_kernel<16, false>, 256, 0)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_ksplit_kernel<8, false>, 256, 0))
         : (H == 512 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<16>, 256, 0)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<8>, 256, 0));
+#else
+    hipError_t e = H == 512 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<16>, 256, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_persistent_kernel<8>, 256, 0);
+#endif
     if (e != hipSuccess) return 0;
     const long grid = 2L * (B / PBR) * (H / PHU);
     return grid <= (long)cus * per_cu ? 1 : 0;
@@ -1567,6 +1576,7 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
         return ocrk::launch_status("ocrk_lstm_bwd_persistent");
     }
     const unsigned grid = 2u * (unsigned)(B / PBR) * (unsigned)(H / PHU);
+#ifdef OCRK_EXPERIMENTS
     if (lstm_bwd_ksplit()) {
         const bool pb16 = opt(OPT_LSTM_BWD_PB16) == 1;            // partial products exchanged in bf16
 #define KSPLIT_LAUNCH(KSV, PB)                                                                                   \
@@ -1578,6 +1588,7 @@ extern "C" int ocrk_lstm_bwd_persistent(const void* wh, const int* seq_len, int 
 #undef KSPLIT_LAUNCH
         return ocrk::launch_status("ocrk_lstm_bwd_persistent");
     }
+#endif
     if (H == 512 && persist_late((int64_t)T * B * 8 * H * 2))
         lstm_bwd_persistent_kernel<16, true><<<grid, 256, 0, st>>>((const bf16*)wh, zx, seq_len, T, B, (const bf16*)dout, cprev_t,
                                                                    (const bf16*)acts_t, (bf16*)dG_t, cnt, err, lstm_spin_limit(), g_lstm_dbg,

@@ -32,11 +32,13 @@ namespace {
 struct OptDef {
     const char* name;
     int64_t def;
+    bool exp = false;       // measured-slower route: only the tools build (make exp) reads / sets it
 };
 constexpr OptDef kOptDefs[OPT_COUNT] = {
     {"CONV_DIRECT", 1}, {"CONV_ROWS", 1}, {"CONV_ROWS_WIDE", 1}, {"CONV_WGRAD_BLOCKS", 1},
-    {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0}, {"LSTM_BWD_PB16", 0},
-    {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1}, {"PP_PERSIST_NK", 8}, {"PP_DEEP", 0}, {"NT_F32_EXACT", 1}, {"NT_F32_MASK", 1},
+    {"LSTM_SPIN_LIMIT", 0}, {"PERSIST_LATE", 1}, {"LSTM_BWD_KSPLIT", 0, true}, {"LSTM_BWD_PB16", 0, true},
+    {"LSTM_BWD_R16", 1}, {"CTC_LDS", 1}, {"PP_PERSIST_NK", 8}, {"PP_DEEP", 0, true}, {"NT_F32_EXACT", 1},
+    {"NT_F32_MASK", 1},
     {"NT_F32_X6", 0}, {"BEAM_WAVE", 1}, {"BN_BWD_BLOCKS", 2048}, {"BN_ROUTE", 1}, {"BN_ROUTE_SEG", 8}, {"BN_ROUTE_NCH", 4},
     {"CONV_TN_ITEMS", 192},
     {"CONV_TN4_ITEMS", 512}, {"CONV_WGRAD_CUS", 192}, {"F32_MFMA", 0}, {"GEMM_NT", 1}, {"GEMM_NT_STAGED", 1},
@@ -46,8 +48,18 @@ constexpr OptDef kOptDefs[OPT_COUNT] = {
 std::atomic<int64_t> g_opts[OPT_COUNT];
 std::once_flag g_opts_once;
 
+#ifdef OCRK_EXPERIMENTS
+constexpr bool kExperiments = true;
+#else
+constexpr bool kExperiments = false;
+#endif
+
 void init_opts() {
     for (int i = 0; i < OPT_COUNT; ++i) {
+        if (kOptDefs[i].exp && !kExperiments) {          // the product library: the default, always
+            g_opts[i].store(kOptDefs[i].def, std::memory_order_relaxed);
+            continue;
+        }
         char env[64];
         snprintf(env, sizeof(env), "OCRK_%s", kOptDefs[i].name);
         const char* e = getenv(env);
@@ -59,7 +71,7 @@ int find_opt(const char* name) {
     if (!name) return -1;
     if (!strncmp(name, "OCRK_", 5)) name += 5;
     for (int i = 0; i < OPT_COUNT; ++i)
-        if (!strcmp(name, kOptDefs[i].name)) return i;
+        if (!strcmp(name, kOptDefs[i].name)) return kOptDefs[i].exp && !kExperiments ? -1 : i;
     return -1;
 }
 }  // namespace
@@ -131,6 +143,11 @@ int ocrk_timer_record(void* ev, void* stream) {
     return OCRK_OK;
 }
 
+#ifdef OCRK_EXPERIMENTS
+// include/ocrk_debug.h (tools build): fence-less stream forks and CU-masked streams.
+// Both measured no gain in the train step; a CU-masked stream is a
+// BLOCKING stream (hipExtStreamCreateWithCUMask takes no flags), so beside work on the
+// legacy NULL stream it serialises with it.
 int ocrk_stream_wait(void* waiter, void* signaller, int mode) {
     OCRK_REQUIRE(mode >= 0 && mode <= 2, "ocrk_stream_wait: mode %d", mode);
     constexpr int RING = 64, MAXDEV = 64;
@@ -196,6 +213,7 @@ int ocrk_stream_destroy(void* stream) {
     if (stream) (void)hipStreamDestroy(ocrk::as_stream(stream));
     return OCRK_OK;
 }
+#endif  // OCRK_EXPERIMENTS
 
 int ocrk_timer_elapsed(void* ev0, void* ev1, float* ms) {
     OCRK_REQUIRE(ev0 && ev1 && ms, "ocrk_timer_elapsed: null argument");

@@ -107,7 +107,8 @@ def conv12_fwd(x, w1, b1, w_nk2, b2, want_y1=True):
 
 def conv2_bwd_weight_c1x(x, w1, b1, dz, dw, accumulate=True):
     """conv2's weight gradient with y1 = relu(conv1(x)) recomputed from the image x [B,IH,IW]
-    (u8 or bf16) instead of read (ocrk_conv2_bwd_weight_c1x); dz [B,IH-2,IW-2,32] bf16."""
+    (u8 or bf16) instead of read (ocrk_conv2_bwd_weight_c1x); dz [B,IH-2,IW-2,32] bf16.
+    Tools build only (include/ocrk_debug.h): +55 us in the step, not the model's route."""
     _chk(x, w1, b1, dz, dw)
     B, IH, IW = x.shape[:3]
     nb = _lib.lib().ocrk_conv3x3_wgrad_workspace_size(B, IH - 2, IW - 2, 32, 32)
@@ -619,16 +620,15 @@ def lstm_fwd(gx, whT, seq_len, T, B, H, dtype, save=True):
     return out, hprev, cprev, acts
 
 
-def lstm_fused_x_ok(B, H, n_in, dtype, force=False):
-    """Run the first layer's input projection fused into the persistent forward
-    (ocrk_lstm_fwd_persistent_x)? Opt-in (OCRK_LSTM_FUSE_X=1, or force): measured
-    at B=256 it removes the 109 us projection GEMM but makes every step 0.7 us
-    longer (3.40 vs 2.68 us: the x.W_x MFMAs and the x-row DMA land on the
-    step's critical path), 480 vs 490 us for GEMM + loop alone and 5.865 vs
-    5.847 ms for the train step (profiles/r3_fused_projection.txt)."""
-    if not force and options.get("LSTM_FUSE_X") != 1:
-        return False
-    if not lstm_persistent_ok(B, H, dtype):
+def lstm_fused_x_ok(B, H, n_in, dtype):
+    """Can the tools build (include/ocrk_debug.h) run the first layer's input
+    projection fused into the persistent forward (ocrk_lstm_fwd_persistent_x)?
+    Never the model's route: measured at B=256 it removes the 109 us projection
+    GEMM but makes every step 0.7 us longer (3.40 vs 2.68 us: the x.W_x MFMAs and
+    the x-row DMA land on the step's critical path), 480 vs 490 us for GEMM +
+    loop alone and 5.865 vs 5.847 ms for the train step
+    (profiles/r3_fused_projection.txt)."""
+    if not lstm_persistent_ok(B, H, dtype) or not hasattr(_lib.lib(), "ocrk_lstm_fwd_persistent_x_supported"):
         return False
     return bool(_lib.lib().ocrk_lstm_fwd_persistent_x_supported(B, H, n_in))
 
@@ -802,22 +802,20 @@ def permute3(x, d0, d1, d2, dtype, out=None):
 
 def stream_wait(waiter, signaller, mode=1):
     """`waiter` (a torch.cuda.Stream) waits for the work issued so far on
-    `signaller` (ocrk_stream_wait: an event without the system-scope release)."""
+    `signaller` (ocrk_stream_wait: an event without the system-scope release).
+    Tools build only (include/ocrk_debug.h, OCRK_LIB=tools/libocrk_exp.so): the
+    fence-less forks measured box-dependent (-35 to +25 us per step)."""
     call("ocrk_stream_wait", ctypes.c_void_p(waiter.cuda_stream), ctypes.c_void_p(signaller.cuda_stream), int(mode))
-
-
-# cross-stream ordering inside a step (the side-stream forks and joins, the status
-# copy's fork): 0 default torch events, 1 / 2 ocrk_stream_wait's modes (OCRK_FORK_EVENTS).
-# Box-dependent: mode 1 5.077-5.087 vs 5.109-5.135 ms on one box, 5.038-5.054 vs
-# 5.019-5.028 (4 x 30 steps) on another -- the default stays 0
-
 
 
 _CU_STREAMS = []        # (handle, ExternalStream): kept for the process
 
 
 def cu_limited_stream(device, n_cus):
-    """torch.cuda.ExternalStream over ocrk_stream_create_cu_limited(n_cus) on `device`."""
+    """torch.cuda.ExternalStream over ocrk_stream_create_cu_limited(n_cus) on `device`
+    (tools build only). A BLOCKING stream: beside a step on the legacy NULL stream it
+    serialises with it; beside a non-blocking step stream masks of 96-192 CUs measured
+    no change (profiles/r6_stream_ab.txt)."""
     with torch.cuda.device(device):
         h = ctypes.c_void_p()
         call("ocrk_stream_create_cu_limited", int(n_cus), ctypes.byref(h))
@@ -826,41 +824,14 @@ def cu_limited_stream(device, n_cus):
     return st
 
 
-def fork_mode():
-    """0: torch events for stream forks; 1 / 2: ocrk_stream_wait's fence-less events (option FORK_EVENTS)."""
-    return options.get("FORK_EVENTS")
-
-
 def fork(waiter, signaller):
-    """waiter.wait_stream(signaller), through ocrk_stream_wait when fork_mode() is
-    set and the signaller is not being captured into a graph."""
-    mode = fork_mode()
-    if mode and not torch.cuda.is_current_stream_capturing():
-        stream_wait(waiter, signaller, mode)
-    else:
-        waiter.wait_stream(signaller)
-
-
-class StreamMark:
-    """A side stream as a wait target (the store's pending list): wait_on(waiter)
-    orders `waiter` after everything issued on the stream up to that call --
-    a superset of the work up to the mark, which is what the joins need (they
-    wait for all of it) -- through ocrk_stream_wait, without the system-scope
-    release a default event record costs the recording stream."""
-
-    def __init__(self, stream, mode):
-        self.stream, self.mode = stream, mode
-
-    def wait_on(self, waiter):
-        stream_wait(waiter, self.stream, self.mode)
+    """waiter.wait_stream(signaller): the step's cross-stream forks (torch events)."""
+    waiter.wait_stream(signaller)
 
 
 def wait_mark(waiter, mark):
-    """waiter waits for a pending entry: a StreamMark or a torch.cuda.Event."""
-    if isinstance(mark, StreamMark):
-        mark.wait_on(waiter)
-    else:
-        waiter.wait_event(mark)
+    """waiter waits for a pending entry (a torch.cuda.Event)."""
+    waiter.wait_event(mark)
 
 
 def copy_batch(table, njobs, total_tiles, stream_of):

@@ -101,15 +101,10 @@ class _ConvBlock(torch.autograd.Function):
                 and options.get("CONV12_FUSED") and K.conv12_fwd_ok(x, dt)):
             # conv1 -> conv2 in one row walk: conv1's rows produced into conv2's ring (never
             # re-read from HBM), y1 and its ReLU bit mask written for the backward
-            # (or, CONV12_RECOMPUTE, only the bit mask: conv2's weight gradient recomputes y1
-            # from the image, conv2_bwd_weight_c1x)
             w_nk2, _ = store.conv_images(even, dt)
-            want_y1 = not options.get("CONV12_RECOMPUTE")
             y_odd, bits, z12, st12 = K.conv12_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], w_nk2,
-                                                  P[pe + "/bias"], want_y1=want_y1)
+                                                  P[pe + "/bias"])
             ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(z12, x) else None
-            if y_odd is None and ctx.relu_bits is None:    # the fused backward is what needs no y1
-                y_odd = K.conv1_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dt)
             zs = (z12, st12)
         elif k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
             # the ReLU's bit mask for the fused conv2 backward-data + conv1 weight gradient
@@ -180,31 +175,19 @@ class _ConvBlock(torch.autograd.Function):
         dp = dp.contiguous()
         if dp.dtype != dt:
             dp = K.cast(dp, dt)
-        # bias-gradient reductions (conv bias in front of the BN with the BN's dgamma, and
-        # the odd conv's bias from the data-gradient GEMM's tile column sums) go to the side
-        # stream with the weight gradients, off the main stream's dependent chain: queued for
-        # the next conv side fork (option CONV_BIAS_SIDE, no fork of their own), or on the
-        # "reduce" lane (DEFER_BIAS=1)
-        bias_side = bool(options.get("CONV_BIAS_SIDE") and options.get("CONV_SIDE_MERGE")
-                         and options.get("CONV_SIDE") and options.get("SIDE_STREAM"))
-        late = [] if (bias_side or _side_enabled("CONV_SIDE")) else None
-
-        def flush_late():
-            if bias_side:
-                store.conv_late.extend(late)
-                late.clear()
-            else:
-                _issue(store, late)
+        # the bias-gradient reductions (conv bias in front of the BN with the BN's dgamma, and
+        # the odd conv's bias from the data-gradient GEMM's tile column sums) stay in the main
+        # stream's order: on the side stream or a lane of their own they measured slower
+        # (rounds 3-5, profiles/r5_ab_summary.txt)
         dz = K.bn_relu_pool_bwd(z, dp, mean, invstd, P[pe + "/batch_norm/gamma"], P[pe + "/batch_norm/beta"],
                                 POOLS[even], dp_time_major=(k == 4),
                                 dgamma=G[pe + "/batch_norm/gamma"], dbeta=G[pe + "/batch_norm/beta"],
-                                dbias=G[pe + "/bias"], defer=late,      # conv bias grad fused
+                                dbias=G[pe + "/bias"],                  # conv bias grad fused
                                 sync=ctx.bn_sync,
                                 # dgamma / dbeta from the saved pooled output instead of a walk over z
                                 pooled=pooled if ctx.bn_sync is None and ctx.pooled_bn else None)
         B, H, W, C = dz.shape
         if k > 1:
-            flush_late()
             with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):   # overlaps the data gradient below
                 _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
@@ -213,14 +196,9 @@ class _ConvBlock(torch.autograd.Function):
             # the step's tail: conv2's weight gradient (y1, dz) on the side stream beside one
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is
             # contracted as it is produced, never stored: its only consumer is conv1's dW)
-            flush_late()
-            with _conv_side(store, x if y_odd is None else y_odd, dz, *_conv_late_tensors(store)):
+            with _conv_side(store, y_odd, dz, *_conv_late_tensors(store)):
                 _conv_late_run(store)
-                if y_odd is None:                          # conv12 wrote no y1: recomputed per row
-                    K.conv2_bwd_weight_c1x(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], dz,
-                                           G[pe + "/kernel"])
-                else:
-                    _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
+                _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             bits = ctx.relu_bits
             K.conv2_bwd_data_conv1_wgrad(dz, w_bwd, None if bits is not None else y_odd, x, G[po + "/kernel"],
                                          G[po + "/bias"], relu_bits=bits)
@@ -228,11 +206,9 @@ class _ConvBlock(torch.autograd.Function):
             return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         # ReLU of conv_{2k-1} fused; its bias gradient from the GEMM's tile column sums (k > 1)
         if k > 1 and ctx.relu_bits is not None:
-            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, dbias=G[po + "/bias"], relu_bits=ctx.relu_bits, defer=late)
+            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, dbias=G[po + "/bias"], relu_bits=ctx.relu_bits)
         else:
-            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None,
-                                        defer=late)
-        flush_late()
+            dy_odd = K.conv3x3_bwd_data(dz, w_bwd, relu_mask=y_odd, dbias=G[po + "/bias"] if k > 1 else None)
         dx = None
         if k == 1:
             # the step's tail: conv1's weight gradient joins the side stream (behind
@@ -245,12 +221,11 @@ class _ConvBlock(torch.autograd.Function):
             _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
             store.join()                                   # side-stream weight gradients are in
         else:
-            if (k > options.get("CONV_SIDE_MERGE_FROM") and options.get("CONV_SIDE_MERGE") and options.get("CONV_SIDE")
-                    and options.get("SIDE_STREAM")):
+            if k > 2 and options.get("CONV_SIDE") and options.get("SIDE_STREAM"):
                 # the odd conv's weight gradient joins the next side-stream fork (the lower
                 # block's even-conv weight gradient): one fork per block instead of two. Not
-                # conv3's (k = 2, CONV_SIDE_MERGE_FROM): deferred to conv2's fork it queued
-                # in front of conv2's weight gradient at the step's tail
+                # conv3's (k = 2): deferred to conv2's fork it queued in front of conv2's
+                # weight gradient at the step's tail
                 store.conv_late.append((lambda x=x, d=dy_odd, dw=G[po + "/kernel"], ex=ctx.exact:
                                         _conv_wgrad(ex, x, d, dw), (x, dy_odd)))
             else:
@@ -296,7 +271,6 @@ def convnet_layers(inputs, widths, mode, store=None):
     if x.dtype not in (torch.uint8, store.cfg.dtype):
         x = K.cast(x, store.cfg.dtype)
     track = torch.is_grad_enabled() and training
-    store.prefetch_images()                                # beside conv1 (f32 weights, no image)
     h = x
     for k in (1, 2, 3, 4):
         variables = _block_variables(store, k) if track else []
@@ -316,13 +290,9 @@ _SIDE_STREAMS = {}
 
 
 def _new_side_stream(dev, lane):
-    """A side stream; with option SIDE_CU_MASK = n > 0 the weight-gradient lane
-    runs on n CUs only (ocrk_stream_create_cu_limited), the rest left to the
-    main stream's data gradients and BN backward (VERDICT r4 next #2)."""
-    n = options.get("SIDE_CU_MASK")
-    if n <= 0 or lane != "side":
-        return torch.cuda.Stream(device=dev)
-    return K.cu_limited_stream(dev, n)
+    """A side stream (non-blocking, torch's). (A CU-masked one measured no change
+    once the step runs on a stream of its own -- round 6)"""
+    return torch.cuda.Stream(device=dev)
 
 
 class side_work:
@@ -345,8 +315,6 @@ class side_work:
         if side is None:
             side = _SIDE_STREAMS[(dev, self.lane)] = _new_side_stream(dev, self.lane)
         self.side = side
-        # with K.fork_mode(): the fork without the system-scope release of a default
-        # event record (a ~6 us bubble on the main stream per fork)
         K.fork(side, torch.cuda.current_stream(dev))
         self.ctx = torch.cuda.stream(side)
         self.ctx.__enter__()
@@ -355,45 +323,13 @@ class side_work:
     def __exit__(self, *exc):
         if self.side is None:
             return False
-        mode = K.fork_mode()
-        if mode and not torch.cuda.is_current_stream_capturing():
-            done = K.StreamMark(self.side, mode)
-        else:
-            done = torch.cuda.Event()
-            done.record(self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
         self.ctx.__exit__(*exc)
         for t in self.tensors:
             t.record_stream(self.side)
         self.store.pending.append(done)
         return False
-
-
-def _run_deferred(store):
-    """Issue weight-gradient work an upper layer deferred (on the side stream,
-    behind everything issued so far on the main stream)."""
-    pending = getattr(store, "deferred", None)
-    while pending:
-        fn, tensors = pending.pop(0)
-        with side_work(store, *tensors):
-            fn()
-
-
-def _side_enabled(var):
-    """Deferred bias reductions go to the side stream unless it is off
-    (options SIDE_STREAM=0 / `var`=0); opt-in DEFER_BIAS=1 (measured slower: 5.95 vs
-    5.80-5.90 ms per step, the side stream being the busier one in the conv backward)."""
-    return bool(options.get("SIDE_STREAM") and options.get(var) and options.get("DEFER_BIAS") == 1)
-
-
-def _issue(store, late):
-    """Run deferred (fn, tensors) bias reductions on their own stream (the
-    "reduce" lane): they have slack until the optimizer step, so they neither
-    sit in the main stream's dependent chain nor delay the side stream's
-    weight-gradient GEMMs (measured: on the side stream they cost 0.12 ms)."""
-    while late:
-        fn, tensors = late.pop(0)
-        with side_work(store, *tensors, lane="reduce"):
-            fn()
 
 
 def _conv_late_tensors(store):
@@ -428,12 +364,8 @@ class _BiLSTM(torch.autograd.Function):
         T, B, n_in = x.shape
         H = store.cfg.rnn_sizes[layer - 1]
         wxT, _wx, whT, _wh, bias = store.lstm_images(layer, dt)
-        if K.lstm_fused_x_ok(B, H, n_in, dt):
-            # the input projection inside the persistent loop (first layer: In = 256)
-            out, hprev, cprev, acts = K.lstm_fwd_fused_x(x, wxT, bias, whT, seq_len, T, B, H)
-        else:
-            gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
-            out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt, save=any(ctx.needs_input_grad))
+        gx = K.gemm(x.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=dt)   # [T*B, 8H]
+        out, hprev, cprev, acts = K.lstm_fwd(gx, whT, seq_len, T, B, H, dt, save=any(ctx.needs_input_grad))
         ctx.store, ctx.layer, ctx.H = store, layer, H
         ctx.save_for_backward(x, seq_len, hprev, cprev, acts)
         return out
@@ -450,20 +382,13 @@ class _BiLSTM(torch.autograd.Function):
             dout = K.cast(dout, dt)
         _wxT, wx, _whT, wh, _bias = store.lstm_images(layer, dt)
         # [T,B,2,4H]; the bias gradient (both directions) formed in the BPTT loop
-        late = [] if _side_enabled("SIDE_STREAM") else None
-        dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer),
-                        defer=late)
+        dG = K.lstm_bwd(wh, seq_len, dout, cprev, acts, T, B, H, dbias=store.flat_bias_pair_grad(layer))
         R = T * B
         dx = None
-        # the lowest layer's data gradient first (option DX_FIRST=1): the side stream's
-        # weight-gradient GEMMs start behind it instead of taking the CUs it needs
-        # (it gates the whole conv-tower backward); upper layers keep dx beside dW_h
-        dx_first = options.get("DX_FIRST") == 1 and layer == 1 and ctx.needs_input_grad[0]
-        if dx_first:
-            dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
-        _run_deferred(store)                                 # an upper layer's dW_x, now behind this BPTT
         pre = f"rnn/bdrnn{layer}"
-        _issue(store, late)                                  # the bias partials' ordered sum
+        # (issue orders measured slower and dropped: the lowest layer's data gradient
+        # first, 5.08-5.09 vs 5.08 ms; an upper layer's dW_x deferred behind the lower
+        # BPTT, 5.17-5.20 -- profiles/r5_ab_summary.txt)
         with side_work(store, x, hprev, dG):               # overlaps the next layer's BPTT
             gf, gb = store.grads[f"{pre}/fw/lstm_cell/kernel"], store.grads[f"{pre}/bw/lstm_cell/kernel"]
             sk = gf.numel()                                                      # [In+H, 4H] f32 each
@@ -479,19 +404,14 @@ class _BiLSTM(torch.autograd.Function):
                 # both directions as one batched GEMM each (batch = direction: dG column
                 # block d * 4H, h_prev column block d * H, gradient d * (In+H) * 4H):
                 # dW_x = x^T . dG_d ; dW_h = h_prev_d^T . dG_d  (split-K over T*B)
-                def dw_x():
-                    for xa, _ha, ga in passes:
-                        K.gemm(xa, ga.view(R, 2 * G4), trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R,
-                               lda=n_in, ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
-                               splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer, late=True)))
                 for _xa, ha, ga in passes:
                     K.gemm(ha.view(R, 2 * H), ga.view(R, 2 * G4), trans_a=True, out=gf[n_in:], accumulate=True,
                            M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4, batch=2, stride_a=H, stride_b=G4,
                            stride_c=sk, splits=_splits(H, G4, R, batch=2, items=_tn_items(layer)))
-                if layer > 1 and options.get("DEFER_DWX") == 1 and ctx.needs_input_grad[0]:
-                    store.deferred.append((dw_x, (x, dG)))   # issued behind the next BPTT (fewer CUs held)
-                else:
-                    dw_x()
+                for xa, _ha, ga in passes:
+                    K.gemm(xa, ga.view(R, 2 * G4), trans_a=True, out=gf, accumulate=True, M=n_in, N=G4, K=R,
+                           lda=n_in, ldb=2 * G4, ldc=G4, batch=2, stride_a=0, stride_b=G4, stride_c=sk,
+                           splits=_splits(n_in, G4, R, batch=2, items=_tn_items(layer)))
             else:
                 for xa, ha, ga in passes:
                     dg = ga.view(R, 2 * G4)
@@ -502,7 +422,7 @@ class _BiLSTM(torch.autograd.Function):
                         K.gemm(ha.view(R, 2 * H)[:, d * H:], dgd, trans_a=True, out=gk[n_in:], accumulate=True,
                                M=H, N=G4, K=R, lda=2 * H, ldb=2 * G4, ldc=G4,
                                splits=_splits(H, G4, R, items=_tn_items(layer)))
-        if ctx.needs_input_grad[0] and not dx_first:
+        if ctx.needs_input_grad[0]:
             dx = K.gemm(dG.view(R, 2 * G4), wx, trans_b=True, out_dtype=dt).view(T, B, n_in)
         return (dx,) + (None,) * (len(ctx.needs_input_grad) - 1)
 
@@ -534,12 +454,9 @@ class _BiGRU(torch.autograd.Function):
             dout = K.cast(dout, dt)
         _wxT, wx, _whgT, _whcT, whg, whc, _bias = store.gru_images(layer, dt)
         # [T,B,2,3H]; the [gates | candidate] bias gradients formed in the BPTT loop
-        late = [] if _side_enabled("SIDE_STREAM") else None
-        dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=store.gru_bias_cat_grad(layer),
-                       defer=late)
+        dG = K.gru_bwd(whg, whc, seq_len, dout, hprev, acts, T, B, H, dbias=store.gru_bias_cat_grad(layer))
         pre = f"rnn/bdrnn{layer}"
         R = T * B
-        _issue(store, late)                                         # the bias partials' ordered sum
         side = side_work(store, x, hprev, rh, dG)
         side.__enter__()
         gf, gb = store.grads[f"{pre}/fw/gru_cell/gates/kernel"], store.grads[f"{pre}/bw/gru_cell/gates/kernel"]
@@ -592,13 +509,13 @@ class _BiGRU(torch.autograd.Function):
 
 
 # an upper layer's dW_x is queued behind the lower BPTT and meets the lower layer's
-# data gradient when that BPTT ends (OCRK_TN_ITEMS_LATE: its own cap; 192: 5.28,
+# data gradient when that BPTT ends (a cap of its own measured slower: 192: 5.28,
 # 128: 5.34 vs 5.27-5.30 ms at 256)
-# (options TN_ITEMS_L1 = 160, TN_ITEMS = 256, TN_ITEMS_LATE = TN_ITEMS)
-def _tn_items(layer, late=False):
+# (options TN_ITEMS_L1 = 160, TN_ITEMS = 256)
+def _tn_items(layer):
     if layer == 1:
         return options.get("TN_ITEMS_L1")
-    return options.get("TN_ITEMS_LATE" if late else "TN_ITEMS")
+    return options.get("TN_ITEMS")
 
 
 def _splits(M, N, Kdim, batch=1, items=None):

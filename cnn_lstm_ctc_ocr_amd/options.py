@@ -13,38 +13,31 @@ its launch path. ``override`` is what tests use to run an alternative route:
 import contextlib
 import os
 
-# host-side options (this package) -> default
+# host-side options (this package) -> default. Round 6 kept only the defaults,
+# alternatives that are real routes or documented A/B switches; the routes measured
+# slower and kept off (LSTM_FUSE_X, DEFER_BIAS, DEFER_DWX, DX_FIRST, PREFETCH_IMAGES,
+# CONV12_RECOMPUTE, CONV_BIAS_SIDE, FORK_EVENTS, SIDE_CU_MASK, TN_ITEMS_LATE, ...) were
+# deleted or moved to the tools build (include/ocrk_debug.h); DESIGN.md section 6.
 _HOST_DEFAULTS = {
+    # real alternatives
     "LSTM_PERSISTENT": 1,     # 0: per-step recurrent kernels instead of the persistent loops
-    "LSTM_FUSE_X": 0,         # 1: first-layer projection inside the persistent forward (opt-in)
-    "BATCHED_IMAGES": 1,      # 0: weight images rebuilt by per-layout copies instead of one batched launch
+    "F32_TRAIN_EXACT": 0,     # fp32 policy, 1: exact f32 products everywhere (else conv tower only)
+    # documented A/B switches (each turns one default route off; the other route stays tested)
     "SIDE_STREAM": 1,         # 0: weight gradients inline on the main stream
     "CONV_SIDE": 1,           # 0: conv weight gradients inline
-    "DEFER_BIAS": 0,          # 1: bias reductions on their own stream (measured slower)
-    "DEFER_DWX": 0,           # 1: an upper layer's dW_x behind the lower BPTT (measured no gain)
-    "DX_FIRST": 0,            # 1: the lowest layer's data gradient before its weight gradients
-    "PREFETCH_IMAGES": 0,     # 1: the weight-image refresh on its own stream beside conv1 (measured slower)
     "CONV12_FUSED": 1,        # 0: conv1 and conv2 forward as two passes (y1 written, then re-read)
-    "CONV12_RECOMPUTE": 0,    # 1: conv12 writes no y1, conv2's weight gradient recomputes it (measured +55 us)
-    "CONV_BIAS_SIDE": 0,      # 1: conv / BN bias-gradient reductions ride the next conv side fork (measured slower)
-    "CONV_SIDE_MERGE_FROM": 2,  # blocks k > this merge their odd weight gradient into the next fork
-    "CONV_SIDE_MERGE": 1,     # 0: a side-stream fork for each conv weight gradient (two per block)
     "RELU_BITS": 1,           # 0: conv3/5/7's ReLU masks for conv4/6/8's backward-data as their bf16 outputs
     "POOLED_BN": 1,           # 0: the BN backward's dgamma / dbeta pass walks z instead of the pooled output
     "CONV1_FUSED": 1,         # 0: conv2's backward-data stores dy1, conv1's weight gradient re-reads it
-    "TN_ITEMS": 256,          # workgroup cap of the recurrent weight-gradient launches
-    "TN_ITEMS_L1": 160,       # the same for the first layer (beside the conv backward)
-    "TN_ITEMS_LATE": 0,       # deferred dW_x cap (0: TN_ITEMS)
-    "ADAM_ZERO": 1,           # 0: separate gradient fill instead of the in-Adam zeroing
-    "UNIT_SEED": 1,           # 0: backward seeded with torch's ones instead of the resident 1.0
-    "FORK_EVENTS": 0,         # 1 / 2: stream forks through ocrk_stream_wait's fence-less events
-    "SIDE_CU_MASK": 0,        # > 0: the weight-gradient side stream restricted to this many CUs
-    "F32_TRAIN_EXACT": 0,     # 1: fp32 training with exact f32 products everywhere (else conv tower only)
+    # tuning (workgroup caps of the recurrent weight-gradient launches)
+    "TN_ITEMS": 256,          # layer 2
+    "TN_ITEMS_L1": 160,       # layer 1 (beside the conv backward)
 }
 # kernel-side options (libocrk's registry, csrc/common.h)
+# (LSTM_BWD_KSPLIT, LSTM_BWD_PB16 and PP_DEEP exist in the tools build only)
 KERNEL_OPTIONS = ("CONV_DIRECT", "CONV_ROWS", "CONV_ROWS_WIDE", "CONV_WGRAD_BLOCKS", "LSTM_SPIN_LIMIT",
-                  "PERSIST_LATE", "LSTM_BWD_KSPLIT", "LSTM_BWD_PB16", "LSTM_BWD_R16", "CTC_LDS",
-                  "PP_PERSIST_NK", "PP_DEEP", "NT_F32_EXACT", "NT_F32_MASK",
+                  "PERSIST_LATE", "LSTM_BWD_R16", "CTC_LDS",
+                  "PP_PERSIST_NK", "NT_F32_EXACT", "NT_F32_MASK",
                   "NT_F32_X6", "BEAM_WAVE", "BN_BWD_BLOCKS", "BN_ROUTE", "BN_ROUTE_SEG", "BN_ROUTE_NCH", "CONV_TN_ITEMS", "CONV_TN4_ITEMS",
                   "CONV_WGRAD_CUS", "F32_MFMA", "GEMM_NT", "GEMM_NT_STAGED", "GEMM_PP", "GEMM_PPTN", "PP_MIN_N", "GEMM_TN",
                   "LSTM_DMA", "LSTM_BWD_DMA", "LSTM_FWD_R16", "NT_TAP_UNIFORM")
@@ -61,8 +54,6 @@ def _env_int(name, default):
 
 
 _HOST = {k: _env_int(k, d) for k, d in _HOST_DEFAULTS.items()}
-if not _HOST["TN_ITEMS_LATE"]:
-    _HOST["TN_ITEMS_LATE"] = _HOST["TN_ITEMS"]
 
 
 def get(name):

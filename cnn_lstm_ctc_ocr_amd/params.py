@@ -14,7 +14,6 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from . import options
 from .config import LAYER_PARAMS, ModelConfig
 
 _ALIGN = 64  # elements (256 B): every view starts 16-B aligned for vector loads
@@ -139,10 +138,7 @@ class ParamStore:
         self.version = 0
         self._images = {}
         self.pending = []          # events of side-stream gradient work not yet joined
-        self.deferred = []         # (launch fn, tensors) of gradient work an upper layer deferred
         self.conv_late = []        # (launch fn, tensors): conv weight gradients queued for the next side fork
-        self._img_stream = None    # the weight-image refresh's own stream (prefetch_images)
-        self._img_wait = None      # its completion, awaited by the first images() consumer
         self.bn_group = None       # SyncBN: the process group TRAIN-mode BatchNorm statistics span
         self.f32_conv_exact = False    # fp32 training: the conv tower on exact f32 products (Trainer)
         self.load_state_dict(values if values is not None else reference_init(self.cfg, seed))
@@ -179,9 +175,6 @@ class ParamStore:
     def join(self):
         """Make the current stream wait for side-stream gradient work
         (model.side_work) so flat_grad is complete in stream order."""
-        while self.deferred:        # never issued (no lower layer ran): issue it here, in order
-            fn, _tensors = self.deferred.pop(0)
-            fn()
         while self.conv_late:       # queued conv weight gradients no later fork took: inline, in order
             fn, _tensors = self.conv_late.pop(0)
             fn()
@@ -196,9 +189,6 @@ class ParamStore:
         self.version += 1
         self._images.clear()
         self._plan_fresh = False
-        if self._img_wait is not None:          # a prefetched refresh lands before any later one
-            K.wait_mark(torch.cuda.current_stream(self.device), self._img_wait)
-            self._img_wait = None
 
     # ---------------------------------------------------- weight images
     def images(self, key, builder):
@@ -211,9 +201,6 @@ class ParamStore:
             if not self._plan_fresh:
                 K.copy_batch(plan["table"], plan["njobs"], plan["tiles"], self.flat)
                 self._plan_fresh = True
-            if self._img_wait is not None:                  # prefetched on its own stream
-                K.wait_mark(torch.cuda.current_stream(self.device), self._img_wait)
-                self._img_wait = None
             return plan["images"][key]
         img = self._images.get(key)
         if img is None:
@@ -221,38 +208,8 @@ class ParamStore:
             self._images[key] = img
         return img
 
-    def prefetch_images(self):
-        """Issue a stale weight-image refresh now on its own stream (option
-        PREFETCH_IMAGES=1): the step's first kernel (conv1, which reads its f32 weights
-        directly) runs beside it instead of ahead of it; the first images() consumer
-        waits for it. Off by default: the refresh is 29 us on the critical path, but
-        beside conv1 the step measured slower (same box, 3 x 30 steps: 5.007-5.016
-        vs 4.978-4.990 ms inline) -- both are HBM streams and the cross-stream wait
-        lands in front of conv2."""
-        if self.device.type != "cuda" or not options.get("PREFETCH_IMAGES"):
-            return
-        if torch.cuda.is_current_stream_capturing():
-            return
-        plan = self._plan_for(("logits", self.cfg.dtype))
-        if plan is None or self._plan_fresh:
-            return
-        if self._img_stream is None:
-            self._img_stream = torch.cuda.Stream(device=self.device)
-        cur = torch.cuda.current_stream(self.device)
-        K.fork(self._img_stream, cur)                       # after the optimizer step that made them stale
-        with torch.cuda.stream(self._img_stream):
-            K.copy_batch(plan["table"], plan["njobs"], plan["tiles"], self.flat)
-        mode = K.fork_mode()
-        if mode:
-            self._img_wait = K.StreamMark(self._img_stream, mode)
-        else:
-            ev = torch.cuda.Event()
-            ev.record(self._img_stream)
-            self._img_wait = ev
-        self._plan_fresh = True
-
     def _plan_for(self, key):
-        if self.device.type != "cuda" or not options.get("BATCHED_IMAGES"):
+        if self.device.type != "cuda":
             return None
         dtype = key[-1]
         if dtype != self.cfg.dtype:

@@ -282,7 +282,7 @@ class Trainer:
         loss = ctc_loss_layer(logits, label, seq_len)
         # d loss / d loss = 1 from a resident scalar: no fill launch per step, and the
         # CTC backward skips its x 1 pass over the logits gradient
-        if loss.dtype == torch.float32 and options.get("UNIT_SEED"):
+        if loss.dtype == torch.float32:
             _model.unit_backward(loss)
         else:
             loss.backward()
@@ -301,7 +301,7 @@ class Trainer:
         t = self.global_step + 1
         lr = self.learning_rate()
         lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
-        zero = bool(options.get("ADAM_ZERO")) and store.device.type == "cuda"
+        zero = store.device.type == "cuda"
         # the update clears the gradient as it reads it: the next loss_and_grads skips its fill
         # (a 4-byte-per-parameter pass at the top of the step)
         K.adam_(store.flat, store.flat_grad, self.m, self.v, lr_t, self.beta1, self.beta2, self.eps,

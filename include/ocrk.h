@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 5
+#define OCRK_ABI_VERSION 6
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -89,20 +89,14 @@ const char* ocrk_last_error(void);
  * ocrk_set_option changes it (process-wide, takes effect at the next launch; the
  * "OCRK_" prefix is optional in `name`). Names: CONV_DIRECT, CONV_ROWS,
  * CONV_ROWS_WIDE, CONV_WGRAD_BLOCKS, LSTM_SPIN_LIMIT, PERSIST_LATE,
- * LSTM_BWD_KSPLIT, LSTM_BWD_PB16, LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, PP_DEEP, NT_F32_EXACT,
+ * LSTM_BWD_R16, CTC_LDS, PP_PERSIST_NK, NT_F32_EXACT,
  * NT_F32_MASK, NT_F32_X6, BEAM_WAVE, BN_BWD_BLOCKS, BN_ROUTE, BN_ROUTE_SEG,
  * BN_ROUTE_NCH, CONV_TN_ITEMS, CONV_TN4_ITEMS,
  * CONV_WGRAD_CUS, F32_MFMA, GEMM_NT, GEMM_NT_STAGED, GEMM_PP, GEMM_PPTN, PP_MIN_N, GEMM_TN, LSTM_DMA,
  * LSTM_BWD_DMA, LSTM_FWD_R16, NT_TAP_UNIFORM (meanings in csrc/common.h). Unknown name: OCRK_ERR_INVALID_ARG.
- * `prev` may be NULL. */
+ * `prev` may be NULL. (LSTM_BWD_KSPLIT, LSTM_BWD_PB16 and PP_DEEP: the tools build
+ * only -- routes measured slower, not compiled into this library.) */
 int ocrk_set_option(const char* name, int64_t value, int64_t* prev);
-
-/* A stream on the current device whose kernels run on only n_cus of its CUs
- * (hipExtStreamCreateWithCUMask; the CUs left out are evenly spaced over the CU
- * order, so every XCD keeps some), for side work that must leave CUs to the
- * main stream (the weight gradients beside the data gradients; option
- * SIDE_CU_MASK). Released with ocrk_stream_destroy. No reference counterpart. */
-int ocrk_stream_create_cu_limited(int n_cus, void** stream);
 
 /* x = hi + lo, hi = bf16(x), lo = bf16(x - hi) (round to nearest even; |x - hi - lo| <=
  * 2^-17 |x|): the bf16x3 split as two bf16 planes [n], so the bf16 GEMM engines form an
@@ -110,7 +104,6 @@ int ocrk_stream_create_cu_limited(int n_cus, void** stream);
  * step's weight gradients, train.Trainer). n % 8 == 0, 16-B aligned buffers.
  * No reference counterpart (TF1 multiplies float32 directly). */
 int ocrk_split_bf16(const float* x, int64_t n, void* hi, void* lo, void* stream);
-int ocrk_stream_destroy(void* stream);
 int ocrk_get_option(const char* name, int64_t* value);
 
 /* a1 -- validate._preprocess_image (src/weinman/validate.py:56-68):
@@ -183,15 +176,6 @@ int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype);
 int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
                     const void* w_nk2, const float* b2, void* y1, void* relu_bits, void* z, float* stats, int dtype,
                     void* stream);
-/* conv2's weight gradient (conv_layer 2's backward, model.py:84-109) with its input
- * y1 = relu(conv1(x)) recomputed per row from the image instead of read: the partner of
- * ocrk_conv12_fwd with y1 = NULL, bit-identical to ocrk_conv3x3_bwd_weight on the y1 that
- * ocrk_conv12_fwd writes. dz bf16 [B,IH-2,IW-2,32]; dw f32 [3][3][32][32] (+)=; ws per
- * ocrk_conv3x3_wgrad_workspace_size(B, IH-2, IW-2, 32, 32). */
-int ocrk_conv2_bwd_weight_c1x_supported(int B, int IH, int IW, int dtype);
-int ocrk_conv2_bwd_weight_c1x(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
-                              const void* dz, float* dw, int accumulate, void* ws, size_t ws_bytes, int dtype,
-                              void* stream);
 /* conv1 weight/bias gradient from dz = dL/d(pre-ReLU conv1), f32 outputs. */
 size_t ocrk_conv1_wgrad_workspace_size(int B, int H, int W, int cout);
 int ocrk_conv1_bwd_weight(const void* x, int x_is_u8, const void* dz, int B, int H, int W, int cout,
@@ -376,15 +360,6 @@ size_t ocrk_lstm_fwd_persistent_workspace_size(int B, int H);
 int ocrk_lstm_fwd_persistent(const void* gx, const void* whT, const int* seq_len, int T, int B, int H,
                              void* out, void* hprev_t, float* cprev_t, void* acts_t, unsigned* err,
                              unsigned* flags, void* ws, size_t ws_bytes, void* stream);
-/* The first layer's forward loop with its input projection FUSED (model_bu.py:186-192's
- * [x, h] . W for the x half): x dtype=bf16 [T][B][n_in] time-major features, wxT
- * [2][4H][n_in] (per-direction W_x^T, gate-major rows), bias f32 [2][4H]; no gx
- * tensor and no projection GEMM. H = 512, n_in = 256 (the conv features). */
-int ocrk_lstm_fwd_persistent_x_supported(int B, int H, int n_in);
-int ocrk_lstm_fwd_persistent_x(const void* x, int n_in, const void* wxT, const float* bias, const void* whT,
-                               const int* seq_len, int T, int B, int H, void* out, void* hprev_t, float* cprev_t,
-                               void* acts_t, unsigned* err, unsigned* flags, void* ws, size_t ws_bytes,
-                               void* stream);
 /* Persistent backward time loop (BPTT of the same layer, bf16): ONE launch runs
  * all T reverse steps of both directions with W_h slices in registers, the
  * gate gradients dz exchanged between the co-resident workgroups of a
@@ -553,14 +528,6 @@ int ocrk_timer_create(void** ev);
 int ocrk_timer_record(void* ev, void* stream);
 int ocrk_timer_elapsed(void* ev0, void* ev1, float* ms);
 int ocrk_timer_destroy(void* ev);
-
-/* Stream ordering on one device: `waiter` waits for everything issued so far on
- * `signaller` (the weight-gradient side streams' fork from the main stream).
- * mode 1: a ring of events created with hipEventDisableSystemFence; mode 2: with
- * hipEventReleaseToDevice -- both skip the system-scope release a default event
- * record makes (a ~6 us bubble on the recording stream); mode 0: a default
- * event. Not for streams being captured (the caller uses a graph-aware event). */
-int ocrk_stream_wait(void* waiter, void* signaller, int mode);
 
 /* Host-side CRC32C (Castagnoli) of n bytes continuing from `crc` (0 to start):
  * TFRecord framing and TensorBundle checksums for the input pipeline and the

@@ -158,66 +158,6 @@ def test_conv12_fused_forward(cuda, B, IH, IW, x_u8):
     assert torch.equal(bits, bits3) and torch.equal(z, z3) and torch.equal(stats, st3)
 
 
-@pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70), (300, 6, 20)])
-@pytest.mark.parametrize("x_u8", [True, False])
-def test_conv2_wgrad_recomputes_y1(cuda, B, IH, IW, x_u8):
-    """conv2's weight gradient with y1 recomputed from the image per row
-    (ocrk_conv2_bwd_weight_c1x) is bit-identical to the rows weight gradient over the y1
-    conv12_fwd stores (same y1 bits, same MFMA order), accumulate included, and within
-    the bf16 tolerance of the float64 sum y1 (x) dz. B = 300: more images than workgroups."""
-    from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    rng = np.random.default_rng(IH * 31 + IW + 5 * x_u8)
-    w1 = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
-    b1 = (rng.standard_normal(32) * 0.3).astype(np.float32)
-    w2 = _bf(rng.standard_normal((3, 3, 32, 32)) / np.sqrt(288))
-    if x_u8:
-        xd = torch.from_numpy(rng.integers(0, 256, (B, IH, IW)).astype(np.uint8)).to(cuda)
-    else:
-        xd = torch.from_numpy(_bf(rng.standard_normal((B, IH, IW)))).to(cuda).bfloat16()
-    w1d, b1d = torch.from_numpy(w1).to(cuda), torch.from_numpy(b1).to(cuda)
-    w_nk = Kn.permute3(torch.from_numpy(w2).to(cuda), 9 * 32, 32, 1, torch.bfloat16).view(32, 9 * 32)
-    b2d = torch.zeros(32, device=cuda)
-    y1, _, _, _ = Kn.conv12_fwd(xd, w1d, b1d, w_nk, b2d)
-    dz = torch.from_numpy(_bf(rng.standard_normal((B, IH - 2, IW - 2, 32)))).to(cuda).bfloat16()
-    seed = torch.from_numpy(rng.standard_normal((3, 3, 32, 32)).astype(np.float32)).to(cuda)
-    dw_ref, dw = seed.clone(), seed.clone()
-    Kn.conv3x3_bwd_weight(y1, dz, dw_ref, accumulate=True)
-    Kn.conv2_bwd_weight_c1x(xd, w1d, b1d, dz, dw, accumulate=True)
-    torch.cuda.synchronize()
-    assert torch.equal(dw, dw_ref)
-    dw0 = torch.full_like(seed, 7.0)
-    Kn.conv2_bwd_weight_c1x(xd, w1d, b1d, dz, dw0, accumulate=False)
-    y64 = y1.double().cpu().numpy()
-    d64 = dz.double().cpu().numpy()
-    H, W = IH - 2, IW - 2
-    yp = np.pad(y64, ((0, 0), (1, 1), (1, 1), (0, 0)))
-    ref = np.stack([np.stack([np.einsum("bhwc,bhwo->co", yp[:, i:i + H, j:j + W], d64) for j in range(3)])
-                    for i in range(3)])
-    got = dw0.double().cpu().numpy()
-    assert np.abs(got - ref).max() <= 1e-4 * (np.abs(ref).max() + 1.0)
-
-
-def test_conv12_recompute_gives_the_same_step(cuda, ocrk_opts):
-    """A bf16 train step with conv12 writing no y1 (CONV12_RECOMPUTE: conv2's weight
-    gradient recomputes it from the image) gives the same gradient bits and loss."""
-    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
-    from cnn_lstm_ctc_ocr_amd.train import Trainer
-    rng = np.random.default_rng(9)
-    img = torch.from_numpy(rng.integers(0, 256, (48, 32, 100, 1), dtype=np.uint8)).to(cuda)
-    labels = [list(rng.integers(0, 95, int(rng.integers(2, 9)))) for _ in range(48)]
-    out = []
-    for m in (0, 1):
-        ocrk_opts("CONV12_RECOMPUTE", m)
-        store = ParamStore(ModelConfig(dtype=torch.bfloat16), device=cuda, seed=4)
-        tr = Trainer(store)
-        loss = tr.loss_and_grads(img, np.full(48, 100, np.int32), labels)
-        store.join()
-        torch.cuda.synchronize()
-        out.append((store.flat_grad.clone(), float(loss.detach()) if torch.is_tensor(loss) else float(loss)))
-    assert torch.equal(out[0][0], out[1][0])
-    assert out[0][1] == out[1][1]
-
-
 @pytest.mark.parametrize("B,H,W,cin,cout,cnext", [(4, 15, 127, 32, 64, 64), (4, 7, 126, 64, 128, 128),
                                                   (8, 3, 125, 128, 256, 256), (3, 5, 37, 64, 64, 64)])
 def test_relu_bit_masks_conv_pair(cuda, B, H, W, cin, cout, cnext):
@@ -321,33 +261,6 @@ def test_bf16_plain_gemms_bias_bf16_out(cuda, M_, N, K, tag):
     # every element within its own bf16 rounding (+ accumulation noise)
     err = np.abs(out.float().cpu().numpy() - ref)
     assert np.all(err <= 2 ** -8 * np.abs(ref) + 1e-3 * np.abs(ref).max()), tag
-
-
-@pytest.mark.parametrize("M_,N,K,relu,with_bias", [(32000, 4096, 1024, False, True), (8000, 4096, 256, False, True),
-                                                   (8000, 1024, 4096, False, False), (7777, 1032, 96, True, True),
-                                                   (4100, 520, 200, False, True)])
-def test_pp_deep_schedule_bit_identical(cuda, ocrk_opts, M_, N, K, relu, with_bias):
-    """The deep-lead ping-pong schedule (option PP_DEEP, csrc/gemm_pp.hip:
-    units issued into slots as they free, persistent workgroups with items
-    prefetched across, C staged in the U2 / U3 slots) multiplies in the same
-    order as the one-tile-lead form, so its output is the same bits -- on the
-    bench shapes (32,000 rows: ~8 items per workgroup), BN = 128 tiles, ragged
-    M / N / K tails, with and without bias, with ReLU."""
-    from cnn_lstm_ctc_ocr_amd import kernels as Kn
-    rng = np.random.default_rng(M_ + N + K)
-    a = torch.from_numpy(_bf(rng.standard_normal((M_, K)))).to(cuda).bfloat16()
-    w = torch.from_numpy(_bf(rng.standard_normal((N, K)) / np.sqrt(K))).to(cuda).bfloat16()
-    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).to(cuda) if with_bias else None
-    outs = []
-    for deep in (0, 1):
-        ocrk_opts("PP_DEEP", deep)
-        outs.append(Kn.gemm(a, w, trans_b=True, bias=bias, relu=relu, out_dtype=torch.bfloat16))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]), (M_, N, K)
-    ref = a[:2048].double() @ w.double().t() + (bias.double() if with_bias else 0)
-    if relu:
-        ref = ref.clamp_min(0)
-    assert _rel(outs[1][:2048].double().cpu().numpy(), ref.cpu().numpy()) < BF16_OUT
 
 
 @pytest.mark.parametrize("R,n_in,G4,splits,col", [(8000, 1024, 2048, 4, 0), (8000, 512, 2048, 8, 2048),

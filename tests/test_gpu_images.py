@@ -22,16 +22,18 @@ def _all_images(store, dtype):
 
 @pytest.mark.parametrize("cell,sizes", [("lstm", (512, 512)), ("gru", (512, 256))])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_batched_images_equal_the_per_image_builders(cuda, ocrk_opts, cell, sizes, dtype):
+def test_batched_images_equal_the_per_image_builders(cuda, cell, sizes, dtype):
     from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore
     store = ParamStore(ModelConfig(cell=cell, rnn_sizes=sizes, dtype=dtype), device=cuda, seed=7)
     for rnd in range(2):
-        ocrk_opts("BATCHED_IMAGES", 1)
         batched = _all_images(store, dtype)
         assert store._plan_fresh                          # the batched launch made them
-        ocrk_opts("BATCHED_IMAGES", 0)
+        plan, store._plan = store._plan, None             # the per-image builders (the path of keys
+        store._plan_for = lambda key: None                # outside the batched plan)
         store._images.clear()
         built = _all_images(store, dtype)
+        del store._plan_for
+        store._plan = plan
         torch.cuda.synchronize()
         assert len(batched) == len(built)
         for a, b in zip(batched, built):
@@ -39,27 +41,3 @@ def test_batched_images_equal_the_per_image_builders(cuda, ocrk_opts, cell, size
         with torch.no_grad():                             # an update: new values, new images
             store.flat.mul_(1.5).add_(0.01)
         store.bump()
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_side_stream_fork_modes_give_the_same_step(cuda, ocrk_opts, mode):
-    """The side-stream fork through ocrk_stream_wait (events without the
-    system-scope release) orders the weight-gradient work exactly as the
-    default torch event: the same gradient bits (every kernel reduces in a
-    fixed order) over a whole bf16 train step with the side streams busy."""
-    import numpy as np
-    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, kernels as K
-    from cnn_lstm_ctc_ocr_amd.train import Trainer
-    rng = np.random.default_rng(5)
-    img = torch.from_numpy(rng.integers(0, 256, (64, 32, 128, 1), dtype=np.uint8)).to(cuda)
-    labels = [list(rng.integers(0, 95, int(rng.integers(2, 9)))) for _ in range(64)]
-    grads = []
-    for m in (0, mode):
-        ocrk_opts("FORK_EVENTS", m)
-        store = ParamStore(ModelConfig(dtype=torch.bfloat16), device=cuda, seed=2)
-        tr = Trainer(store)
-        tr.loss_and_grads(img, np.full(64, 128, np.int32), labels)
-        store.join()
-        torch.cuda.synchronize()
-        grads.append(store.flat_grad.clone())
-    assert torch.equal(grads[0], grads[1])

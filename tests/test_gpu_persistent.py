@@ -67,18 +67,7 @@ def test_persistent_fwd_bwd_match_step_kernels_and_oracle(cuda, ocrk_opts, T, B,
     dz_ref = _bptt_ref(caches, ks, dout_np, T, B, H, n_in)
     got = dpers.float().cpu().numpy()
     assert np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
-    # the K-split form of the persistent BPTT (OCRK_LSTM_BWD_KSPLIT=1, opt-in) against
-    # the gather default: same bounds against the oracle and the per-step kernels
-    ocrk_opts("LSTM_BWD_KSPLIT", 1)
-    dgat = K.lstm_bwd(wh, seq_d, dout, cprev, acts, T, B, H)
-    torch.cuda.synchronize()
-    ocrk_opts.reset("LSTM_BWD_KSPLIT")
-    assert K.lstm_error_word(cuda).item() == 0
-    assert (dstep.float() - dgat.float()).abs().max().item() < 2e-2 * max(scale, 1e-6)
-    gg = dgat.float().cpu().numpy()
-    assert np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref) < 5e-2
-    print(f"dz rel err vs oracle: gather {np.linalg.norm(got - dz_ref) / np.linalg.norm(dz_ref):.3e} "
-          f"K-split {np.linalg.norm(gg - dz_ref) / np.linalg.norm(dz_ref):.3e}")
+    # (the K-split BPTT, measured slower, lives in the tools build only since round 6)
 
 
 def _bptt_ref(caches, ks, dout_np, T, B, H, n_in):
@@ -187,44 +176,6 @@ def test_persistent_timeout_sets_status_and_raises(cuda, ocrk_opts):
     # the default limit on the same launch: no bit
     K.lstm_fwd(gx, whT, seq, T, B, H, torch.bfloat16)
     assert K.read_status(cuda) == 0
-
-
-@pytest.mark.parametrize("B", [64, 256])
-def test_fused_input_projection_forward(cuda, B):
-    """The first layer's forward with x . W_x + b fused into the persistent loop
-    (ocrk_lstm_fwd_persistent_x, In = 256, H = 512) against the projection GEMM +
-    persistent loop, and both against the float oracle; ragged lengths. The
-    fused form skips gx's bf16 rounding, so the two differ by a few bf16 ulps."""
-    from cnn_lstm_ctc_ocr_amd import kernels as K
-    T, n_in, H = 23, 256, 512
-    rng = np.random.default_rng(31 + B)
-    bf = lambda a: torch.from_numpy(a.astype(np.float32)).bfloat16().float().numpy()   # noqa: E731
-    x = bf(rng.standard_normal((T, B, n_in)))
-    ks = [bf(rng.standard_normal((n_in + H, 4 * H)) * 0.1) for _ in range(2)]
-    bs = [(rng.standard_normal(4 * H) * 0.2).astype(np.float32) for _ in range(2)]
-    seq = rng.integers(1, T + 1, B).astype(np.int32)
-    seq[:3] = [T, 1, T - 1]
-    outs, _ = zip(*[G.lstm_dir_fwd(x, seq, ks[d], bs[d], d == 1) for d in range(2)])
-    ref = np.concatenate(outs, axis=2)
-    wxT = torch.from_numpy(np.ascontiguousarray(np.concatenate([k[:n_in].T for k in ks], 0))).to(cuda).bfloat16()
-    whT = torch.from_numpy(np.ascontiguousarray(np.stack([k[n_in:].T for k in ks]))).to(cuda).bfloat16()
-    bias = torch.from_numpy(np.concatenate(bs)).to(cuda)
-    xd = torch.from_numpy(x).to(cuda).bfloat16().contiguous()
-    seq_d = torch.from_numpy(seq).to(cuda)
-    assert K.lstm_fused_x_ok(B, H, n_in, torch.bfloat16, force=True)
-    K.status_word(cuda).zero_()
-    gx = K.gemm(xd.view(T * B, n_in), wxT, trans_b=True, bias=bias, out_dtype=torch.bfloat16)
-    unf = K.lstm_fwd(gx, whT, seq_d, T, B, H, torch.bfloat16)
-    fus = K.lstm_fwd_fused_x(xd, wxT, bias, whT, seq_d, T, B, H)
-    torch.cuda.synchronize()
-    assert K.read_status(cuda) == 0
-    for a, b in zip(unf, fus):
-        assert (a.float() - b.float()).abs().max().item() < 6e-2 * max(1.0, a.float().abs().max().item())
-    out = fus[0].float().cpu().numpy()
-    assert np.linalg.norm(out - ref) / np.linalg.norm(ref) < 3e-2
-    assert np.all(out[seq[1]:, 1] == 0)
-    # the saved tensors the BPTT reads: activations of the unfused path within bf16 noise
-    np.testing.assert_allclose(fus[2].cpu().numpy(), unf[2].cpu().numpy(), atol=5e-2)
 
 
 @pytest.mark.parametrize("T,B,n_in", [(19, 64, 64), (23, 160, 256)])

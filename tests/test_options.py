@@ -25,11 +25,11 @@ def test_every_kernel_option_is_registered_and_documented():
 
 def test_set_and_override_restore():
     before = options.get("BN_BWD_BLOCKS")
-    with options.override(BN_BWD_BLOCKS=512, DX_FIRST=1):
+    with options.override(BN_BWD_BLOCKS=512, CONV_SIDE=0):
         assert options.get("BN_BWD_BLOCKS") == 512
-        assert options.get("DX_FIRST") == 1
+        assert options.get("CONV_SIDE") == 0
     assert options.get("BN_BWD_BLOCKS") == before
-    assert options.get("DX_FIRST") == 0
+    assert options.get("CONV_SIDE") == 1
     prev = options.set("GEMM_TN", 0)
     try:
         assert options.get("GEMM_TN") == 0

@@ -35,8 +35,7 @@ def test_default_caps_fill_one_round_at_the_bench_shapes():
 def test_per_layer_caps(ocrk_opts):
     from cnn_lstm_ctc_ocr_amd import options
     ocrk_opts("TN_ITEMS_L1", 128)
-    ocrk_opts("TN_ITEMS_LATE", 192)
-    assert model._tn_items(1) == 128 and model._tn_items(1, late=True) == 128
-    assert model._tn_items(2) == options.get("TN_ITEMS") and model._tn_items(2, late=True) == 192
+    assert model._tn_items(1) == 128
+    assert model._tn_items(2) == options.get("TN_ITEMS")
     s = model._splits(256, 2048, 32000, batch=2, items=model._tn_items(1))
     assert _items(256, 2048, s, 2) == 128
