@@ -58,6 +58,9 @@ SIGNATURES = {
     "ocrk_conv2_bwd_data_conv1_wgrad_workspace_size": [_i32, _i32, _i32],
     "ocrk_conv2_bwd_data_conv1_wgrad": [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _i32, _p, _sz, _i32,
                                         _p],
+    "ocrk_conv12_bwd_supported": [_i32, _i32, _i32, _i32],
+    "ocrk_conv12_bwd_workspace_size": [_i32, _i32, _i32],
+    "ocrk_conv12_bwd": [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p, _i32, _p, _sz, _i32, _p],
     "ocrk_conv12_fwd_supported": [_i32, _i32, _i32, _i32],
     "ocrk_conv12_fwd": [_p, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p],
     "ocrk_conv1_fwd_relu_bits": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i32, _p],

@@ -343,6 +343,10 @@ bool nt_staged_enabled();
 int64_t conv_rows_dgrad_c1_parts(int B);
 int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
                        const void* relu_bits, const void* x, int x_is_u8, float* part, hipStream_t s);
+int64_t conv_rows_bwd_w2_parts(int B);
+int conv_rows_bwd_w2(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                     const void* relu_bits, const void* x, int x_is_u8, const float* w1, const float* b1,
+                     float* c1part, float* w2part, float* dw2, int accumulate, hipStream_t s);
 }
 
 // conv1 -> conv2 forward as one row walk (bf16 training): conv1's output rows are produced
@@ -425,6 +429,52 @@ extern "C" int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int
     if (st) return st;
     double* part2 = (double*)((char*)ws + ((size_t)nb * 10 * 32 * sizeof(float) + 15) / 16 * 16);
     return ocrk::slab_sum(part, (int)nb, 10 * 32, part2, nullptr, dw, db, 9 * 32, accumulate, s);
+}
+
+// conv1 -> conv2 backward as one row walk (bf16 training; the backward of ocrk_conv12_fwd,
+// src/weinman/model.py:84-123): conv2's data gradient (dy1 = relu'(y1) . conv2^T(dz2),
+// contracted into conv1's weight gradient as it is produced, as
+// ocrk_conv2_bwd_data_conv1_wgrad) AND conv2's weight gradient, whose input y1 =
+// relu(conv1(x)) is recomputed per row from the image (the bits ocrk_conv12_fwd produced)
+// instead of read -- so the forward need not write y1. dz2 [B,H,W,32] bf16, w_bwd conv2's
+// backward image, relu_mask / relu_bits as ocrk_conv2_bwd_data_conv1_wgrad, x [B,H+2,W+2]
+// u8 or bf16, w1 [3][3][1][32] / b1 [32] f32 conv1's variables; dw2 [3][3][32][32],
+// dw1 [3][3][1][32], db1 [32] f32 (+)= the sums.
+// workspace: conv1 partials | slab_sum's doubles | conv2 partials [max(2, B)][9216] f32
+static size_t conv12_bwd_c1_bytes(int B) {
+    return ((size_t)ocrk::conv_rows_bwd_w2_parts(std::max(B, 1)) * 10 * 32 * sizeof(float) + 15) / 16 * 16;
+}
+
+extern "C" int ocrk_conv12_bwd_supported(int B, int H, int W, int dtype) {
+    return dtype == OCRK_BF16 && ocrk::conv_rows_dgrad_c1_covers(B, H, W, 32, 32) ? 1 : 0;
+}
+
+extern "C" size_t ocrk_conv12_bwd_workspace_size(int B, int H, int W) {
+    (void)H; (void)W;
+    return conv12_bwd_c1_bytes(B) + (size_t)ocrk::SLAB_P * 10 * 32 * sizeof(double) +
+           (size_t)std::max<int64_t>(2, ocrk::conv_rows_bwd_w2_parts(std::max(B, 1))) * 9 * 32 * 32 * sizeof(float);
+}
+
+extern "C" int ocrk_conv12_bwd(const void* dz, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                               const void* relu_bits, const void* x, int x_is_u8, const float* w1, const float* b1,
+                               float* dw2, float* dw1, float* db1, int accumulate, void* ws, size_t ws_bytes,
+                               int dtype, void* stream) {
+    OCRK_REQUIRE(ocrk_conv12_bwd_supported(B, H, W, dtype), "ocrk_conv12_bwd: B=%d H=%d W=%d dtype=%d not covered",
+                 B, H, W, dtype);
+    OCRK_REQUIRE(dz && w_bwd && x && w1 && b1 && dw2 && dw1 && db1 && ws, "ocrk_conv12_bwd: null pointer");
+    OCRK_REQUIRE(!relu_mask != !relu_bits, "ocrk_conv12_bwd: give exactly one of relu_mask / relu_bits");
+    OCRK_REQUIRE(ws_bytes >= ocrk_conv12_bwd_workspace_size(B, H, W) && (uintptr_t)ws % 16 == 0,
+                 "ocrk_conv12_bwd: workspace too small or misaligned");
+    const int64_t nb = ocrk::conv_rows_bwd_w2_parts(B);
+    OCRK_REQUIRE(nb < (1ll << 31), "ocrk_conv12_bwd: too many rows");
+    hipStream_t s = ocrk::as_stream(stream);
+    float* c1part = (float*)ws;
+    double* c1sum = (double*)((char*)ws + conv12_bwd_c1_bytes(B));
+    float* w2part = (float*)((char*)c1sum + (size_t)ocrk::SLAB_P * 10 * 32 * sizeof(double));
+    int st = ocrk::conv_rows_bwd_w2(dz, B, H, W, w_bwd, relu_mask, relu_bits, x, x_is_u8, w1, b1, c1part, w2part, dw2,
+                                    accumulate, s);
+    if (st) return st;
+    return ocrk::slab_sum(c1part, (int)nb, 10 * 32, c1sum, nullptr, dw1, db1, 9 * 32, accumulate, s);
 }
 
 extern "C" int ocrk_conv3x3_fwd(const void* x, int B, int H, int W, int cin, const void* w_nk,

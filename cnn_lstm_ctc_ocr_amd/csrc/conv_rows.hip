@@ -97,58 +97,70 @@ __device__ __forceinline__ void c1_frags(C1Frags& f, const float* __restrict__ w
     f.b1 = b1;
 }
 
-// conv1's output row r (relu(b1 + 3x3 'valid' conv of image rows r .. r + 2, held
-// preprocessed in the 8-row f32 image ring `ximg`)) into a conv row ring slot ([pixel + 1]
-// [32 channels], rw_off layout; pixels past W untouched) on the MFMA: per 16-pixel tile
-// and 16-channel tile D[ch][px] = b1 + W1^T[ch][tap] . X[tap][px], K = 9 taps padded to 32,
-// hi + lo bf16 operands (3 products; XIN 2 = a bf16 image, exact in hi: 2). Wave w covers
-// pixels 64 w .. 64 w + 63. y1row / bitsrow (or NULL): the row's bf16 values and its
-// ReLU bit mask (u32 per pixel) to global memory. The same bits wherever it runs.
-template <int XIN>
+// conv1's output at one 16-pixel tile of row r (relu(b1 + 3x3 'valid' conv of image rows
+// r .. r + 2, held preprocessed in the XS-row f32 image ring `ximg`) on the MFMA: per
+// 16-channel tile D[ch][px] = b1 + W1^T[ch][tap] . X[tap][px], K = 9 taps padded to 32,
+// hi + lo bf16 operands (3 products; XIN 2 = a bf16 image, exact in hi: 2). The lane's
+// pixel is px (its i16); o[j] = the bf16 pairs of channels 16 j + 4 g .. + 3, mword |=
+// their ReLU bits (bit c = channel c). The same bits wherever it runs.
+typedef unsigned int c1_u32x2 __attribute__((ext_vector_type(2)));
+template <int XIN, int XS>
+__device__ __forceinline__ void c1_px16(const float* ximg, int r, int px, int g, const C1Frags& f, c1_u32x2 (&o)[2],
+                                        unsigned& mword) {
+    float xv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int t = 8 * g + e;
+        const int kh = t / 3, kw = t - 3 * (t / 3);
+        xv[e] = t < 9 ? ximg[((r + kh) & (XS - 1)) * RD_XROW + px + kw] : 0.f;
+    }
+    u32x4 bh, bl;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned hh, ll;
+        split2_bf16(xv[2 * p], xv[2 * p + 1], hh, ll);
+        bh[p] = hh;
+        bl[p] = ll;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        floatx4 d = *reinterpret_cast<const floatx4*>(f.b1 + 16 * j + 4 * g);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
+                                                    __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wl[j]),
+                                                    __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
+        if constexpr (XIN == 1)
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
+                                                        __builtin_bit_cast(bf16x8, bl), d, 0, 0, 0);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[e] = fmaxf(d[e], 0.f);
+            mword |= (v[e] > 0.f ? 1u : 0u) << (16 * j + 4 * g + e);
+        }
+        o[j][0] = pack_bf16x2(v[0], v[1]);
+        o[j][1] = pack_bf16x2(v[2], v[3]);
+    }
+}
+
+// conv1's output row r into a conv row ring slot ([pixel + 1][32 channels], rw_off
+// layout; pixels past W untouched). Wave w covers pixels 64 w .. 64 w + 63. y1row /
+// bitsrow (or NULL): the row's bf16 values and its ReLU bit mask (u32 per pixel) to
+// global memory.
+template <int XIN, int XS = C12_XSLOTS>
 __device__ __forceinline__ void c1_make_row(char* slot, const float* ximg, int r, int W, int wave, int i16, int g,
                                             const C1Frags& f, bf16* y1row, unsigned* bitsrow) {
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const int px = 64 * wave + 16 * n + i16;
-        float xv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int t = 8 * g + e;
-            const int kh = t / 3, kw = t - 3 * (t / 3);
-            xv[e] = t < 9 ? ximg[((r + kh) & (C12_XSLOTS - 1)) * RD_XROW + px + kw] : 0.f;
-        }
-        u32x4 bh, bl;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            unsigned hh, ll;
-            split2_bf16(xv[2 * p], xv[2 * p + 1], hh, ll);
-            bh[p] = hh;
-            bl[p] = ll;
-        }
+        c1_u32x2 o[2];
         unsigned mword = 0;
+        c1_px16<XIN, XS>(ximg, r, px, g, f, o, mword);
+        if (px < W) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            floatx4 d = *reinterpret_cast<const floatx4*>(f.b1 + 16 * j + 4 * g);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
-                                                        __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wl[j]),
-                                                        __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
-            if constexpr (XIN == 1)
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.wh[j]),
-                                                            __builtin_bit_cast(bf16x8, bl), d, 0, 0, 0);
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[e] = fmaxf(d[e], 0.f);
-                mword |= (v[e] > 0.f ? 1u : 0u) << (16 * j + 4 * g + e);
-            }
-            u32x2 o;
-            o[0] = pack_bf16x2(v[0], v[1]);
-            o[1] = pack_bf16x2(v[2], v[3]);
-            if (px < W) {
-                *reinterpret_cast<u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o;
-                if (y1row) *reinterpret_cast<u32x2*>(y1row + (size_t)px * RW_CI + 16 * j + 4 * g) = o;
+            for (int j = 0; j < 2; ++j) {
+                *reinterpret_cast<c1_u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o[j];
+                if (y1row) *reinterpret_cast<c1_u32x2*>(y1row + (size_t)px * RW_CI + 16 * j + 4 * g) = o[j];
             }
         }
         if (bitsrow) {
@@ -614,6 +626,316 @@ conv3x3_dgrad_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
     }
 }
 
+// conv1 -> conv2's whole backward as one row walk, two wave roles per CU: waves 0-3 run
+// conv2's backward-data with conv1's weight gradient contracted in (the loop of
+// conv3x3_dgrad_rows_kernel<XIN, BITS>, unchanged), waves 4-7 conv2's weight gradient
+//   dW[kh][kw][ci][co] += sum_w y1[h][w][ci] . dz[h+1-kh][w+1-kw][co]
+// on the same dz ring rows (h-1 .. h+1 at step h), y1's row h recomputed from the image ring
+// (c1_px16: the bits ocrk_conv12_fwd produced, so the forward writes no y1), 32 pixels at a
+// time through the wave's own 2 KB tile (A = y1^T by frag_tr, B = the ring rows shifted by
+// 1 - kw; the wgrad row kernel's 9 x 2 x 2 accumulator tiles). Wave q of each role sits on
+// SIMD q: a dgrad wave and a wgrad wave share each MFMA pipe, and neither role's registers
+// (resident weights + data-gradient tiles; 144 accumulator registers) are live in the
+// other's loop, so two waves of <= 256 registers fit a SIMD. The roles meet at one barrier
+// per row: the dgrad waves load the ring rows and image rows for both, into slots neither
+// reads in that step. One band per image (one workgroup per CU, 86.6 KB of ring + tiles, the
+// end's wave partials 149 KB). Partials: c1part [B][10][32] as the dgrad kernel's,
+// w2part [B][9][32][32] (the four wgrad waves summed in wave order).
+constexpr int C12B_TILES = RD_LDS + RD_XRING;                           // 4 dy1 tiles (2 KB), then 4 y1 tiles (4 KB)
+constexpr int C12B_LDS_WALK = C12B_TILES + 12 * RD_TSLOT;               // 94.6 KB
+constexpr int C12B_C1RED = 4 * RW_PART * 4;                             // the wgrad partials end here
+constexpr int C12B_LDS = C12B_C1RED + 4 * RD_C1_PART * 4;               // 149 KB
+static_assert(C12B_LDS >= C12B_LDS_WALK, "end partials overlay the walk's LDS");
+
+template <int XIN, bool BITS>
+__global__ void __launch_bounds__(512, 1)
+conv12_bwd_rows_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wb, const bf16* __restrict__ mask,
+                       int B, int H, int W, const void* __restrict__ xin, const float* __restrict__ w1,
+                       const float* __restrict__ b1, float* __restrict__ c1part, float* __restrict__ w2part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = wave & 3;                                  // SIMD / pixel quarter
+    const bool wgrad_role = wave >= 4;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int b = blockIdx.x;
+    const int kr0 = 4 * g + (i16 >> 2), mq = 4 * (i16 & 3);   // frag_tr lane geometry
+    const int XW = W + 2;
+    float* xring = reinterpret_cast<float*>(smem + RD_LDS);
+
+    for (int i = tid; i < C12B_LDS_WALK / 16; i += 512) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+
+    if (!wgrad_role) {
+        // ---- waves 0-3: conv2's backward-data + conv1's weight gradient (tid 0 .. 255)
+        char* tile = smem + C12B_TILES + q * RD_TSLOT;
+        unsigned xraw = 0;
+        auto x_fetch = [&](int r) {
+            const size_t o = ((size_t)b * (H + 2) + r) * XW + min(tid, XW - 1);
+            if constexpr (XIN == 1) xraw = reinterpret_cast<const uint8_t*>(xin)[o];
+            else xraw = reinterpret_cast<const unsigned short*>(xin)[o];
+        };
+        auto x_put = [&](int r) {
+            if (tid < XW) xring[(r & 3) * RD_XROW + tid] = XIN == 1 ? conv1_pre_u8(xraw) : __uint_as_float(xraw << 16);
+        };
+        floatx4 c1acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+        const int tap = min(i16, 8), tkh = tap / 3, tkw = tap - 3 * tkh;
+        bf16x8 wa[9][2];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                wa[t][i] = *reinterpret_cast<const bf16x8*>(wb + ((size_t)(16 * i + i16) * 9 + t) * RW_CO + 8 * g);
+        constexpr int PER = 4;
+        const int qmax = W * 4 - 1;
+        u32x4 sd[2][PER];
+        const bf16* dyb = dy + (size_t)b * H * W * RW_CO;
+        auto drow = [&](int r) { return dyb + (size_t)r * W * RW_CO; };
+        auto load_row = [&](const bf16* base, u32x4 (&v)[PER]) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int qq = min(tid + 256 * i, qmax);
+                v[i] = *reinterpret_cast<const u32x4*>(base + (size_t)qq * 8);
+            }
+        };
+        auto store_row = [&](int row, const u32x4 (&v)[PER]) {
+            char* slot = smem + (row & 3) * RW_XSLOT;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int qq = tid + 256 * i;
+                if (qq < W * 4) *reinterpret_cast<u32x4*>(slot + rw_off((qq >> 2) + 1, qq & 3)) = v[i];
+            }
+        };
+        auto zero_row = [&](int row) {
+            char* slot = smem + (row & 3) * RW_XSLOT;
+            for (int i = tid; i < RW_XSLOT / 16; i += 256) reinterpret_cast<u32x4*>(slot)[i] = u32x4{0u, 0u, 0u, 0u};
+        };
+        // prologue: dy rows -1, 0, 1 (zero rows past the image), x rows 0 .. 2, dy row 2 into set 0
+        for (int r = -1; r <= 1; ++r) {
+            if (r < 0 || r >= H) {
+                zero_row(r);
+            } else {
+                load_row(drow(r), sd[1]);
+                store_row(r, sd[1]);
+            }
+        }
+        for (int r = 0; r <= 2; ++r) {
+            x_fetch(r);
+            x_put(r);
+        }
+        load_row(drow(min(2, H - 1)), sd[0]);
+
+        auto step = [&](int h, auto P_) {
+            constexpr int P = decltype(P_)::value;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            load_row(drow(min(h + 3, H - 1)), sd[1 - P]);
+            x_fetch(min(h + 3, H + 1));
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 mk[4][2];
+            unsigned mb[4];
+            if constexpr (BITS) {
+                const unsigned* mrow = reinterpret_cast<const unsigned*>(mask) + ((size_t)b * H + h) * W;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) mb[n] = mrow[min(64 * q + 16 * n + i16, W - 1)];
+            } else {
+                const bf16* mrow = mask + ((size_t)b * H + h) * W * RW_CI;
+#pragma unroll
+                for (int n = 0; n < 4; ++n)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int px = min(64 * q + 16 * n + i16, W - 1);
+                        mk[n][i] = *reinterpret_cast<const u32x2*>(mrow + (size_t)px * RW_CI + 16 * i + 4 * g);
+                    }
+            }
+            floatx4 acc[4][2];
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[n][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const char* slot = smem + ((h + 1 - kh) & 3) * RW_XSLOT;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+                    for (int n = 0; n < 4; ++n) {
+                        const int r = 64 * q + 16 * n + i16 + 2 - kw;
+                        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + rw_off(r, g));
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            acc[n][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kh * 3 + kw][i], bf, acc[n][i], 0, 0, 0);
+                    }
+                }
+            }
+            auto dx_bits = [&](int n, int i) {
+                u32x2 o;
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2) {
+                    bool k0, k1;
+                    if constexpr (BITS) {
+                        const unsigned sh = mb[n] >> (16 * i + 4 * g + 2 * e2);
+                        k0 = sh & 1u;
+                        k1 = sh & 2u;
+                    } else {
+                        const unsigned m = mk[n][i][e2];
+                        k0 = __uint_as_float(m << 16) > 0.f;
+                        k1 = __uint_as_float(m & 0xffff0000u) > 0.f;
+                    }
+                    o[e2] = pack_bf16x2(k0 ? acc[n][i][2 * e2] : 0.f, k1 ? acc[n][i][2 * e2 + 1] : 0.f);
+                }
+                return o;
+            };
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+                for (int nn = 0; nn < 2; ++nn) {
+                    const int n = 2 * kb + nn;
+                    const bool in = 64 * q + 16 * n + i16 < W;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        u32x2 o = dx_bits(n, i);
+                        if (!in) o = u32x2{0u, 0u};
+                        *reinterpret_cast<u32x2*>(tile + rw_off(16 * nn + i16, 2 * i + (g >> 1)) + (g & 1) * 8) = o;
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bf16x8 bfr[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c = 16 * j + mq;
+                    bfr[j] = frag_tr(reinterpret_cast<const unsigned short*>(tile + rw_off(kr0, c >> 3) + (c & 7) * 2),
+                                     16 * RW_CO);
+                }
+                const float* xs = xring + ((h + tkh) & 3) * RD_XROW + 64 * q + 32 * kb + 4 * g + tkw;
+                u32x4 ah, al;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int qq = (p & 1) * 2 + (p >> 1) * 16;
+                    unsigned hi2, lo2;
+                    split2_bf16(xs[qq], xs[qq + 1], hi2, lo2);
+                    ah[p] = i16 < 9 ? hi2 : (i16 == 9 ? 0x3f803f80u : 0u);
+                    al[p] = i16 < 9 ? lo2 : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c1acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), bfr[j], c1acc[j],
+                                                                       0, 0, 0);
+                if constexpr (XIN == 1) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        c1acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), bfr[j],
+                                                                           c1acc[j], 0, 0, 0);
+                }
+            }
+            // dy row h+2 into the slot of row h-2 (or zeros past the image); x row h+3 into
+            // the slot of row h-1 (the wgrad waves read rows h-1 .. h+1 / h .. h+2 this step)
+            if (h + 2 < H) store_row(h + 2, sd[P]);
+            else if (h + 2 == H) zero_row(h + 2);
+            if (h + 3 < H + 2) x_put(h + 3);
+        };
+        for (int h = 0; h < H; h += 2) {
+            step(h, std::integral_constant<int, 0>{});
+            if (h + 1 < H) step(h + 1, std::integral_constant<int, 1>{});
+        }
+        __syncthreads();                                     // the walk is over: LDS is free
+        float* red = reinterpret_cast<float*>(smem + C12B_C1RED);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * g + e < 10) red[q * RD_C1_PART + (4 * g + e) * RW_CI + 16 * j + i16] = c1acc[j][e];
+    } else {
+        // ---- waves 4-7: conv2's weight gradient over pixels 64 q .. 64 q + 63
+        char* tile = smem + C12B_TILES + (4 + 2 * q) * RD_TSLOT;      // 64 pixel rows
+        C1Frags f1;
+        c1_frags(f1, w1, b1, i16, g);
+        floatx4 wacc[9][2][2];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) wacc[t][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int h = 0; h < H; ++h) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            // y1's pixels 64 q .. 64 q + 63 of row h (zero past W) into the wave's tile (the
+            // previous row's reads of it are done: the barrier's lgkmcnt wait)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int px = 64 * q + 16 * n + i16;
+                c1_u32x2 o[2];
+                unsigned mword = 0;
+                c1_px16<XIN, 4>(xring, h, px, g, f1, o, mword);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    *reinterpret_cast<c1_u32x2*>(tile + rw_off(16 * n + i16, 2 * i + (g >> 1)) + (g & 1) * 8) =
+                        px < W ? o[i] : c1_u32x2{0u, 0u};
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                bf16x8 ya[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int m = 16 * i + mq;
+                    ya[i] = frag_tr(reinterpret_cast<const unsigned short*>(tile + rw_off(32 * kb + kr0, m >> 3) + (m & 7) * 2),
+                                    16 * RW_CI);
+                }
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    const char* dsl = smem + ((h + 1 - kh) & 3) * RW_XSLOT;   // zero rows past the image
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const int rd = 64 * q + 32 * kb + kr0 + 2 - kw;
+                        bf16x8 zb[2];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int n = 16 * j + mq;
+                            zb[j] = frag_tr(reinterpret_cast<const unsigned short*>(dsl + rw_off(rd, n >> 3) + (n & 7) * 2),
+                                            16 * RW_CO);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                wacc[kh * 3 + kw][i][j] =
+                                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(ya[i], zb[j], wacc[kh * 3 + kw][i][j], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();                                     // the walk is over: LDS is free
+        float* red = reinterpret_cast<float*>(smem) + q * RW_PART;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        red[(t * RW_CI + 16 * i + 4 * g + e) * RW_CO + 16 * j + i16] = wacc[t][i][j][e];
+    }
+    __syncthreads();
+    // both roles' partials, the waves added in wave order
+    const float* c1r = reinterpret_cast<const float*>(smem + C12B_C1RED);
+    for (int o = tid; o < RD_C1_PART; o += 512)
+        c1part[(size_t)b * RD_C1_PART + o] = ((c1r[o] + c1r[RD_C1_PART + o]) + c1r[2 * RD_C1_PART + o]) +
+                                             c1r[3 * RD_C1_PART + o];
+    const float* r0 = reinterpret_cast<const float*>(smem);
+    float* out = w2part + (size_t)b * RW_PART;
+    for (int o = tid * 4; o < RW_PART; o += 512 * 4) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(r0 + o);
+#pragma unroll
+        for (int qq = 1; qq < 4; ++qq) v += *reinterpret_cast<const f32x4*>(r0 + qq * RW_PART + o);
+        *reinterpret_cast<f32x4*>(out + o) = v;
+    }
+}
+
 // Forward of conv2 by rows: z[h][w][co] = bias[co] + sum_{kh,kw,ci}
 // x[h+kh-1][w+kw-1][ci] . Wn[co][kh][kw][ci] (w_nk image), optional ReLU, and
 // the BatchNorm partial statistics of each OUTPUT ROW (tile = one image row of
@@ -1026,22 +1348,9 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
     for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) bco[j][e] = bias ? bias[16 * j + 4 * g + e] : 0.f;
-    // conv1's A fragments (hi, lo): channel tile j, lane row = channel 16 j + i16, k = taps 8 g .. 8 g + 7
-    u32x4 w1h[2], w1l[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int t0 = 8 * g + 2 * p, t1 = t0 + 1;
-            const float v0 = t0 < 9 ? w1[t0 * RW_CO + 16 * j + i16] : 0.f;
-            const float v1 = t1 < 9 ? w1[t1 * RW_CO + 16 * j + i16] : 0.f;
-            unsigned hh, ll;
-            split2_bf16(v0, v1, hh, ll);
-            w1h[j][p] = hh;
-            w1l[j][p] = ll;
-        }
-    }
-
+    // conv1's A fragments (hi, lo) and bias (c1_frags: the layout every conv1 producer uses)
+    C1Frags f1;
+    c1_frags(f1, w1, b1, i16, g);
     const int XW = W + 2;
     unsigned xraw = 0;
     auto x_fetch = [&](int r) {                      // this thread's pixel of image row r (clamped)
@@ -1065,45 +1374,15 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const int px = 64 * wave + 16 * n + i16;
-            // B: X[tap][px] for taps 8 g .. 8 g + 7 (taps >= 9: zero)
-            float xv[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int t = 8 * g + e;
-                const int kh = t / 3, kw = t - 3 * (t / 3);
-                xv[e] = t < 9 ? ximg[((r + kh) & (C12_XSLOTS - 1)) * RD_XROW + px + kw] : 0.f;
-            }
-            u32x4 bh, bl;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                unsigned hh, ll;
-                split2_bf16(xv[2 * p], xv[2 * p + 1], hh, ll);
-                bh[p] = hh;
-                bl[p] = ll;
-            }
+            c1_u32x2 o[2];
             unsigned mword = 0;
+            c1_px16<XIN, C12_XSLOTS>(ximg, r, px, g, f1, o, mword);
+            if (px < W) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                floatx4 d = *reinterpret_cast<const floatx4*>(b1 + 16 * j + 4 * g);   // at use: fewer live registers
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1h[j]),
-                                                            __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1l[j]),
-                                                            __builtin_bit_cast(bf16x8, bh), d, 0, 0, 0);
-                if constexpr (XIN == 1)                  // a bf16 image is exact in hi
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w1h[j]),
-                                                                __builtin_bit_cast(bf16x8, bl), d, 0, 0, 0);
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    v[e] = fmaxf(d[e], 0.f);
-                    mword |= (v[e] > 0.f ? 1u : 0u) << (16 * j + 4 * g + e);
-                }
-                u32x2 o;
-                o[0] = pack_bf16x2(v[0], v[1]);
-                o[1] = pack_bf16x2(v[2], v[3]);
-                if (px < W) {
-                    *reinterpret_cast<u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o;
-                    if (WY1 && own) *reinterpret_cast<u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o;
+                for (int j = 0; j < 2; ++j) {
+                    *reinterpret_cast<c1_u32x2*>(slot + rw_off(px + 1, 2 * j + (g >> 1)) + (g & 1) * 8) = o[j];
+                    if (WY1 && own)
+                        *reinterpret_cast<c1_u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o[j];
                 }
             }
             mword |= __shfl_xor(mword, 16, 64);
@@ -1647,8 +1926,16 @@ static bool rows_wgrad_blocks() { return opt(OPT_CONV_WGRAD_BLOCKS) != 0; }
 // OCRK_CONV_WGRAD_BLOCKS=2: conv7 / conv8 as channel blocks too (else the ping-pong TN engine)
 static bool rows_wgrad_blocks_wide() { return opt(OPT_CONV_WGRAD_BLOCKS) == 2; }
 
+// (at least two partials: splitk_finish sums two or more, a single one is paired with zeros)
 size_t conv_rows_wgrad_ws_bytes(int B, int cin, int cout) {
-    return (size_t)std::min(B, std::max(cu_count(), 1)) * 9 * cin * cout * sizeof(float);
+    return (size_t)std::max(2, std::min(B, std::max(cu_count(), 1))) * 9 * cin * cout * sizeof(float);
+}
+
+// one partial slab: the reduce that turns partials into dw needs two, so the second is zero
+static int single_partial_pad(GemmParams& p, float* ws, size_t slab_floats, hipStream_t s) {
+    if (p.splits > 1) return OCRK_OK;
+    p.splits = 2;
+    return hipMemsetAsync(ws + slab_floats, 0, slab_floats * sizeof(float), s) == hipSuccess ? OCRK_OK : OCRK_ERR_HIP;
 }
 
 // OCRK_CONV_ROWS_WIDE=0: the wider layers (conv3-conv6) stay on the GEMM / direct engines
@@ -1815,6 +2102,40 @@ int conv_rows_dgrad_c1(const void* dy, int B, int H, int W, const void* w_bwd, c
     return launch_status("conv3x3_dgrad_rows_c1");
 }
 
+int64_t conv_rows_bwd_w2_parts(int B) { return (int64_t)B; }
+
+// conv2's whole backward with conv1's weight gradient as one row walk
+// (conv12_bwd_rows_kernel): c1part [B][10 * 32] as conv_rows_dgrad_c1, and conv2's weight
+// gradient dw2 [3][3][32][32] (+)= the sum of w2part [B][9216] in a fixed order (splitk_finish)
+template <int XIN, bool BITS>
+static void launch_bwd_w2(const void* dy, int B, int H, int W, const void* w_bwd, const void* mask, const void* x,
+                          const float* w1, const float* b1, float* c1part, float* w2part, hipStream_t s) {
+    static DeviceOnce cfg;
+    set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv12_bwd_rows_kernel<XIN, BITS>), C12B_LDS);
+    conv12_bwd_rows_kernel<XIN, BITS><<<B, 512, C12B_LDS, s>>>((const bf16*)dy, (const bf16*)w_bwd, (const bf16*)mask,
+                                                               B, H, W, x, w1, b1, c1part, w2part);
+}
+
+int conv_rows_bwd_w2(const void* dy, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                     const void* relu_bits, const void* x, int x_is_u8, const float* w1, const float* b1,
+                     float* c1part, float* w2part, float* dw2, int accumulate, hipStream_t s) {
+    if (relu_bits) {
+        if (x_is_u8) launch_bwd_w2<1, true>(dy, B, H, W, w_bwd, relu_bits, x, w1, b1, c1part, w2part, s);
+        else launch_bwd_w2<2, true>(dy, B, H, W, w_bwd, relu_bits, x, w1, b1, c1part, w2part, s);
+    } else {
+        if (x_is_u8) launch_bwd_w2<1, false>(dy, B, H, W, w_bwd, relu_mask, x, w1, b1, c1part, w2part, s);
+        else launch_bwd_w2<2, false>(dy, B, H, W, w_bwd, relu_mask, x, w1, b1, c1part, w2part, s);
+    }
+    int st = launch_status("conv12_bwd_rows");
+    if (st) return st;
+    GemmParams p = {};
+    p.M = 9 * RW_CI; p.N = RW_CO; p.K = B * H * W; p.batch = 1;
+    p.C = dw2; p.ldc = RW_CO; p.c_bf16 = 0; p.accumulate = accumulate; p.alpha = 1.f;
+    p.splits = (int)conv_rows_bwd_w2_parts(B); p.splitk_ws = w2part;
+    st = single_partial_pad(p, w2part, RW_PART, s);
+    return st ? st : splitk_finish(p, s);
+}
+
 // an XCT -> DCT layer as (XCT / CI) x (DCT / CO) channel blocks of CI x CO
 template <int CI, int KPX, int CO = 64>
 static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, int xct, int dct, float* dw,
@@ -1828,7 +2149,9 @@ static int launch_rows_co(const void* x, const void* dy, int B, int H, int W, in
     // (OCRK_CONV_WGRAD_CUS overrides; 0 = every CU)
     const int cap = (int)opt(OPT_CONV_WGRAD_CUS);
     const int cus = (nb > 1 && cap > 0) ? std::min(cap, cu_count()) : cu_count();
-    const int grid = std::max(1, std::min(B, std::max(cus, 1) / nb));
+    // (at least two: the split-K reduce sums two or more partials; a workgroup past the
+    // batch writes zeros)
+    const int grid = std::max(2, std::min(B, std::max(cus, 1) / nb));
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_co_kernel<CI, KPX, CO>), C::LDS);
     conv3x3_wgrad_rows_co_kernel<CI, KPX, CO><<<dim3(grid, nb), C::NT, C::LDS, s>>>(
@@ -1865,7 +2188,7 @@ int conv_rows_wgrad(const void* x, const void* dy, int B, int H, int W, int cin,
     if (cout == 256 && W <= 128 && (cin == 128 || cin == 256) && rows_wgrad_blocks_wide())
         return launch_rows_co<64, 128>(x, dy, B, H, W, cin, 256, dw, accumulate, ws, s);
     if (cin != RW_CI || cout != RW_CO || W > RW_MAXW) return -1;
-    const int grid = std::min(B, std::max(cu_count(), 1));
+    const int grid = std::max(2, std::min(B, std::max(cu_count(), 1)));   // (>= 2: as launch_rows_co)
     static DeviceOnce cfg;
     set_dyn_lds(cfg, reinterpret_cast<const void*>(&conv3x3_wgrad_rows_kernel<0>), RW_LDS);
     conv3x3_wgrad_rows_kernel<0><<<grid, 256, RW_LDS, s>>>((const bf16*)x, (const bf16*)dy, (float*)ws, B, H, W);

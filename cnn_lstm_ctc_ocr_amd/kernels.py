@@ -153,6 +153,32 @@ def conv2_bwd_data_conv1_wgrad(dz, w_bwd, relu_mask, x, dw, db, accumulate=True,
          _stream(dz))
 
 
+def conv12_bwd_ok(x, dtype):
+    """The fused conv1 -> conv2 backward (ocrk_conv12_bwd) covers this image batch x
+    [B, IH, IW] (u8, or bf16 in a bf16 model): dz [B, IH-2, IW-2, 32]."""
+    B, IH, IW = x.shape[:3]
+    return (x.dim() == 3 and dtype == torch.bfloat16 and x.dtype in (torch.uint8, torch.bfloat16)
+            and IH >= 3 and IW >= 3 and bool(_lib.lib().ocrk_conv12_bwd_supported(B, IH - 2, IW - 2, BF16)))
+
+
+def conv12_bwd(dz, w_bwd, x, w1, b1, dw2, dw1, db1, relu_mask=None, relu_bits=None, accumulate=True):
+    """conv2's data and weight gradients and conv1's weight / bias gradients as one row
+    walk (ocrk_conv12_bwd): dw2 (+)= conv2's weight gradient with y1 = relu(conv1(x))
+    recomputed from the image, dw1 / db1 (+)= conv1's through conv2's backward-data and
+    conv1's ReLU (relu_mask = y1, or relu_bits = its bit mask u8 [B, H, W, 4])."""
+    _chk(dz, w_bwd, relu_mask, relu_bits, x, w1, b1, dw2, dw1, db1)
+    if (relu_mask is None) == (relu_bits is None):
+        raise ValueError("give exactly one of relu_mask / relu_bits")
+    B, H, W, _ = dz.shape
+    if relu_bits is not None and (relu_bits.dtype != torch.uint8 or tuple(relu_bits.shape) != (B, H, W, 4)):
+        raise ValueError("relu_bits must be uint8 [B, H, W, 4]")
+    nb = _lib.lib().ocrk_conv12_bwd_workspace_size(B, H, W)
+    ws = _ws(nb, dz.device)
+    call("ocrk_conv12_bwd", ptr(dz), B, H, W, ptr(w_bwd), ptr(relu_mask), ptr(relu_bits), ptr(x),
+         int(x.dtype == torch.uint8), ptr(w1), ptr(b1), ptr(dw2), ptr(dw1), ptr(db1), int(accumulate), ptr(ws), nb,
+         BF16, _stream(dz))
+
+
 def conv_stats_tiles(M):
     return _lib.lib().ocrk_conv_stats_tiles(M)
 

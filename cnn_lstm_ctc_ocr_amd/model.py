@@ -96,15 +96,18 @@ class _ConvBlock(torch.autograd.Function):
         # block may end between the forward and the backward)
         ctx.c1_fused = bool(k == 1 and not ctx.exact and options.get("CONV1_FUSED"))
         ctx.pooled_bn = bool(options.get("POOLED_BN"))
+        ctx.conv12_bwd = False
         zs = None
         if (k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED")
                 and options.get("CONV12_FUSED") and K.conv12_fwd_ok(x, dt)):
             # conv1 -> conv2 in one row walk: conv1's rows produced into conv2's ring (never
-            # re-read from HBM), y1 and its ReLU bit mask written for the backward
+            # re-read from HBM) and their ReLU bit mask written for the backward; y1 only when
+            # the backward does not recompute it (ocrk_conv12_bwd)
+            ctx.conv12_bwd = bool(options.get("CONV12_BWD") and K.conv12_bwd_ok(x, dt))
             w_nk2, _ = store.conv_images(even, dt)
             y_odd, bits, z12, st12 = K.conv12_fwd(x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], w_nk2,
-                                                  P[pe + "/bias"])
-            ctx.relu_bits = bits if K.conv2_bwd_data_conv1_wgrad_ok(z12, x) else None
+                                                  P[pe + "/bias"], want_y1=not ctx.conv12_bwd)
+            ctx.relu_bits = bits if ctx.conv12_bwd or K.conv2_bwd_data_conv1_wgrad_ok(z12, x) else None
             zs = (z12, st12)
         elif k == 1 and training and dt == torch.bfloat16 and not ctx.exact and options.get("CONV1_FUSED"):
             # the ReLU's bit mask for the fused conv2 backward-data + conv1 weight gradient
@@ -192,6 +195,17 @@ class _ConvBlock(torch.autograd.Function):
                 _conv_late_run(store)
                 _conv_wgrad(ctx.exact, y_odd, dz, G[pe + "/kernel"])
         _, w_bwd = store.conv_images(even, dt)
+        if ctx.conv12_bwd:
+            # the step's tail as ONE row walk: conv2's data gradient contracted into conv1's
+            # weight gradient, and conv2's weight gradient on y1 recomputed from the image
+            # (the forward wrote no y1); the queued conv3 weight gradient on the side stream
+            if store.conv_late:
+                with _conv_side(store, *_conv_late_tensors(store)):
+                    _conv_late_run(store)
+            K.conv12_bwd(dz, w_bwd, x, P["convnet/conv1/kernel"], P["convnet/conv1/bias"], G[pe + "/kernel"],
+                         G[po + "/kernel"], G[po + "/bias"], relu_bits=ctx.relu_bits)
+            store.join()                                   # side-stream weight gradients are in
+            return (None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
         if ctx.c1_fused and K.conv2_bwd_data_conv1_wgrad_ok(dz, x):
             # the step's tail: conv2's weight gradient (y1, dz) on the side stream beside one
             # pass that is conv2's backward-data and conv1's weight gradient (dy1 is

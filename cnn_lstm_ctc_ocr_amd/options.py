@@ -29,6 +29,7 @@ _HOST_DEFAULTS = {
     "RELU_BITS": 1,           # 0: conv3/5/7's ReLU masks for conv4/6/8's backward-data as their bf16 outputs
     "POOLED_BN": 1,           # 0: the BN backward's dgamma / dbeta pass walks z instead of the pooled output
     "CONV1_FUSED": 1,         # 0: conv2's backward-data stores dy1, conv1's weight gradient re-reads it
+    "CONV12_BWD": 1,          # 0: conv2's weight gradient as its own launch on y1 (written by the forward)
     # tuning (workgroup caps of the recurrent weight-gradient launches)
     "TN_ITEMS": 256,          # layer 2
     "TN_ITEMS_L1": 160,       # layer 1 (beside the conv backward)

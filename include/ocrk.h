@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCRK_ABI_VERSION 6
+#define OCRK_ABI_VERSION 7   /* 7: ocrk_conv12_bwd (+ _supported, _workspace_size) */
 
 enum ocrk_status {
     OCRK_OK = 0,
@@ -196,6 +196,21 @@ size_t ocrk_conv2_bwd_data_conv1_wgrad_workspace_size(int B, int H, int W);
 int ocrk_conv2_bwd_data_conv1_wgrad(const void* dz, int B, int H, int W, const void* w_bwd, const void* relu_mask,
                                     const void* relu_bits, const void* x, int x_is_u8, float* dw, float* db,
                                     int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
+
+/* conv1 -> conv2 backward as one row walk (round 6; the backward of ocrk_conv12_fwd,
+ * src/weinman/model.py:84-123 -- TF's conv2d backprop-input / backprop-filter of conv2 and
+ * backprop-filter of conv1): conv2's data gradient contracted into conv1's weight gradient
+ * as above, plus conv2's weight gradient, its input y1 = relu(conv1(x)) recomputed per row
+ * from the image (the bits ocrk_conv12_fwd made), so the forward may pass y1 = NULL.
+ * dz [B,H,W,32] bf16; w_bwd conv2's backward image; relu_mask [B,H,W,32] bf16 or relu_bits
+ * [B,H,W] u32 (exactly one); x [B,H+2,W+2] u8 (x_is_u8) or bf16; w1 [3][3][1][32] / b1 [32]
+ * f32; dw2 [3][3][32][32], dw1 [3][3][1][32], db1 [32] f32 (+)= the batch sums (fixed-order
+ * reductions: deterministic). */
+int ocrk_conv12_bwd_supported(int B, int H, int W, int dtype);
+size_t ocrk_conv12_bwd_workspace_size(int B, int H, int W);
+int ocrk_conv12_bwd(const void* dz, int B, int H, int W, const void* w_bwd, const void* relu_mask,
+                    const void* relu_bits, const void* x, int x_is_u8, const float* w1, const float* b1, float* dw2,
+                    float* dw1, float* db1, int accumulate, void* ws, size_t ws_bytes, int dtype, void* stream);
 
 /* a2 conv2..conv8 -- conv_layer (model.py:84-109) with 'same' padding as an
  * implicit GEMM on MFMA. x [B,H,W,cin]; w_nk [cout][3][3][cin] (dtype);

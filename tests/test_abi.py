@@ -41,7 +41,7 @@ def test_library_exports_every_symbol():
     lib = _lib.lib()
     for name in _declarations():
         assert hasattr(lib, name), name
-    assert lib.ocrk_version() == 6
+    assert lib.ocrk_version() == 7
 
 
 def test_no_compute_without_device_pointers():

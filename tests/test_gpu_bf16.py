@@ -151,7 +151,7 @@ def test_conv12_fused_forward(cuda, B, IH, IW, x_u8):
     torch.cuda.synchronize()
     assert torch.equal(z, z2)
     assert torch.equal(stats, st2)
-    # without y1 (CONV12_RECOMPUTE): the same bits, z and partials
+    # without y1 (the fused backward, ocrk_conv12_bwd, recomputes it): the same bits, z and partials
     none, bits3, z3, st3 = Kn.conv12_fwd(xd, w1d, b1d, w_nk, b2d, want_y1=False)
     torch.cuda.synchronize()
     assert none is None
@@ -241,6 +241,80 @@ def test_conv2_bwd_data_fused_conv1_wgrad(cuda, B, IH, IW, x_u8, mask):
     assert _rel(db.cpu().numpy() - prev_b, db2.cpu().numpy()) < 2e-5
     np.testing.assert_allclose(dw.cpu().numpy() - prev_w, dw2.cpu().numpy(), rtol=1e-3,
                                atol=1e-5 * float(np.abs(dw_ref).max()))
+
+
+@pytest.mark.parametrize("B,IH,IW", [(4, 32, 256), (3, 17, 130), (2, 3, 9), (5, 32, 70), (1, 32, 256)])
+@pytest.mark.parametrize("x_u8", [True, False])
+@pytest.mark.parametrize("mask", ["bf16", "bits"])
+def test_conv12_bwd_fused(cuda, B, IH, IW, x_u8, mask):
+    """conv1 -> conv2's whole backward as one row walk (ocrk_conv12_bwd, the bench's k = 1
+    backward): conv2's weight gradient with y1 recomputed from the image against the
+    float64 sum over the forward's y1 (ocrk_conv12_fwd) and against the separate weight
+    gradient kernel on that y1 (summation order only); conv1's weight / bias gradients as
+    ocrk_conv2_bwd_data_conv1_wgrad's. Shapes: the bench crop, odd heights, one conv1 output
+    row, a narrow row, B = 1 (a single partial)."""
+    from cnn_lstm_ctc_ocr_amd import kernels as Kn
+    rng = np.random.default_rng(IH * 1000 + IW + x_u8 + 17 * B)
+    H, W = IH - 2, IW - 2
+    img = rng.integers(0, 256, (B, IH, IW)).astype(np.uint8)
+    xf = _bf(rng.standard_normal((B, IH, IW)))
+    xd = torch.from_numpy(img).to(cuda) if x_u8 else torch.from_numpy(xf).to(cuda).bfloat16()
+    w1 = rng.standard_normal((3, 3, 1, 32)).astype(np.float32)
+    b1 = (rng.standard_normal(32) * 0.3).astype(np.float32)
+    w2 = _bf(rng.standard_normal((3, 3, 32, 32)) / np.sqrt(288))
+    w1d, b1d = torch.from_numpy(w1).to(cuda), torch.from_numpy(b1).to(cuda)
+    w_nk = Kn.permute3(torch.from_numpy(w2).to(cuda), 9 * 32, 32, 1, torch.bfloat16).view(32, 9 * 32)
+    w_bwd = Kn.permute3(torch.from_numpy(w2).to(cuda), 9, 32, 32, torch.bfloat16).view(32, 9 * 32)
+    y1d, bits, _, _ = Kn.conv12_fwd(xd, w1d, b1d, w_nk, torch.zeros(32, device=cuda))
+    dz = _bf(rng.standard_normal((B, H, W, 32)))
+    dzd = torch.from_numpy(dz).to(cuda).bfloat16()
+    assert Kn.conv12_bwd_ok(xd, torch.bfloat16)
+    prev = [rng.standard_normal(s).astype(np.float32) for s in ((3, 3, 32, 32), (3, 3, 1, 32), (32,))]
+    dw2, dw1, db1 = (torch.from_numpy(p).to(cuda) for p in prev)
+    if mask == "bits":
+        Kn.conv12_bwd(dzd, w_bwd, xd, w1d, b1d, dw2, dw1, db1, relu_bits=bits)
+    else:
+        Kn.conv12_bwd(dzd, w_bwd, xd, w1d, b1d, dw2, dw1, db1, relu_mask=y1d)
+    got2, got1, gotb = (t.cpu().numpy() - p for t, p in zip((dw2, dw1, db1), prev))
+    y1 = y1d.float().cpu().numpy().astype(np.float64)
+    _, dw2_ref, _ = G.conv2d_bwd(y1, w2.astype(np.float64), dz.astype(np.float64), "same", need_dx=False)
+    assert _rel(got2, dw2_ref) < 1e-5
+    # the separate weight-gradient kernel on the forward's y1: the same products, another order
+    sep = torch.zeros(3, 3, 32, 32, device=cuda)
+    Kn.conv3x3_bwd_weight(y1d, dzd, sep, accumulate=False)
+    assert _rel(got2, sep.cpu().numpy()) < 1e-5
+    # conv1's gradients: the two-output walk's (one band per image) against the data-gradient
+    # walk's (two bands per image) -- the same dy1 bits, another partial grouping
+    c1w, c1b = torch.zeros(3, 3, 1, 32, device=cuda), torch.zeros(32, device=cuda)
+    if mask == "bits":
+        Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, None, xd, c1w, c1b, accumulate=False, relu_bits=bits)
+    else:
+        Kn.conv2_bwd_data_conv1_wgrad(dzd, w_bwd, y1d, xd, c1w, c1b, accumulate=False)
+    assert _rel(got1, c1w.cpu().numpy()) < 2e-5
+    assert _rel(gotb, c1b.cpu().numpy()) < 2e-5
+
+
+def test_conv12_bwd_route_in_the_train_step(cuda):
+    """The step's k = 1 backward as one walk (CONV12_BWD=1, the default; the forward writes
+    no y1) against the two-launch route (conv2's weight gradient on the forward's y1,
+    CONV12_BWD=0), bench width, B = 32: every gradient but conv1's and conv2's kernel /
+    bias bit-identical, those to the summation order (2e-5)."""
+    import bench
+    from cnn_lstm_ctc_ocr_amd import ModelConfig, ParamStore, options
+    from cnn_lstm_ctc_ocr_amd.train import Trainer
+    img, width, lab = bench.synthetic_batch(np.random.default_rng(3), 32, 256, 125, cuda)
+    out = []
+    for route in (0, 1):
+        store = ParamStore(ModelConfig(cell="lstm", rnn_sizes=(512, 512), dtype=torch.bfloat16), device=cuda, seed=11)
+        with options.override(CONV12_BWD=route):
+            Trainer(store).loss_and_grads(img, width, lab)
+        torch.cuda.synchronize()
+        out.append({k: v.cpu().numpy().copy() for k, v in store.grads.items()})
+    for k in out[0]:
+        if k.startswith("convnet/conv1/") or k == "convnet/conv2/kernel":
+            assert _rel(out[1][k], out[0][k]) < 2e-5, k
+        else:
+            np.testing.assert_array_equal(out[1][k], out[0][k], err_msg=k)
 
 
 @pytest.mark.parametrize("M_,N,K,tag", [(8000, 4096, 256, "proj L1"), (8000, 4096, 1024, "proj L2"),
@@ -451,7 +525,7 @@ def test_bf16_recurrent_weight_gradients_bench_launches(cuda, cell, layer, items
     f32 gradient (accumulate) -- against float64."""
     from cnn_lstm_ctc_ocr_amd import kernels as Kn
     from cnn_lstm_ctc_ocr_amd.model import _splits, _tn_items
-    cap_x = items or _tn_items(layer, late=(cell == "lstm"))
+    cap_x = items or _tn_items(layer)
     cap_h = items or _tn_items(layer)
     R = 32000
     H = 512 if (cell == "lstm" or layer == 1) else 256
