@@ -47,9 +47,19 @@ constexpr int RW_PART = 9 * RW_CI * RW_CO;         // floats per partial
 constexpr int RW_LDS = 4 * RW_PART * 4 > RW_RING ? 4 * RW_PART * 4 : RW_RING;   // 144 KB (end: wave partials)
 constexpr int RW_MAXW = 254;
 
-// LDS byte offset of 16-B chunk c of image row r (4 chunks per row, XOR-swizzled
-// by (r >> 2) & 3 as the TN engine's 64-B rows, so a transposed read's 16 k-rows spread)
-__device__ __forceinline__ int rw_off(int r, int c) { return r * RW_ROWB + ((c ^ ((r >> 2) & 3)) << 4); }
+// The XOR swizzle of a 4-chunk (64-B) row r: v = (r >> 2) & 3 with its two bits swapped
+// (0, 2, 1, 3). Any 16 consecutive rows then have distinct (r mod 4, swizzle) pairs (a
+// ds_read_b128 of one chunk per row, 16 lanes a clock: no bank conflict), and rows r and r + 4
+// use the other chunk PAIR (a ds_read_b64_tr_b16 of a chunk pair over 8 rows, 32 lanes a
+// clock: with v itself rows r and r + 4 hit the same pair -- 2-way conflicts, 0.41-0.45 of
+// the row kernels' LDS cycles; profiles/r6_conv12_bwd.txt)
+__device__ __forceinline__ int swz4(int r) {
+    const int v = (r >> 2) & 3;
+    return ((v & 1) << 1) | (v >> 1);
+}
+
+// LDS byte offset of 16-B chunk c of image row r (4 chunks per row, swz4-swizzled)
+__device__ __forceinline__ int rw_off(int r, int c) { return r * RW_ROWB + ((c ^ swz4(r)) << 4); }
 
 // two fp32 values -> one word of two RNE bf16 (a single v_cvt_pk_bf16_f32; the
 // per-value casts + shift / or took three VALU instructions per pair)
@@ -1146,12 +1156,10 @@ conv3x3_fwd_rows_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wn,
 // 15 x 127): the same ring walk, but wave q owns output channels 16q .. 16q+15
 // over the WHOLE row (K = KPX pixels, KPX/32 k-steps), so no cross-wave sum:
 // acc [9 taps][CI/16 tiles] (18 / 36 f32x4). x rows are CI*2 bytes, dy rows 128 B,
-// 16-B chunks XOR-swizzled per row as in the TN engine (rows of >= 8 chunks by
-// r mod 8, of 4 chunks by (r >> 2) mod 4).
+// 16-B chunks XOR-swizzled per row (rows of >= 8 chunks by r mod 8, of 4 chunks by swz4).
 template <int CPR>
 __device__ __forceinline__ int rc_off(int r, int c) {
-    constexpr int SWM = CPR >= 8 ? 7 : 3;
-    const int sw = CPR >= 8 ? (r & SWM) : ((r >> 2) & SWM);
+    const int sw = CPR >= 8 ? (r & 7) : swz4(r);
     return r * CPR * 16 + ((c ^ sw) << 4);
 }
 
