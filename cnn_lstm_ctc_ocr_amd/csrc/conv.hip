@@ -355,8 +355,8 @@ int conv_rows_bwd_w2(const void* dy, int B, int H, int W, const void* w_bwd, con
 // [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32]; outputs y1 [B,IH-2,IW-2,32]
 // bf16 (conv1's ReLU output), relu_bits u8 [B,IH-2,IW-2][4] (its bit mask), z (conv2's
 // pre-BN output, same shape) and stats [B*(IH-2)][2][32] (conv2's per-row BN partials,
-// ocrk_bn_finalize_tiles with tile_rows = IW-2). y1 may be NULL: not written (the tools
-// build's ocrk_conv2_bwd_weight_c1x recomputes it).
+// ocrk_bn_finalize_tiles with tile_rows = IW-2). y1 may be NULL: not written
+// (ocrk_conv12_bwd recomputes it).
 extern "C" int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype) {
     return dtype == OCRK_BF16 && IH >= 3 && IW >= 3 && ocrk::conv12_fwd_covers(B, IH - 2, IW - 2) ? 1 : 0;
 }

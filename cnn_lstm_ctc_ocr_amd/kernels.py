@@ -90,7 +90,7 @@ def conv12_fwd_ok(x, dtype):
 def conv12_fwd(x, w1, b1, w_nk2, b2, want_y1=True):
     """conv1 (fused preprocess, ReLU) -> conv2 (no activation) with conv2's per-row BN
     partials (ocrk_conv12_fwd). Returns y1 [B,IH-2,IW-2,32] bf16 (None unless want_y1:
-    the backward recomputes it, conv2_bwd_weight_c1x), its ReLU bit mask u8 [.., 4],
+    the backward recomputes it, conv12_bwd), its ReLU bit mask u8 [.., 4],
     z [B,IH-2,IW-2,32] bf16, stats [B*(IH-2), 2, 32]."""
     _chk(x, w1, b1, w_nk2, b2)
     B, IH, IW = x.shape[:3]

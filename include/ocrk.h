@@ -170,7 +170,8 @@ int ocrk_conv1_fwd_relu_bits(const void* x, int x_is_u8, int B, int H, int W, co
  * the MFMA with hi + lo bf16 operands) instead of being written and re-read by conv2. Replaces
  * ocrk_conv1_fwd_relu_bits + ocrk_conv3x3_fwd_rowstats of the first block. x [B,IH,IW] u8
  * (x_is_u8) or bf16; w1 f32 [3][3][1][32], b1 [32]; w_nk2 bf16 [32][3][3][32], b2 [32];
- * y1, z bf16 [B,IH-2,IW-2,32] (y1 may be NULL: not written); relu_bits u8 [B,IH-2,IW-2][4];
+ * y1, z bf16 [B,IH-2,IW-2,32] (y1 may be NULL: not written -- ocrk_conv12_bwd recomputes it);
+ * relu_bits u8 [B,IH-2,IW-2][4];
  * stats [B*(IH-2)][2][32] (tile_rows = IW-2). */
 int ocrk_conv12_fwd_supported(int B, int IH, int IW, int dtype);
 int ocrk_conv12_fwd(const void* x, int x_is_u8, int B, int IH, int IW, const float* w1, const float* b1,
