@@ -26,10 +26,16 @@ by the session (conftest.trained_fp32 / trained_bf16). Then:
   (800 crops, widths 37-330): logits <= 1e-4 relative L2, greedy and beam-16
   decodes compared on EVERY row; a row may differ only where the float64 graph
   has a near-tie, and such rows stay <= 2 %;
-* bf16 and fp32 runs agree step for step before the plateau (50-step window
-  means within 5 % over the first 1,000 steps) and both end with shard CER
-  <= 0.2 (the trajectories separate once the models leave the plateau: a
-  different rounding of one update changes which crops are learned first).
+* bf16 and fp32 runs agree step for step on the plateau (50-step window means
+  within 1 % over the first 500 steps, within 10 % up to step 1,000) and both
+  end with shard CER <= 0.2 (the trajectories separate once the models leave
+  the plateau: a different rounding of one update changes which crops are
+  learned first). The 1,000-step window bound was 5 % until round 6: the same
+  bf16 step with only conv1's / conv2's gradient summation order changed
+  (ocrk_conv12_bwd vs the two-launch route, gradients within 2e-5) moved the
+  worst window before step 1,000 from 2.2 % to 6.1 % (steps 950-1,000; every
+  window of the first 500 steps stays under 0.2 % in both), so that
+  window measures the chaos of the trajectory, not the kernels.
 
 $OCRK_TRAINED_OUT, when set, receives the curves, CERs and parity counts as JSON.
 The serving configurations at these weights: tests/test_gpu_trained_serving.py.
@@ -103,9 +109,11 @@ def test_bf16_trains_like_fp32_on_reference_shard(trained_fp32, trained_bf16):
     w16 = l16.reshape(-1, WINDOW).mean(1)
     rel = np.abs(w16 - w32) / w32
     early = rel[:EARLY // WINDOW]
+    first = rel[:500 // WINDOW]
     TM.report(bf16_loss=[round(v, 4) for v in l16.tolist()], bf16_window_mean=w16.tolist(),
               window_rel_diff=rel.tolist(), bf16_cer=c16)
     print(f"early windows max rel {early.max():.4f}; CER fp32 {c32[-1][1]:.4f} bf16 {c16[-1][1]:.4f}")
     assert np.isfinite(l16).all()
-    assert early.max() < 0.05, early
+    assert first.max() < 0.01, first
+    assert early.max() < 0.10, early
     assert c32[-1][1] <= CER_BAR and c16[-1][1] <= CER_BAR, (c32, c16)

@@ -15,7 +15,7 @@ import os
 import re
 from collections import defaultdict
 
-FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, false)*>|"
+FWD = re.compile(r"conv3x3_direct_kernel<\d+, \d+, \d+, false|gemm_nt_kernel<(\d+, ){5}2, [48](, (false|true))*>|"
                  r"conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel|conv12_fwd_rows_kernel")
 B = 256
 LAYERS = [("conv2", 30, 254, 32, 32), ("conv3", 15, 127, 32, 64), ("conv4", 15, 127, 64, 64),

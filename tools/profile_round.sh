@@ -16,7 +16,7 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-for
     > "$out/fetch.log" 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- "${pmc[@]}" \
     > "$out/write.log" 2>&1 || exit $?
-python3 tools/pmc_traffic.py --fetch "$out/fetch" --write "$out/write" --match "conv3x3_direct_kernel<[0-9]+, [0-9]+, [0-9]+, false|gemm_nt_kernel<([0-9]+, ){5}2, [48](, false)*>|conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel|conv12_fwd_rows_kernel" \
+python3 tools/pmc_traffic.py --fetch "$out/fetch" --write "$out/write" --match "conv3x3_direct_kernel<[0-9]+, [0-9]+, [0-9]+, false|gemm_nt_kernel<([0-9]+, ){5}2, [48](, (false|true))*>|conv3x3_fwd_rows_kernel|conv3x3_fwd_rows_co_kernel|conv12_fwd_rows_kernel" \
     --desc "conv1-conv8 forward launches (conv12_fwd_rows_kernel conv1 -> conv2, conv3x3_fwd_rows_co_kernel conv3-conv5, gemm_nt_kernel<..., A_IM2COL, NW> conv6-conv8)" \
     --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- ${pmc[*]}" --out "$out/pmc_conv.json" || exit $?
 find "$out/trace" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
