@@ -80,10 +80,12 @@ def main():
         fl = 2.0 * M * 9 * cin * cout
         alg = (M * cin + M * cout + 9 * cin * cout) * 2
         if name == "conv2" and "conv12" in names.get(name, ""):
-            # conv1 -> conv2 in one launch: the u8 image in; y1 (bf16), its ReLU bit mask
-            # (4 B per pixel) and z (bf16) out; both layers' weights
+            # conv1 -> conv2 in one launch: the u8 image in; y1 (bf16; not written by the
+            # <XIN, false> form, whose backward recomputes it), its ReLU bit mask (4 B per
+            # pixel) and z (bf16) out; both layers' weights
             fl = 2.0 * M * 9 * (1 * 32 + cin * cout)
-            alg = B * (H + 2) * (W + 2) + M * (2 * cin + 4 + 2 * cout) + 9 * 32 * 4 + 9 * cin * cout * 2
+            y1 = 0 if names[name].endswith("false>") else 2 * cin
+            alg = B * (H + 2) * (W + 2) + M * (y1 + 4 + 2 * cout) + 9 * 32 * 4 + 9 * cin * cout * 2
             name_shown = "conv1+2 1->32->32"
         else:
             name_shown = f"{name} {cin}->{cout}"
