@@ -117,13 +117,18 @@ typedef unsigned int c1_u32x2 __attribute__((ext_vector_type(2)));
 template <int XIN, int XS>
 __device__ __forceinline__ void c1_px16(const float* ximg, int r, int px, int g, const C1Frags& f, c1_u32x2 (&o)[2],
                                         unsigned& mword) {
+    // B operand, k = tap t = 8 g + e (K padded to 32): lane group g = 0 holds taps 0-7
+    // (kh = e / 3, kw = e % 3, compile-time), g = 1 tap 8 in slot 0, the rest zero -- so all
+    // lanes gather the nine taps from three wave-uniform row bases and select (no per-lane
+    // tap division: ~50 VALU fewer per 16-pixel tile, the same values)
+    const float* x0 = ximg + (r & (XS - 1)) * RD_XROW + px;
+    const float* x1 = ximg + ((r + 1) & (XS - 1)) * RD_XROW + px;
+    const float* x2 = ximg + ((r + 2) & (XS - 1)) * RD_XROW + px;
+    const float tp[9] = {x0[0], x0[1], x0[2], x1[0], x1[1], x1[2], x2[0], x2[1], x2[2]};
     float xv[8];
+    xv[0] = g == 0 ? tp[0] : (g == 1 ? tp[8] : 0.f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int t = 8 * g + e;
-        const int kh = t / 3, kw = t - 3 * (t / 3);
-        xv[e] = t < 9 ? ximg[((r + kh) & (XS - 1)) * RD_XROW + px + kw] : 0.f;
-    }
+    for (int e = 1; e < 8; ++e) xv[e] = g == 0 ? tp[e] : 0.f;
     u32x4 bh, bl;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
