@@ -185,6 +185,27 @@ __device__ __forceinline__ void vm_wait() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
 }
 
+// A lane's value combined with its partner lane l ^ 16 / l ^ 32 without the LDS crossbar
+// (__shfl_xor is a ds_bpermute): gfx950's v_permlane16_swap / v_permlane32_swap with both
+// operands v return, per lane, v of the lane and of its partner (in either order; + and | are
+// commutative, so the bits equal the shuffle forms').
+__device__ __forceinline__ unsigned or_xor16(unsigned v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return r[0] | r[1];
+}
+__device__ __forceinline__ unsigned or_xor32(unsigned v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return r[0] | r[1];
+}
+__device__ __forceinline__ float add_xor16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // 64-lane wave reductions.
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

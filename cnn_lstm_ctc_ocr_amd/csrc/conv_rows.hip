@@ -179,8 +179,7 @@ __device__ __forceinline__ void c1_make_row(char* slot, const float* ximg, int r
             }
         }
         if (bitsrow) {
-            mword |= __shfl_xor(mword, 16, 64);
-            mword |= __shfl_xor(mword, 32, 64);
+            mword = or_xor32(or_xor16(mword));
             if (g == 0 && px < W) bitsrow[px] = mword;
         }
     }
@@ -1398,8 +1397,7 @@ conv12_fwd_rows_kernel(const void* __restrict__ img, const float* __restrict__ w
                         *reinterpret_cast<c1_u32x2*>(y1 + (((size_t)b * H + r) * W + px) * RW_CI + 16 * j + 4 * g) = o[j];
                 }
             }
-            mword |= __shfl_xor(mword, 16, 64);
-            mword |= __shfl_xor(mword, 32, 64);
+            mword = or_xor32(or_xor16(mword));
             if (own && g == 0 && px < W) bits[((size_t)b * H + r) * W + px] = mword;
         }
     };
@@ -1664,8 +1662,7 @@ conv3x3_fwd_rows_co_kernel(const bf16* __restrict__ x, const bf16* __restrict__ 
                         unsigned m = 0;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) m |= (acc[n][e] > 0.f ? 1u : 0u) << (4 * g + e);
-                        m |= __shfl_xor(m, 16, 64);
-                        m |= __shfl_xor(m, 32, 64);
+                        m = or_xor32(or_xor16(m));
                         if (g == 0 && px < W) bits[((size_t)b * H + h) * W * (CO / 16) + (size_t)px * (CO / 16) + wave] =
                             (uint16_t)m;
                     }

@@ -348,8 +348,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 if (row_base + i * 16 + r < p.M) s += acc[i][j][r];
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
+        s = add_xor32(add_xor16(s));
         tsum[j] = s;
     }
     if (lane < 16)
@@ -375,8 +374,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmParams p) {
                     float d = acc[i][j][r] - tmean[j];
                     s += d * d;
                 }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
+        s = add_xor32(add_xor16(s));
         if (lane < 16) s_red[wm][wn * WN + j * 16 + lane] = s;
     }
     __syncthreads();
