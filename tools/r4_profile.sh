@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: these runs used switches removed from the product in round 6 --
+#  SIDE_CU_MASK, FORK_EVENTS, PP_DEEP, ... -- their results are kept under profiles/.)
 # Round-4 profiling on the GPU box: kernel stats of the fp32 serving configs
 # (C2, C5) and kernel traces of the C3 step with and without the upper layer's
 # dW_x deferred behind the lower BPTT (OCRK_DEFER_DWX; d2: also the lowest layer's data

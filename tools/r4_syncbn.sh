@@ -1,4 +1,6 @@
 set -o pipefail
+# (Historical: these runs used switches removed from the product in round 6 --
+#  SIDE_CU_MASK, FORK_EVENTS, PP_DEEP, ... -- their results are kept under profiles/.)
 mkdir -p gpurun_out/syncbn
 export TMPDIR=/tmp
 timeout -k 10 700 python3 -u -m pytest tests/test_gpu_syncbn.py tests/test_gpu_images.py tests/test_gpu_ops.py tests/test_gpu_dist.py tests/test_gpu_model.py -x -v --timeout 300 --timeout-method thread > gpurun_out/syncbn/tests.log 2>&1; rc=$?; tail -25 gpurun_out/syncbn/tests.log; [ $rc -eq 0 ] || exit $rc

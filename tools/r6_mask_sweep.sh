@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: these runs used switches removed from the product in round 6 --
+#  SIDE_CU_MASK, FORK_EVENTS, PP_DEEP, ... -- their results are kept under profiles/.)
 # The step on its own stream, CU-masked weight-gradient side stream: masks 0/96/128/160/192,
 # two passes; then kernel-trace timelines of mask 0 and 128.
 set -o pipefail

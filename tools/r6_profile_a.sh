@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: these runs used switches removed from the product in round 6 --
+#  SIDE_CU_MASK, FORK_EVENTS, PP_DEEP, ... -- their results are kept under profiles/.)
 # Round-6 counter passes (VERDICT r5 "next" #3, #4, #6), GPU box, repo root:
 #  1. SQ counters of every conv forward / backward-data kernel of the bench
 #     shape (tools/bench_conv.py): the NT engine on conv6-8 had none;

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: these runs used switches removed from the product in round 6 --
+#  SIDE_CU_MASK, FORK_EVENTS, PP_DEEP, ... -- their results are kept under profiles/.)
 # A/B: the step on the NULL stream vs its own non-blocking stream, x the CU-masked
 # weight-gradient side stream (OCRK_SIDE_CU_MASK: 0 = off, 192, 224 of 256 CUs).
 # Two passes of every arm on one box. Prints ms_per_step per arm.
