@@ -21,6 +21,17 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# HIP hardware queues per process, read once when HIP initialises (so before the
+# torch import below): one process per GPU (world 1) spreads the step's streams
+# (main, weight-gradient side stream, status copy) over 2 hardware queues --
+# measured 4.799-4.813 vs 4.821-4.828 ms/step with HIP's default 4, 3 and 8 no
+# better (profiles/r6_queues_ab.txt). OCRK_HW_QUEUES picks another count (the GPU
+# boxes export GPU_MAX_HW_QUEUES=4, HIP's default, so that variable alone cannot
+# say whether a user chose it). Data-parallel ranks keep the environment's
+# setting: RCCL's streams beside the step's were not measured with fewer queues.
+if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("OCRK_HW_QUEUES", "2")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -378,7 +389,8 @@ def run_c2(args, world, rank, device):
                        "decode_output": "device [B, T] dense (-1 padded), read back after the timed steps",
                        "execution": "hipGraph replay per batch (infer.InferGraph)" if args.c2_mode == "graph"
                        else "eager launches",
-                       "image": f"32x{W}", "parallelism": f"dp{world}"},
+                       "image": f"32x{W}", "parallelism": f"dp{world}",
+                       "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default (4)")},
             "loss": round(float(loss.item()), 4)}, elapsed, world * B * args.steps
 
 
@@ -472,6 +484,7 @@ def run_c5(args, world, rank, device, n_crops=2048, beam=16):
             "data": f"synthetic: {n_crops} uint8 crops, true widths U{{65..512}}, server-style 32-px buckets",
             "config": {"workload": "C5: bucketed INFER + CTC beam search (beam 16), LSTM 512/512",
                        "buckets": len(buckets), "crops": n_crops, "beam_width": beam,
+                       "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default (4)"),
                        "parallelism": f"replicas x{world} (whole buckets per rank)",
                        "decode": "second stream, beside the next bucket's forward" if args.c5_pipeline
                        else "in line",
@@ -860,7 +873,8 @@ def main():
                    "collective": "one bucketed SUM all-reduce of the flat fp32 gradient per step "
                                  "(RCCL over xGMI, backend nccl)" + (" + SyncBN: 8 small all-reduces"
                                                                      if args.sync_bn else "")
-                                 if world > 1 else "none"},
+                                 if world > 1 else "none",
+                   "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default (4)")},
         "world_size_seen": dist.get_world_size() if world > 1 else 1,
         "roofline": {"bound": "mfma", "kernel": op_desc, "achieved": round(achieved, 2), "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
