@@ -21,17 +21,6 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# HIP hardware queues per process, read once when HIP initialises (so before the
-# torch import below): one process per GPU (world 1) spreads the step's streams
-# (main, weight-gradient side stream, status copy) over 2 hardware queues --
-# measured 4.799-4.813 vs 4.821-4.828 ms/step with HIP's default 4, 3 and 8 no
-# better (profiles/r6_queues_ab.txt). OCRK_HW_QUEUES picks another count (the GPU
-# boxes export GPU_MAX_HW_QUEUES=4, HIP's default, so that variable alone cannot
-# say whether a user chose it). Data-parallel ranks keep the environment's
-# setting: RCCL's streams beside the step's were not measured with fewer queues.
-if int(os.environ.get("WORLD_SIZE", "1")) == 1:
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("OCRK_HW_QUEUES", "2")
-
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -701,6 +690,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.selftest:
         return selftest(args, world, rank)
+    # HIP hardware queues per process, read once when HIP initialises (so here, before
+    # the first HIP call): one process per GPU (world 1) running eager launches spreads
+    # the step's streams (main, weight-gradient side stream, status copy) over 2
+    # hardware queues -- 4.799-4.813 vs 4.821-4.828 ms/step with HIP's default 4, 3 and
+    # 8 no better (profiles/r6_queues_ab.txt). OCRK_HW_QUEUES picks another count (the
+    # GPU boxes export GPU_MAX_HW_QUEUES=4, HIP's default, so that variable alone cannot
+    # say whether a user chose it). Kept at the environment's setting: hipGraph replays
+    # (--mode graph, C2's default graph mode) -- the multi-stream captured train step
+    # replay faults on the host with 2 queues (profiles/r6l_gpu_tests_segv.log) -- and
+    # data-parallel ranks, whose RCCL streams were not measured with fewer queues.
+    graphs = args.mode == "graph" or (args.config == "c2" and args.c2_mode == "graph") or \
+        (args.config == "c5" and args.c5_mode == "graph")
+    if world == 1 and not graphs:
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("OCRK_HW_QUEUES", "2")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:

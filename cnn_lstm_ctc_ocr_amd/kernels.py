@@ -850,28 +850,9 @@ def cu_limited_stream(device, n_cus):
     return st
 
 
-# While a GraphedStep captures, every fork / side-work event recorded into the
-# capture is kept here and then held by the graph for its lifetime, instead of
-# being destroyed mid-capture (hardening: one host segfault inside hipGraph
-# replay was seen in round 6, cause not established -- DESIGN.md section 6).
-_CAPTURE_EVENTS = None
-
-
-def retain_capture_event(ev):
-    """Keep `ev` alive with the graph being captured (no-op outside a capture)."""
-    if _CAPTURE_EVENTS is not None:
-        _CAPTURE_EVENTS.append(ev)
-
-
 def fork(waiter, signaller):
     """waiter.wait_stream(signaller): the step's cross-stream forks (torch events)."""
-    if _CAPTURE_EVENTS is None:
-        waiter.wait_stream(signaller)
-        return
-    ev = torch.cuda.Event()
-    ev.record(signaller)
-    waiter.wait_event(ev)
-    _CAPTURE_EVENTS.append(ev)
+    waiter.wait_stream(signaller)
 
 
 def wait_mark(waiter, mark):

@@ -339,7 +339,6 @@ class side_work:
             return False
         done = torch.cuda.Event()
         done.record(self.side)
-        K.retain_capture_event(done)
         self.ctx.__exit__(*exc)
         for t in self.tensors:
             t.record_stream(self.side)

@@ -465,12 +465,8 @@ class GraphedStep:
         if before_capture is not None:
             before_capture()         # e.g. drop timers recorded by the eager warm-up
         self.graph = torch.cuda.CUDAGraph()
-        self._capture_events = K._CAPTURE_EVENTS = []     # the capture's fork / join events live with the graph
-        try:
-            with torch.cuda.graph(self.graph, stream=self.stream):
-                self.loss = trainer.loss_and_grads(self.image, self.width, (self.labels, self.label_len))
-        finally:
-            K._CAPTURE_EVENTS = None
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.loss = trainer.loss_and_grads(self.image, self.width, (self.labels, self.label_len))
         torch.cuda.current_stream(dev).wait_stream(self.stream)
 
     def load(self, image=None, width=None, label=None):
